@@ -1,0 +1,114 @@
+"""ctypes binding of the C ABI in include/flearn_amd.h (libflearn_amd.so, built for gfx950).
+
+torch is imported first on purpose: torch ships its own ROCm runtime whose soname
+(libamdhip64.so.7) is the same as the system one, so loading torch first makes the dynamic
+linker bind libflearn_amd.so to the runtime torch already initialised — one HIP runtime per
+process, and device pointers from torch tensors are valid in our kernels.
+
+There is no fallback: if the library is missing or the process has no GPU, every entry point
+raises NativeUnavailable.
+"""
+from __future__ import annotations
+
+import ctypes
+import threading
+from pathlib import Path
+
+import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
+
+LIB_PATH = Path(__file__).resolve().parent / "lib" / "libflearn_amd.so"
+ABI_VERSION = 1
+
+FA_OK = 0
+MODE_W32_DIV64, MODE_W32_DIV32, MODE_W64 = 0, 1, 2
+OP_MEAN, OP_AVGM, OP_ADAGRAD, OP_YOGI, OP_ADAM = 0, 1, 2, 3, 4
+PREC_F32, PREC_F64 = 0, 1
+OP_BY_NAME = {"mean": OP_MEAN, "avgm": OP_AVGM, "adagrad": OP_ADAGRAD, "yogi": OP_YOGI, "adam": OP_ADAM}
+
+#: every symbol include/flearn_amd.h declares (checked by tests/test_cabi.py)
+EXPORTS = (
+    "fa_abi_version",
+    "fa_last_error",
+    "fa_reduce_f32",
+    "fa_reduce_f64",
+    "fa_reduce_i64",
+    "fa_opt_apply",
+    "fa_fill_uniform_f32",
+)
+
+
+class NativeUnavailable(RuntimeError):
+    """The HIP library or a GPU is missing: the aggregation path cannot run."""
+
+
+class NativeError(RuntimeError):
+    """A C-ABI call returned an error code."""
+
+
+class Epilogue(ctypes.Structure):
+    """struct fa_epilogue (include/flearn_amd.h)."""
+
+    _fields_ = [
+        ("op", ctypes.c_int32),
+        ("reserved", ctypes.c_int32),
+        ("prev", ctypes.c_void_p),
+        ("v", ctypes.c_void_p),
+        ("beta", ctypes.c_double),
+        ("eta", ctypes.c_double),
+        ("tau", ctypes.c_double),
+        ("beta2", ctypes.c_double),
+    ]
+
+
+_lock = threading.Lock()
+_lib = None
+
+
+def load(require_gpu: bool = False):
+    """Load and type the library (no GPU needed just to load).  Raises NativeUnavailable."""
+    global _lib
+    with _lock:
+        if _lib is None:
+            if not LIB_PATH.exists():
+                raise NativeUnavailable(
+                    f"{LIB_PATH} not built; run `python -c 'import __graft_entry__ as g; g.build()'`"
+                )
+            L = ctypes.CDLL(str(LIB_PATH))
+            P, I32, I64, D = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_double
+            sig = {
+                "fa_abi_version": ([], ctypes.c_int),
+                "fa_last_error": ([], ctypes.c_char_p),
+                "fa_reduce_f32": ([P, I64, I32, I32, P, D, I64, I64, ctypes.POINTER(Epilogue), P, P, P],
+                                  ctypes.c_int),
+                "fa_reduce_f64": ([P, I64, I32, P, D, I64, I64, P, P], ctypes.c_int),
+                "fa_reduce_i64": ([P, I64, I32, P, D, I64, I64, P, P], ctypes.c_int),
+                "fa_opt_apply": ([I32, ctypes.POINTER(Epilogue), P, P, I64, P, P, P], ctypes.c_int),
+                "fa_fill_uniform_f32": ([P, I64, I32, I64, ctypes.c_uint64, I64, I64, P], ctypes.c_int),
+            }
+            for name, (args, res) in sig.items():
+                fn = getattr(L, name)
+                fn.argtypes = args
+                fn.restype = res
+            v = L.fa_abi_version()
+            if v != ABI_VERSION:
+                raise NativeUnavailable(f"libflearn_amd ABI {v}, expected {ABI_VERSION}")
+            _lib = L
+    if require_gpu and not torch.cuda.is_available():
+        raise NativeUnavailable("no HIP device visible: the aggregation kernels need an MI355X")
+    return _lib
+
+
+def lib():
+    """The library, with a GPU required (the product path)."""
+    return load(require_gpu=True)
+
+
+def check(rc: int, what: str) -> None:
+    if rc != FA_OK:
+        msg = _lib.fa_last_error().decode(errors="replace") if _lib is not None else "?"
+        raise NativeError(f"{what} failed with code {rc}: {msg}")
+
+
+def stream_handle(device) -> int:
+    """hipStream_t of torch's current stream on `device` (what every launch is queued on)."""
+    return torch.cuda.current_stream(device).cuda_stream

@@ -1,0 +1,309 @@
+"""Device aggregation engine behind Strategy.server_ensemble.
+
+`Aggregator.ensemble(agg_weight_lst, w_local_lst, key_lst)` is the MI355X replacement for
+flearn/common/strategy/strategy.py:102-130: plan the buckets (bucket.py), copy the uploads into
+HBM, run ONE fused reduce launch per bucket kind on torch's current stream, and hand back a
+fresh dict with the reference's value types.
+
+`ServerOptimizer` keeps the previous global model and the optimizer state v_t resident in HBM
+and fuses the FedAVGM / FedOPT update (avgm.py:19-36, opt.py:23-65 — in the reference these run
+in client_receive with w_local = the client's weights; here w_local = the previous global model)
+into the same launch, so the server step reads every client byte once and touches the O(P)
+state once.
+
+Device-level entry points (`reduce_stack`, `apply_update`, `fill_uniform`) operate on torch CUDA
+tensors directly and are what bench.py and the multi-GPU path use.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _native as na
+from .bucket import BucketPlan, Packer, make_plan
+from .semantics import KIND_F32, KIND_F64, KIND_I64, Numerics
+
+_F64 = np.dtype(np.float64)
+
+
+def _ptr(t: torch.Tensor | None) -> int | None:
+    return None if t is None else t.data_ptr()
+
+
+def _check_cuda(t: torch.Tensor, name: str, dtype: torch.dtype, ndim: int | None = None):
+    if not isinstance(t, torch.Tensor) or t.device.type != "cuda":
+        raise TypeError(f"{name} must be a CUDA (HIP) tensor")
+    if t.dtype != dtype:
+        raise TypeError(f"{name} must be {dtype}, got {t.dtype}")
+    if ndim is not None and t.dim() != ndim:
+        raise ValueError(f"{name} must be {ndim}-D, got shape {tuple(t.shape)}")
+
+
+def _epilogue(op: int, prev, v, beta=0.9, eta=1e-1, tau=1e-9, beta2=0.99):
+    return na.Epilogue(op, 0, _ptr(prev), _ptr(v), beta, eta, tau, beta2)
+
+
+# ---------------------------------------------------------------------------------------------
+# device-level entry points
+# ---------------------------------------------------------------------------------------------
+
+
+def reduce_stack(
+    stack: torch.Tensor,
+    weights: torch.Tensor,
+    mode: int,
+    denom: float,
+    *,
+    col_begin: int = 0,
+    n_cols: int | None = None,
+    n_clients: int | None = None,
+    out32: torch.Tensor | None = None,
+    out64: torch.Tensor | None = None,
+    op: int = na.OP_MEAN,
+    prev: torch.Tensor | None = None,
+    v: torch.Tensor | None = None,
+    beta: float = 0.9,
+    eta: float = 1e-1,
+    tau: float = 1e-9,
+    beta2: float = 0.99,
+) -> None:
+    """Weighted mean of the fp32 client stack [N, stride] over columns [col_begin, +n_cols)
+    (+ fused update), queued on torch's current stream.  out32/out64/prev/v are indexed from
+    col_begin.  weights: fp32 for MODE_W32_*, f64 for MODE_W64 (device tensors)."""
+    L = na.lib()
+    _check_cuda(stack, "stack", torch.float32, 2)
+    if stack.stride(1) != 1:
+        raise ValueError("stack rows must be contiguous")
+    n = stack.shape[0] if n_clients is None else n_clients
+    if not 1 <= n <= stack.shape[0]:
+        raise ValueError("n_clients out of range")
+    stride = stack.stride(0)
+    ncols = stack.shape[1] - col_begin if n_cols is None else n_cols
+    if col_begin < 0 or ncols < 0 or col_begin + ncols > stack.shape[1]:
+        raise ValueError("column window out of range")
+    wdt = torch.float64 if mode == na.MODE_W64 else torch.float32
+    _check_cuda(weights, "weights", wdt)
+    if weights.numel() < n:
+        raise ValueError("fewer weights than clients")
+    for name, t, dt in (("out32", out32, torch.float32), ("out64", out64, torch.float64)):
+        if t is not None:
+            _check_cuda(t, name, dt)
+            if t.numel() < ncols or not t.is_contiguous():
+                raise ValueError(f"{name} too small or not contiguous")
+    epi = None
+    if op != na.OP_MEAN:
+        vdt = torch.float32 if mode == na.MODE_W32_DIV32 else torch.float64
+        _check_cuda(prev, "prev", torch.float32)
+        _check_cuda(v, "v", vdt)
+        if prev.numel() < ncols or v.numel() < ncols:
+            raise ValueError("prev / v too small")
+        epi = _epilogue(op, prev, v, beta, eta, tau, beta2)
+    rc = L.fa_reduce_f32(
+        stack.data_ptr(), stride, n, mode, weights.data_ptr(), float(denom), col_begin, ncols,
+        ctypes.byref(epi) if epi is not None else None, _ptr(out32), _ptr(out64),
+        na.stream_handle(stack.device),
+    )
+    na.check(rc, "fa_reduce_f32")
+
+
+def reduce_stack_f64(stack, weights, denom, out64, n_clients=None):
+    L = na.lib()
+    _check_cuda(stack, "stack", torch.float64, 2)
+    _check_cuda(weights, "weights", torch.float64)
+    _check_cuda(out64, "out64", torch.float64)
+    n = stack.shape[0] if n_clients is None else n_clients
+    rc = L.fa_reduce_f64(stack.data_ptr(), stack.stride(0), n, weights.data_ptr(), float(denom), 0,
+                         stack.shape[1], out64.data_ptr(), na.stream_handle(stack.device))
+    na.check(rc, "fa_reduce_f64")
+
+
+def reduce_stack_i64(stack, weights, denom, out64, n_clients=None):
+    L = na.lib()
+    _check_cuda(stack, "stack", torch.int64, 2)
+    _check_cuda(weights, "weights", torch.int64)
+    _check_cuda(out64, "out64", torch.float64)
+    n = stack.shape[0] if n_clients is None else n_clients
+    rc = L.fa_reduce_i64(stack.data_ptr(), stack.stride(0), n, weights.data_ptr(), float(denom), 0,
+                         stack.shape[1], out64.data_ptr(), na.stream_handle(stack.device))
+    na.check(rc, "fa_reduce_i64")
+
+
+def apply_update(op: int, local32, glob, v, *, out32=None, out64=None, beta=0.9, eta=1e-1, tau=1e-9,
+                 beta2=0.99) -> None:
+    """Standalone AVGM/OPT update (client_receive form): w = update(glob, local32, v)."""
+    L = na.lib()
+    prec = na.PREC_F64 if glob.dtype == torch.float64 else na.PREC_F32
+    _check_cuda(local32, "local", torch.float32)
+    _check_cuda(glob, "glob", torch.float64 if prec == na.PREC_F64 else torch.float32)
+    _check_cuda(v, "v", glob.dtype)
+    n = local32.numel()
+    if glob.numel() != n or v.numel() != n:
+        raise ValueError("local / glob / v sizes differ")
+    epi = _epilogue(op, local32, v, beta, eta, tau, beta2)
+    rc = L.fa_opt_apply(prec, ctypes.byref(epi), local32.data_ptr(), glob.data_ptr(), n, _ptr(out32),
+                        _ptr(out64), na.stream_handle(local32.device))
+    na.check(rc, "fa_opt_apply")
+
+
+def fill_uniform(dst: torch.Tensor, seed: int, row_begin: int = 0, col_begin: int = 0,
+                 n_cols: int | None = None) -> None:
+    """Synthetic client data on device: dst[r, c] = U(-1,1) hash of (seed, row_begin+r,
+    col_begin+c) for c < n_cols (default: all columns)."""
+    L = na.lib()
+    _check_cuda(dst, "dst", torch.float32)
+    d2 = dst if dst.dim() == 2 else dst.view(1, -1)
+    ncols = d2.shape[1] if n_cols is None else n_cols
+    for r0 in range(0, d2.shape[0], 65535):
+        rows = min(65535, d2.shape[0] - r0)
+        rc = L.fa_fill_uniform_f32(d2[r0].data_ptr(), d2.stride(0), rows, ncols, seed & (2**64 - 1),
+                                   row_begin + r0, col_begin, na.stream_handle(dst.device))
+        na.check(rc, "fa_fill_uniform_f32")
+
+
+# ---------------------------------------------------------------------------------------------
+# server-side optimizer state
+# ---------------------------------------------------------------------------------------------
+
+
+class ServerOptimizer:
+    """FedAVGM / FedOPT state for the fused server step.
+
+    op     : "avgm" | "adagrad" | "yogi" | "adam"
+    state  : prev (fp32 previous global, flattened like the f32 bucket) and v_t (f64, or fp32 when
+             the weights make the reference's w_glob float32), both resident in HBM.
+    First round without `init_global`: the update is skipped (the mean is returned), prev is set
+    to the fp32 mean and v_t to zeros — the reference has no previous global model either.
+    """
+
+    def __init__(self, op: str, beta=0.9, eta=1e-1, tau=1e-9, beta2=0.99):
+        if op not in ("avgm", "adagrad", "yogi", "adam"):
+            raise ValueError(f"unknown server optimizer {op!r}")
+        self.op = na.OP_BY_NAME[op]
+        self.name = op
+        self.beta, self.eta, self.tau, self.beta2 = beta, eta, tau, beta2
+        self.prev = None
+        self.v = None
+        self._sig = None
+        self._pending_init = None
+
+    def init_global(self, glob: dict):
+        """Set the previous global model (dict of arrays/tensors); v_t is reset to zeros."""
+        self._pending_init = {k: np.asarray(v.cpu() if isinstance(v, torch.Tensor) else v) for k, v in glob.items()}
+        self.prev = self.v = self._sig = None
+
+    @staticmethod
+    def _signature(plan: BucketPlan, numerics: Numerics):
+        g = plan.f32
+        return tuple((s.key, s.shape) for s in g.segments), numerics.out_dtype.str
+
+    def prepare(self, plan: BucketPlan, device) -> bool:
+        """Bind the state to this plan's f32 bucket.  Returns False when there is no previous
+        model yet (first round): the caller then runs a plain mean and calls `adopt`."""
+        g = plan.f32
+        sig = self._signature(plan, g.numerics)
+        vdt = torch.float32 if g.numerics.out_dtype == np.float32 else torch.float64
+        if self._pending_init is not None:
+            prev = torch.zeros(g.stride, dtype=torch.float32)
+            for s in g.segments:
+                prev[s.offset : s.offset + s.numel] = torch.from_numpy(
+                    np.asarray(self._pending_init[s.key], dtype=np.float32).reshape(-1).copy()
+                )
+            self.prev = prev.to(device)
+            self.v = torch.zeros(g.stride, dtype=vdt, device=device)
+            self._sig = sig
+            self._pending_init = None
+            return True
+        if self._sig is None:
+            return False
+        if sig != self._sig:
+            raise ValueError("model layout changed between rounds; call init_global() again")
+        return True
+
+    def adopt(self, plan: BucketPlan, mean32: torch.Tensor):
+        g = plan.f32
+        vdt = torch.float32 if g.numerics.out_dtype == np.float32 else torch.float64
+        self.prev = mean32.clone()
+        self.v = torch.zeros(g.stride, dtype=vdt, device=mean32.device)
+        self._sig = self._signature(plan, g.numerics)
+
+    def v_t(self, plan: BucketPlan) -> dict:
+        """The state as the reference exposes it (self.v_t dict of arrays)."""
+        host = self.v.cpu().numpy()
+        return {s.key: host[s.offset : s.offset + s.numel].reshape(s.shape).copy() for s in plan.f32.segments}
+
+
+# ---------------------------------------------------------------------------------------------
+# the engine behind Strategy.server_ensemble
+# ---------------------------------------------------------------------------------------------
+
+OUTPUTS = ("reference", "float32", "device")
+
+
+class Aggregator:
+    """output: "reference" — values with the reference's types and dtypes (float64 ndarrays, numpy
+    scalars for 0-d buffers, torch CPU tensors when the uploads were tensors);
+    "float32" — fp32 ndarrays for fp32 keys (the values load_state_dict ends up with);
+    "device" — fresh torch CUDA tensors, fp32 for fp32 keys (no D2H)."""
+
+    def __init__(self, device=None, output: str = "reference", workers: int = 8):
+        na.lib()  # fail loudly right away if the HIP path is unavailable
+        if output not in OUTPUTS:
+            raise ValueError(f"output must be one of {OUTPUTS}")
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.output = output
+        self.packer = Packer(self.device, workers)
+        self.last_plan: BucketPlan | None = None
+
+    def _weights(self, nm: Numerics) -> torch.Tensor:
+        return torch.from_numpy(nm.weights).to(self.device)
+
+    def ensemble(self, agg_weight_lst, w_local_lst, key_lst=None, server_opt: ServerOptimizer | None = None):
+        plan = make_plan(agg_weight_lst, w_local_lst, key_lst)
+        self.last_plan = plan
+        with torch.cuda.device(self.device):
+            stacks = self.packer.pack(plan, w_local_lst)
+            results = {}
+            for kind, g in plan.groups.items():
+                nm = g.numerics
+                w = self._weights(nm)
+                if kind == KIND_F32:
+                    results[kind] = self._reduce_f32(plan, g, stacks[kind], w, server_opt)
+                elif kind == KIND_F64:
+                    out = self.packer.device_bucket(("out64", kind), (g.stride,), torch.float64)
+                    reduce_stack_f64(stacks[kind], w, nm.denom, out)
+                    results[kind] = out
+                elif kind == KIND_I64:
+                    out = self.packer.device_bucket(("out64", kind), (g.stride,), torch.float64)
+                    reduce_stack_i64(stacks[kind], w, nm.denom, out)
+                    results[kind] = out
+            return self._finish(plan, results)
+
+    def _reduce_f32(self, plan, g, stack, w, server_opt):
+        nm = g.numerics
+        want64 = self.output == "reference" and nm.out_dtype == _F64
+        out64 = self.packer.device_bucket(("out64", KIND_F32), (g.stride,), torch.float64) if want64 else None
+        out32 = None if want64 else self.packer.device_bucket(("out32", KIND_F32), (g.stride,), torch.float32)
+        if server_opt is None:
+            reduce_stack(stack, w, nm.mode, nm.denom, out32=out32, out64=out64)
+            return out64 if want64 else out32
+        if not server_opt.prepare(plan, self.device):
+            mean32 = self.packer.device_bucket(("mean32", KIND_F32), (g.stride,), torch.float32)
+            reduce_stack(stack, w, nm.mode, nm.denom, out32=mean32, out64=out64)
+            server_opt.adopt(plan, mean32)
+            return out64 if want64 else mean32
+        # fused: prev is updated in place to fl32(w) — the model clients load next round
+        reduce_stack(stack, w, nm.mode, nm.denom, out32=server_opt.prev, out64=out64, op=server_opt.op,
+                     prev=server_opt.prev, v=server_opt.v, beta=server_opt.beta, eta=server_opt.eta,
+                     tau=server_opt.tau, beta2=server_opt.beta2)
+        return out64 if want64 else server_opt.prev
+
+    def _finish(self, plan: BucketPlan, results: dict):
+        if self.output == "device":
+            glob = {}
+            for k in plan.keys:
+                s = plan.key_segment[k]
+                glob[k] = results[plan.key_group[k]][s.offset : s.offset + s.numel].view(s.shape).clone()
+            return glob
+        return self.packer.unpack(plan, results, as_torch=plan.input_kind == "torch")

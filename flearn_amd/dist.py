@@ -1,0 +1,117 @@
+"""Multi-GPU aggregation: element-range sharding of the bucket + RCCL all-gather over xGMI.
+
+One process per GPU (torch.distributed, backend "nccl" = RCCL).  The aggregation is independent
+per element, so the flattened fp32 bucket is split by COLUMNS: every rank holds its columns of
+all N clients and reduces them with the same fused kernel; the only exchange is reassembling the
+global model.  Layer-granular sharding (what the north star's wording suggests) would cap
+ResNet-18 at ~5x on 8 GPUs because fc/layer4 tensors are up to 20% of the model; columns
+balance exactly.
+
+Column layout (block-cyclic, `stripes` stripes):
+    P_pad = stripes * world * S,  S a multiple of 64 (256-B aligned shard slices)
+    stripe c covers global columns [c*W*S, (c+1)*W*S); rank r owns [c*W*S + r*S, +S)
+    rank r's local stack is [N, stripes*S]: local column c*S + j <-> global c*W*S + r*S + j
+so the all-gather of stripe c writes one contiguous range of the global bucket, and stripe c's
+gather (on RCCL's stream) overlaps the reduce of stripe c+1 (on the compute stream).
+Optimizer state (prev, v_t) is sharded the same way and never communicated.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import torch
+import torch.distributed as dist
+
+ALIGN = 64
+
+
+@dataclass(frozen=True)
+class ShardPlan:
+    n_cols: int  # real global columns (parameters)
+    world: int
+    rank: int
+    stripes: int
+    shard: int  # S: columns per (stripe, rank) slice
+
+    @staticmethod
+    def make(n_cols: int, world: int, rank: int, stripes: int = 4) -> "ShardPlan":
+        if world < 1 or not 0 <= rank < world or stripes < 1:
+            raise ValueError("bad world / rank / stripes")
+        per = -(-max(n_cols, 1) // (world * stripes))
+        shard = -(-per // ALIGN) * ALIGN
+        return ShardPlan(n_cols, world, rank, stripes, shard)
+
+    @property
+    def padded(self) -> int:
+        return self.stripes * self.world * self.shard
+
+    @property
+    def local_cols(self) -> int:
+        return self.stripes * self.shard
+
+    def global_begin(self, stripe: int, rank: int | None = None) -> int:
+        r = self.rank if rank is None else rank
+        return stripe * self.world * self.shard + r * self.shard
+
+    def local_begin(self, stripe: int) -> int:
+        return stripe * self.shard
+
+    def local_to_global(self, local_col: int) -> int:
+        c, j = divmod(local_col, self.shard)
+        return self.global_begin(c) + j
+
+    def real_cols_in_slice(self, stripe: int, rank: int | None = None) -> int:
+        """Columns of this slice that are real parameters (the tail slices may be padding)."""
+        g0 = self.global_begin(stripe, rank)
+        return max(0, min(self.shard, self.n_cols - g0))
+
+
+class ShardedReducer:
+    """Runs one aggregation step on this rank's shard and reassembles the full bucket.
+
+    reduce_fn(col_begin, n_cols, out_slice) reduces local columns [col_begin, +n_cols) into
+    out_slice — on a GPU it is the HIP kernel (aggregator.reduce_stack); the CPU tests inject
+    the oracle to check the sharding and gather logic with gloo.
+    """
+
+    def __init__(self, plan: ShardPlan, reduce_fn, device, group=None, local_out=None):
+        self.plan = plan
+        self.reduce_fn = reduce_fn
+        self.device = torch.device(device)
+        self.group = group
+        # local_out may alias the sharded `prev` of a fused optimizer (updated in place)
+        self.local_out = (torch.empty(plan.local_cols, dtype=torch.float32, device=self.device)
+                          if local_out is None else local_out)
+        # one rank: local columns ARE the global columns, nothing to reassemble
+        self.full = (self.local_out if plan.world == 1
+                     else torch.empty(plan.padded, dtype=torch.float32, device=self.device))
+
+    def step(self) -> torch.Tensor:
+        p = self.plan
+        works = []
+        for c in range(p.stripes):
+            lo = p.local_begin(c)
+            self.reduce_fn(lo, p.shard, self.local_out[lo : lo + p.shard])
+            if p.world > 1:
+                dst = self.full[c * p.world * p.shard : (c + 1) * p.world * p.shard]
+                works.append(dist.all_gather_into_tensor(dst, self.local_out[lo : lo + p.shard],
+                                                         group=self.group, async_op=True))
+        for w in works:
+            w.wait()
+        return self.full[: p.n_cols]
+
+
+def hip_reduce_fn(stack, weights, mode, denom, **epilogue):
+    """reduce_fn over a device-resident local stack [N, local_cols] with the fused HIP kernel.
+    Epilogue state tensors (prev, v), if any, are local-column tensors and are sliced alike."""
+    from .aggregator import reduce_stack
+
+    prev, v = epilogue.pop("prev", None), epilogue.pop("v", None)
+
+    def fn(col_begin, n_cols, out_slice):
+        kw = dict(epilogue)
+        if prev is not None:
+            kw.update(prev=prev[col_begin : col_begin + n_cols], v=v[col_begin : col_begin + n_cols])
+        reduce_stack(stack, weights, mode, denom, col_begin=col_begin, n_cols=n_cols, out32=out_slice, **kw)
+
+    return fn

@@ -1,0 +1,122 @@
+/*
+ * flearn_amd.h — C ABI of the MI355X FedAVG-family aggregation engine.
+ *
+ * The reference (wnma3mz/flearn v0.0.5) is pure Python and has no FFI; every entry point below
+ * replaces a numpy expression sequence inside the reference's Strategy plugins.  The reference
+ * interface each function stands in for is cited (paths relative to the flearn repo root).
+ *
+ * Conventions (all functions):
+ *   - every data pointer is a DEVICE pointer (hipMalloc / torch CUDA tensor storage) on the
+ *     current HIP device, except where noted;
+ *   - `stream` is a hipStream_t passed as void* (0 = legacy default stream); launches are
+ *     asynchronous, nothing here synchronises, allocates or frees;
+ *   - a client stack is a row-major [n_clients][row_stride] array: row r holds client r's
+ *     flattened bucket; the functions read the column window [col_begin, col_begin + n_cols)
+ *     of every row, and index every per-column array (out32, out64, prev, v) from 0 at col_begin;
+ *   - vector paths need `stack`, `col_begin` and `row_stride` aligned so that each row window
+ *     starts on 16 bytes (FA_ERR_ALIGN otherwise); n_cols may be any value >= 0;
+ *   - return FA_OK (0) or a negative FA_ERR_*; fa_last_error() gives a thread-local message.
+ *   - client order is the list order: client 0's product initialises the sum and clients
+ *     1..n-1 are added strictly in order, with no fused multiply-add, which is what makes the
+ *     fp32 path bit-identical to the reference's numpy loop.
+ */
+#ifndef FLEARN_AMD_H_
+#define FLEARN_AMD_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FA_ABI_VERSION 1
+
+/* return codes */
+#define FA_OK 0
+#define FA_ERR_ARG (-1)    /* bad size / null pointer / unknown enum */
+#define FA_ERR_ALIGN (-2)  /* row window not 16-byte aligned */
+#define FA_ERR_LAUNCH (-3) /* HIP launch error */
+
+/* Reduce modes: how numpy (NEP 50, numpy >= 2) evaluates
+ *   w = a0*x0; w += a_n*x_n; w = np.divide(w, np.sum(a))          strategy.py:123-129
+ * for fp32 client tensors, by the Python type of the weights a_n.                               */
+#define FA_MODE_W32_DIV64 0 /* Python float/int weights: fl32(a)*x, fp32 sum, f64 divide by the
+                               f64/int64 np.sum -> float64 result (flearn default, Client.py:157) */
+#define FA_MODE_W32_DIV32 1 /* np.float32 weights: fp32 product/sum, fp32 divide by the fp32
+                               np.sum -> float32 result                                           */
+#define FA_MODE_W64 2       /* np.float64 / np.int64 weights: f64 product, f64 sum, f64 divide   */
+
+/* Server-side epilogues fused after the mean (the reference runs the same formulas in
+ * client_receive with w_local = the client's weights; the fused server form uses
+ * w_local = prev = the previous global model).                                                  */
+#define FA_OP_MEAN 0    /* w = mean                                                  avg.py:25-33 */
+#define FA_OP_AVGM 1    /* d = g - l; v = d + beta*v; w = l + v                    avgm.py:19-36 */
+#define FA_OP_ADAGRAD 2 /* d = g - l; v = v + d*d; w = l + (eta*d)/(sqrt(v)+tau)   opt.py:52-63 */
+#define FA_OP_YOGI 3    /* v = v - (c*d*d)*sign(v - d*d), c = 1-beta2               opt.py:54-58 */
+#define FA_OP_ADAM 4    /* v = beta2*v + c*d*d                                      opt.py:59-60 */
+
+/* Precision of the epilogue state / the mean (FA_PREC_F64 for modes DIV64 and W64,
+ * FA_PREC_F32 for mode DIV32 — the dtype numpy gives w_glob in that mode).                      */
+#define FA_PREC_F32 0
+#define FA_PREC_F64 1
+
+typedef struct fa_epilogue {
+  int32_t op;        /* FA_OP_*                                                         */
+  int32_t reserved;  /* must be 0                                                       */
+  const float* prev; /* [n_cols] fp32 previous global model (AVGM/OPT), else NULL       */
+  void* v;           /* [n_cols] optimizer state v_t: double* (F64) or float* (F32)     */
+  double beta;       /* AVGM momentum beta (reference default 0.9, avgm.py:38)          */
+  double eta;        /* OPT step size 1e-1 (opt.py:24)                                  */
+  double tau;        /* OPT epsilon 1e-9 (opt.py:25)                                    */
+  double beta2;      /* OPT beta2 0.99 (opt.py:27); kernels use c = 1 - beta2 and beta2 */
+} fa_epilogue;
+
+int fa_abi_version(void);
+const char* fa_last_error(void);
+
+/* Weighted mean of fp32 client tensors (+ optional fused epilogue).
+ * Replaces Strategy.server_ensemble (flearn/common/strategy/strategy.py:102-130) for the
+ * fp32 keys of the bucket, and — with epi->op != FA_OP_MEAN — the AVGM/OPT update math of
+ * flearn/common/strategy/avgm.py:19-36 / opt.py:23-65.
+ *   weights : device array of n_clients values, already cast the way numpy casts them:
+ *             float (fp32) for FA_MODE_W32_*, double for FA_MODE_W64.
+ *   denom   : np.sum(agg_weight_lst) as a double (exact for every dtype numpy produces here).
+ *   out32   : [n_cols] fp32 result (what load_state_dict ends up with), may be NULL.
+ *   out64   : [n_cols] f64 result (the reference's w_glob dtype for DIV64/W64), may be NULL.
+ *   epi     : host pointer, NULL == FA_OP_MEAN.                                                */
+int fa_reduce_f32(const float* stack, int64_t row_stride, int32_t n_clients, int32_t mode,
+                  const void* weights, double denom, int64_t col_begin, int64_t n_cols,
+                  const fa_epilogue* epi, float* out32, double* out64, void* stream);
+
+/* Weighted mean of f64 client tensors (float64 buffers, and int64 buffers the host has cast to
+ * f64 — numpy promotes int64 * Python-float to float64).  f64 product and sum, f64 divide.
+ * Replaces server_ensemble for those keys (strategy.py:123-129).                              */
+int fa_reduce_f64(const double* stack, int64_t row_stride, int32_t n_clients,
+                  const double* weights, double denom, int64_t col_begin, int64_t n_cols,
+                  double* out64, void* stream);
+
+/* Weighted sum of int64 client tensors with int64 weights (Python-int weights times int64
+ * buffers stay int64 in numpy, wrapping on overflow), then true division in f64.
+ * Replaces server_ensemble for int64 keys with integer weights (strategy.py:123-129).         */
+int fa_reduce_i64(const int64_t* stack, int64_t row_stride, int32_t n_clients,
+                  const int64_t* weights, double denom, int64_t col_begin, int64_t n_cols,
+                  double* out64, void* stream);
+
+/* Standalone AVGM/OPT update of a received global model (no reduce): the reference location
+ * of this math, AVGM.client_receive (avgm.py:38-45) / OPT.client_receive (opt.py:67-76).
+ *   prec   : FA_PREC_F64 (glob is double*, v is double*) or FA_PREC_F32 (float*, float*).
+ *   local  : [n] fp32 w_local; glob : [n] the received w_glob.                                */
+int fa_opt_apply(int32_t prec, const fa_epilogue* epi, const float* local, const void* glob,
+                 int64_t n, float* out32, double* out64, void* stream);
+
+/* Synthetic client data: dst[r*row_stride + c] = U(-1,1) from splitmix64 of
+ * (seed, row_begin + r, col_global_begin + c) — the bench/test generator; the CPU oracle
+ * regenerates any element.  Not a reference interface.                                        */
+int fa_fill_uniform_f32(float* dst, int64_t row_stride, int32_t n_rows, int64_t n_cols,
+                        uint64_t seed, int64_t row_begin, int64_t col_global_begin, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* FLEARN_AMD_H_ */

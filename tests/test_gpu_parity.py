@@ -1,0 +1,322 @@
+"""GPU parity: the HIP path (through the C ABI) against the reference's golden vectors and the
+C oracle.  Bar: bit-exact (every output dtype, NaN position and sign of zero) — the kernels run
+the reference's fp32/f64 operation sequence with no contraction."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from flearn_amd import AVG, AVGM, BN, LG, LG_R, OPT
+from flearn_amd import _native as na
+from flearn_amd import aggregator as agg
+from flearn_amd import layouts
+from golden_io import Golden, assert_dict_bitwise, bitwise_equal, cases
+
+pytestmark = pytest.mark.gpu
+
+REDUCE_CASES = [c for c in cases() if c.startswith(("avg_", "bn_", "lg_", "trace_"))]
+ROUND_CASES = [c for c in cases() if c.endswith("_rounds3")]
+
+
+def upload(clients, weights):
+    return [{"agg_weight": w, "params": c} for w, c in zip(weights, clients)]
+
+
+def strategy_for(g: Golden):
+    call = g.meta["call"]
+    if call.startswith("BN()"):
+        return BN()
+    if call.startswith("LG_R("):
+        return LG_R(g.meta["shared_key_layers"])
+    if call.startswith("LG("):
+        return LG(g.meta["shared_key_layers"])
+    return AVG()
+
+
+# ---------------------------------------------------------------------------------------------
+# golden vectors from the reference
+# ---------------------------------------------------------------------------------------------
+
+
+@pytest.mark.parametrize("name", REDUCE_CASES)
+def test_strategy_server_matches_reference(name, cuda):
+    g = Golden(name)
+    s = strategy_for(g)
+    got = s.server(upload(g.clients(), g.weights()), 0)["w_glob"]
+    want = g.output()
+    assert_dict_bitwise(got, want, name)
+    kinds = g.output_kinds()
+    for k, v in got.items():  # value types as the reference returns them
+        if kinds[k].startswith("scalar:"):
+            assert type(v).__name__ == kinds[k].split(":")[1], k
+        elif kinds[k].startswith("torch:"):
+            assert isinstance(v, torch.Tensor) and str(v.dtype) == kinds[k][6:], k
+        else:
+            assert isinstance(v, np.ndarray), k
+
+
+@pytest.mark.parametrize("name", REDUCE_CASES)
+def test_float32_output_is_cast_of_reference(name, cuda):
+    """output='float32' returns fl32(w_glob) — what load_state_dict stores."""
+    g = Golden(name)
+    if g.meta.get("input_kind") == "torch":
+        pytest.skip("torch uploads keep torch outputs")
+    s = strategy_for(g)
+    s.output = "float32"
+    got = s.server(upload(g.clients(), g.weights()), 0)["w_glob"]
+    for k, w in g.output().items():
+        w = np.asarray(w)
+        if w.dtype == np.float64 and g.meta["in_dtypes"][k] == "float32":
+            assert bitwise_equal(np.asarray(got[k]), w.astype(np.float32)), k
+
+
+def _round_inputs(g, r):
+    from golden_io import decode_weight, regenerate
+
+    layout = [(k, tuple(s)) for k, s in g.meta["gen"]["layout"]]
+    clients = regenerate(layout, 6, g.meta["gen"]["seeds"][r])
+    return clients, [decode_weight(e) for e in g.meta["round_weights"][r]]
+
+
+@pytest.mark.parametrize("name", ROUND_CASES)
+def test_server_side_fused_optimizer_matches_reference(name, cuda):
+    """Server-fused FedAVGM / FedOPT: round r = mean of fresh uploads, then the reference update
+    with w_local = previous global (fp32); 3 rounds, state carried in HBM."""
+    g = Golden(name)
+    op = g.meta["op"]
+    s = AVGM(server_side=True) if op == "avgm" else OPT(server_side=True, method=op)
+    s.server_opt.init_global({k[6:]: v for k, v in g.arrays.items() if k.startswith("prev0:")})
+    for r in range(g.meta["rounds"]):
+        clients, weights = _round_inputs(g, r)
+        got = s.server(upload(clients, weights), r)["w_glob"]
+        assert_dict_bitwise(got, g.output(f"w{r}"), f"{name} w{r}")
+        v = s.server_opt.v_t(s.engine.last_plan)
+        assert_dict_bitwise(v, g.output(f"v{r}"), f"{name} v{r}")
+
+
+@pytest.mark.parametrize("name", ROUND_CASES)
+def test_client_side_update_matches_reference(name, cuda):
+    """AVGM.mean_momentum / OPT.adaptive_opt on the GPU (the reference's client_receive math)."""
+    g = Golden(name)
+    op = g.meta["op"]
+    s = AVGM() if op == "avgm" else OPT()
+    prev = {k[6:]: v.copy() for k, v in g.arrays.items() if k.startswith("prev0:")}
+    for r in range(g.meta["rounds"]):
+        avg = g.output(f"avg{r}")
+        if op == "avgm":
+            w = s.mean_momentum(dict(prev), avg, 0.9)
+        else:
+            w = s.adaptive_opt(dict(prev), avg, op)
+        assert_dict_bitwise(w, g.output(f"w{r}"), f"{name} w{r}")
+        assert_dict_bitwise(s.v_t, g.output(f"v{r}"), f"{name} v{r}")
+        prev = {k: np.asarray(w[k]).astype(np.float32) for k in prev}
+
+
+def test_empty_upload_list_exits_like_reference(cuda):
+    with pytest.raises(SystemExit):
+        AVG().server([], 0)
+
+
+def test_shape_mismatch_is_rejected(cuda):
+    a = {"w": np.ones((10, 1), np.float32)}
+    b = {"w": np.ones((10,), np.float32)}
+    with pytest.raises(SystemExit):
+        AVG().server(upload([a, b], [1.0, 1.0]), 0)
+
+
+def test_device_uploads(cuda):
+    """Uploads already resident on the GPU are packed device-to-device."""
+    g = Golden("avg_w1_n10")
+    cl = [{k: torch.from_numpy(v).to(cuda) for k, v in c.items()} for c in g.clients()]
+    s = AVG(output="device")
+    got = s.server(upload(cl, g.weights()), 0)["w_glob"]
+    for k, w in g.output().items():
+        assert got[k].device.type == "cuda"
+        assert bitwise_equal(got[k].cpu().numpy(), np.asarray(w).astype(np.float32)), k
+
+
+# ---------------------------------------------------------------------------------------------
+# kernel vs C oracle (seeded synthetic inputs generated on device, regenerated on the host)
+# ---------------------------------------------------------------------------------------------
+
+
+def _device_stack(n, stride, seed, cols=None):
+    x = torch.empty((n, stride), dtype=torch.float32, device="cuda")
+    agg.fill_uniform(x, seed, n_cols=cols)
+    return x
+
+
+@pytest.mark.parametrize("n", [1, 2, 7, 8, 9, 16, 17, 100])
+@pytest.mark.parametrize("ncols", [1, 3, 4, 5, 63, 1023, 2048, 2049, 4099, 70001])
+def test_reduce_kernel_bit_exact(n, ncols, cuda):
+    stride = -(-ncols // 64) * 64
+    x = _device_stack(n, stride, seed=n * 7919 + ncols)
+    w32 = (np.arange(1, n + 1, dtype=np.float64) * 0.37).astype(np.float32)
+    denom = float(np.sum([float(v) for v in w32]))
+    out64 = torch.empty(ncols, dtype=torch.float64, device=cuda)
+    out32 = torch.empty(ncols, dtype=torch.float32, device=cuda)
+    agg.reduce_stack(x, torch.from_numpy(w32).to(cuda), na.MODE_W32_DIV64, denom, n_cols=ncols,
+                     out32=out32, out64=out64)
+    want = oracle.c_reduce(oracle.MODE_W32_DIV64, x[:, :ncols].cpu().numpy(), w32, denom)
+    assert bitwise_equal(out64.cpu().numpy(), want)
+    assert bitwise_equal(out32.cpu().numpy(), want.astype(np.float32))
+
+
+@pytest.mark.parametrize("col_begin", [0, 4, 64, 1000, 4096])
+def test_column_window(col_begin, cuda):
+    """A window [col_begin, +n) equals the same columns of the full reduce (sharding property)."""
+    n, stride = 13, 8192
+    x = _device_stack(n, stride, seed=5)
+    w = torch.ones(n, dtype=torch.float32, device=cuda)
+    full = torch.empty(stride, dtype=torch.float64, device=cuda)
+    agg.reduce_stack(x, w, na.MODE_W32_DIV64, float(n), out64=full)
+    ncols = 3001
+    part = torch.empty(ncols, dtype=torch.float64, device=cuda)
+    agg.reduce_stack(x, w, na.MODE_W32_DIV64, float(n), col_begin=col_begin, n_cols=ncols, out64=part)
+    assert torch.equal(part, full[col_begin : col_begin + ncols])
+
+
+@pytest.mark.parametrize("mode", [na.MODE_W32_DIV64, na.MODE_W32_DIV32, na.MODE_W64])
+def test_modes_bit_exact(mode, cuda):
+    n, p = 37, 12345
+    x = _device_stack(n, 12352, seed=mode + 3)
+    rng = np.random.default_rng(mode)
+    wv = rng.uniform(0.1, 3.0, n)
+    if mode == na.MODE_W64:
+        w = wv.astype(np.float64)
+        denom = float(np.sum(w))
+    elif mode == na.MODE_W32_DIV32:
+        w = wv.astype(np.float32)
+        denom = float(np.sum(w))  # np.float32 pairwise sum, exact as double
+    else:
+        w = wv.astype(np.float32)
+        denom = float(np.sum([float(v) for v in wv]))
+    wd = torch.from_numpy(w).to(cuda)
+    want = oracle.c_reduce(mode, x[:, :p].cpu().numpy(), w, denom)
+    if want.dtype == np.float32:
+        out = torch.empty(p, dtype=torch.float32, device=cuda)
+        agg.reduce_stack(x, wd, mode, denom, n_cols=p, out32=out)
+    else:
+        out = torch.empty(p, dtype=torch.float64, device=cuda)
+        agg.reduce_stack(x, wd, mode, denom, n_cols=p, out64=out)
+    assert bitwise_equal(out.cpu().numpy(), want)
+
+
+@pytest.mark.parametrize("op", ["avgm", "adagrad", "yogi", "adam"])
+@pytest.mark.parametrize("prec", ["f64", "f32"])
+def test_fused_epilogue_bit_exact(op, prec, cuda):
+    n, p, stride = 11, 5001, 5056
+    mode = na.MODE_W32_DIV64 if prec == "f64" else na.MODE_W32_DIV32
+    x = _device_stack(n, stride, seed=17)
+    w = (np.arange(n, dtype=np.float32) + 1.0).astype(np.float32)
+    denom = float(np.sum([float(v) for v in w])) if prec == "f64" else float(np.sum(w))
+    prev = torch.empty((1, stride), dtype=torch.float32, device=cuda)
+    agg.fill_uniform(prev, seed=99)
+    prev_h = prev[0, :p].cpu().numpy().copy()
+    vdt = torch.float64 if prec == "f64" else torch.float32
+    v = (torch.rand(p, dtype=torch.float64, device=cuda) * 0.01).to(vdt)
+    v_h = v.cpu().numpy().copy()
+    out32 = torch.empty(p, dtype=torch.float32, device=cuda)
+    out64 = torch.empty(p, dtype=torch.float64, device=cuda) if prec == "f64" else None
+    agg.reduce_stack(x, torch.from_numpy(w).to(cuda), mode, denom, n_cols=p, out32=out32, out64=out64,
+                     op=na.OP_BY_NAME[op], prev=prev[0], v=v)
+    g = oracle.c_reduce(mode, x[:, :p].cpu().numpy(), w, denom)
+    want = oracle.c_update(op, g, prev_h, v_h)
+    assert bitwise_equal(v.cpu().numpy(), v_h)
+    if prec == "f64":
+        assert bitwise_equal(out64.cpu().numpy(), want)
+    assert bitwise_equal(out32.cpu().numpy(), want.astype(np.float32))
+
+
+def test_fused_epilogue_in_place_prev(cuda):
+    """prev may double as out32 (how ServerOptimizer advances the global model)."""
+    n, p = 5, 4096
+    x = _device_stack(n, p, seed=1)
+    w = torch.ones(n, dtype=torch.float32, device=cuda)
+    prev = torch.empty((1, p), dtype=torch.float32, device=cuda)
+    agg.fill_uniform(prev, seed=2)
+    prev_h = prev[0].cpu().numpy().copy()
+    v = torch.zeros(p, dtype=torch.float64, device=cuda)
+    v_h = np.zeros(p)
+    agg.reduce_stack(x, w, na.MODE_W32_DIV64, 5.0, out32=prev[0], op=na.OP_AVGM, prev=prev[0], v=v)
+    want = oracle.c_update("avgm", oracle.c_reduce(0, x.cpu().numpy(), np.ones(n, np.float32), 5.0), prev_h, v_h)
+    assert bitwise_equal(prev[0].cpu().numpy(), want.astype(np.float32))
+
+
+def test_f64_and_i64_kernels(cuda):
+    rng = np.random.default_rng(3)
+    n, p = 9, 777
+    xs = rng.standard_normal((n, p))
+    w = rng.uniform(0.5, 2.0, n)
+    stack = torch.zeros((n, 832), dtype=torch.float64)
+    stack[:, :p] = torch.from_numpy(xs)
+    out = torch.empty(832, dtype=torch.float64, device=cuda)
+    agg.reduce_stack_f64(stack.to(cuda), torch.from_numpy(w).to(cuda), float(w.sum()), out)
+    assert bitwise_equal(out[:p].cpu().numpy(), oracle.c_reduce("f64", xs, w, float(w.sum())))
+    xi = rng.integers(-(2**40), 2**40, (n, p), dtype=np.int64)
+    wi = rng.integers(1, 600, n).astype(np.int64)
+    stack = torch.zeros((n, 832), dtype=torch.int64)
+    stack[:, :p] = torch.from_numpy(xi)
+    agg.reduce_stack_i64(stack.to(cuda), torch.from_numpy(wi).to(cuda), float(wi.sum()), out)
+    assert bitwise_equal(out[:p].cpu().numpy(), oracle.c_reduce("i64", xi, wi, float(wi.sum())))
+
+
+def test_misaligned_window_fails_loudly(cuda):
+    x = torch.zeros((2, 128), dtype=torch.float32, device=cuda)
+    w = torch.ones(2, dtype=torch.float32, device=cuda)
+    out = torch.empty(10, dtype=torch.float64, device=cuda)
+    with pytest.raises(na.NativeError):
+        agg.reduce_stack(x, w, na.MODE_W32_DIV64, 2.0, col_begin=1, n_cols=10, out64=out)
+
+
+def test_deterministic(cuda):
+    x = _device_stack(50, 1 << 20, seed=8)
+    w = torch.ones(50, dtype=torch.float32, device=cuda)
+    a = torch.empty(1 << 20, dtype=torch.float32, device=cuda)
+    b = torch.empty_like(a)
+    agg.reduce_stack(x, w, na.MODE_W32_DIV64, 50.0, out32=a)
+    agg.reduce_stack(x, w, na.MODE_W32_DIV64, 50.0, out32=b)
+    assert torch.equal(a, b)
+
+
+# ---------------------------------------------------------------------------------------------
+# BASELINE-size cases: full HIP run, spot-checked column windows regenerated on the host
+# ---------------------------------------------------------------------------------------------
+
+
+def _spot_windows(p, width=4096):
+    starts = [0, (p // 3) & ~63, (p // 2) & ~63, max(0, (p - width) & ~63)]
+    return [(s, min(width, p - s)) for s in starts]
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("layout,n,op", [("resnet18", 100, "mean"), ("resnet50", 100, "avgm"),
+                                         ("vit_b_16", 100, "adagrad"), ("resnet18", 1000, "mean")])
+def test_baseline_config_spot_parity(layout, n, op, cuda):
+    """Configs 2-5 at full size on one GPU: the kernel runs over the whole bucket; column windows
+    at the start / middle / end are recomputed by the C oracle from regenerated inputs."""
+    p = layouts.padded_f32_stride(layouts.get(layout))
+    x = torch.empty((n, p), dtype=torch.float32, device=cuda)
+    agg.fill_uniform(x, seed=1234)
+    w = torch.ones(n, dtype=torch.float32, device=cuda)
+    out32 = torch.empty(p, dtype=torch.float32, device=cuda)
+    kw = {}
+    if op != "mean":
+        prev = torch.empty((1, p), dtype=torch.float32, device=cuda)
+        agg.fill_uniform(prev, seed=1)
+        v = torch.zeros(p, dtype=torch.float64, device=cuda)
+        kw = dict(op=na.OP_BY_NAME[op], prev=prev[0], v=v)
+        prev_h = prev[0].cpu().numpy().copy()
+    agg.reduce_stack(x, w, na.MODE_W32_DIV64, float(n), out32=out32, **kw)
+    got = out32.cpu().numpy()
+    del x
+    torch.cuda.empty_cache()
+    for c0, width in _spot_windows(p):
+        cols = oracle.fill_uniform(n, width, 1234, row0=0, col0=c0)
+        g = oracle.c_reduce(oracle.MODE_W32_DIV64, cols, np.ones(n, np.float32), float(n))
+        if op != "mean":
+            g = oracle.c_update(op, g, prev_h[c0 : c0 + width], np.zeros(width))
+        assert bitwise_equal(got[c0 : c0 + width], g.astype(np.float32)), (layout, c0)
+    assert np.isfinite(got).all()
