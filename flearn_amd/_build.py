@@ -9,6 +9,7 @@ from pathlib import Path
 HERE = Path(__file__).resolve().parent
 REPO = HERE.parent
 SOURCES = [HERE / "csrc" / "fa_reduce.hip"]
+DEPS = [HERE / "csrc" / "fa_device.hpp"]
 HEADERS = [REPO / "include" / "flearn_amd.h"]
 OUT = HERE / "lib" / "libflearn_amd.so"
 ARCH = os.environ.get("FLEARN_AMD_ARCH", "gfx950")
@@ -22,7 +23,7 @@ def hipcc() -> str:
 
 
 def build_native(force: bool = False, verbose: bool = False) -> Path:
-    newest = max(p.stat().st_mtime for p in SOURCES + HEADERS + [Path(__file__)])
+    newest = max(p.stat().st_mtime for p in SOURCES + DEPS + HEADERS + [Path(__file__)])
     if OUT.exists() and not force and OUT.stat().st_mtime >= newest:
         return OUT
     OUT.parent.mkdir(parents=True, exist_ok=True)

@@ -1,0 +1,375 @@
+// fa_device.hpp — device code of the FedAVG-family aggregation engine (gfx950).
+//
+// Included by fa_reduce.hip (the product C ABI) and by tools/tune_reduce.hip (the geometry
+// sweep).  Everything here is header-only templates in namespace fa.
+//
+// Hot path: Strategy.server_ensemble (flearn/common/strategy/strategy.py:102-130), i.e. for
+// every element p of the flattened model bucket
+//     acc = a0*x[0][p];  acc += a_n*x[n][p]  (n = 1..N-1, in list order);  w = acc / sum(a)
+// optionally followed by the AVGM / FedOPT update (avgm.py:19-36, opt.py:23-65).
+//
+// Mapping (HBM-bound streaming reduce, 0.5 flop/B, no MFMA):
+//   * a TILE is kThreads*V quads (4 contiguous fp32 = one 16-B global_load_dwordx4) of every
+//     client row; thread t owns quads t, t+kThreads, ... so each wave instruction reads 1 KiB
+//     contiguous of one row;
+//   * the client loop walks the rows in list order (the bit-exact sequential fp32 sum numpy
+//     does) unrolled U deep: U*V independent 16-B loads in flight per thread hide HBM latency
+//     behind a running sum that depends only on already-arrived data;
+//   * every client value is read exactly once per launch (NT: non-temporal loads);
+//   * the epilogue (divide, optional momentum/adaptive update, f32/f64 stores) is fused: the only
+//     HBM traffic is N*P*4 bytes of client reads plus O(P) output/state bytes.
+// Compile with -ffp-contract=off: a fused a*x+acc changes fp32 rounding and breaks bit-parity.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "flearn_amd.h"
+
+namespace fa {
+
+constexpr int kThreads = 256;
+
+template <typename T>
+struct vec4 {
+  typedef T type __attribute__((ext_vector_type(4)));
+};
+
+template <typename T, bool NT>
+__device__ __forceinline__ typename vec4<T>::type load_quad(const T* p) {
+  if constexpr (NT)
+    return __builtin_nontemporal_load(reinterpret_cast<const typename vec4<T>::type*>(p));
+  else
+    return *reinterpret_cast<const typename vec4<T>::type*>(p);
+}
+
+template <typename T>
+__device__ __forceinline__ typename vec4<T>::type load_quad_guarded(const T* p, int valid) {
+  typename vec4<T>::type r = {T(0), T(0), T(0), T(0)};
+  if (valid > 0) r[0] = p[0];
+  if (valid > 1) r[1] = p[1];
+  if (valid > 2) r[2] = p[2];
+  if (valid > 3) r[3] = p[3];
+  return r;
+}
+
+template <typename T>
+__device__ __forceinline__ void store_quad(T* p, typename vec4<T>::type v, int valid) {
+  if (valid == 4) {
+    *reinterpret_cast<typename vec4<T>::type*>(p) = v;
+  } else {
+    if (valid > 0) p[0] = v[0];
+    if (valid > 1) p[1] = v[1];
+    if (valid > 2) p[2] = v[2];
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Accumulation policies: product dtype = sum dtype, chosen by numpy's promotion of the weight
+// type against the tensor dtype (resolved on the host: flearn_amd/semantics.py).
+// ---------------------------------------------------------------------------------------------
+struct AccF32 {  // fp32 tensors x Python-float/int or np.float32 weights
+  typedef float x_t;
+  typedef float w_t;
+  typedef float acc_t;
+  static __device__ __forceinline__ float mul(float w, float x) { return w * x; }
+};
+struct AccF32W64 {  // fp32 tensors x np.float64/np.int64 weights: promoted to f64
+  typedef float x_t;
+  typedef double w_t;
+  typedef double acc_t;
+  static __device__ __forceinline__ double mul(double w, float x) { return w * (double)x; }
+};
+struct AccF64 {  // f64 tensors (and int64 buffers cast to f64) x f64 weights
+  typedef double x_t;
+  typedef double w_t;
+  typedef double acc_t;
+  static __device__ __forceinline__ double mul(double w, double x) { return w * x; }
+};
+struct AccI64 {  // int64 buffers x Python-int weights: int64 arithmetic, wraps like numpy
+  typedef int64_t x_t;
+  typedef int64_t w_t;
+  typedef int64_t acc_t;
+  static __device__ __forceinline__ int64_t mul(int64_t w, int64_t x) {
+    return (int64_t)((uint64_t)w * (uint64_t)x);
+  }
+};
+
+template <typename A>
+__device__ __forceinline__ A add(A a, A b) {
+  return a + b;
+}
+template <>
+__device__ __forceinline__ int64_t add<int64_t>(int64_t a, int64_t b) {
+  return (int64_t)((uint64_t)a + (uint64_t)b);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Epilogue: mean in precision T (double for DIV64/W64, float for DIV32) and the optional
+// server-side optimizer update, all in T with the reference's operation order.
+// ---------------------------------------------------------------------------------------------
+template <typename T>
+struct Epi {
+  T denom;
+  const float* prev;
+  T* v;
+  T beta, eta, tau, beta2, c;  // c = 1 - beta2 (evaluated in double on the host, as Python does)
+  float* out32;
+  double* out64;
+};
+
+template <typename T>
+__device__ __forceinline__ T sign_of(T x) {
+  // np.sign: -1, 0, +1, NaN for NaN
+  return x > T(0) ? T(1) : (x < T(0) ? T(-1) : (x == T(0) ? T(0) : x));
+}
+
+template <typename T, int OP>
+__device__ __forceinline__ T update(const Epi<T>& e, T g, T l, T& vv) {
+  if constexpr (OP == FA_OP_MEAN) {
+    return g;
+  } else {
+    const T d = g - l;  // delta_w = w_glob - w_local            avgm.py:22-25 / opt.py:30-33
+    if constexpr (OP == FA_OP_AVGM) {
+      vv = d + e.beta * vv;  // v_t = delta + beta*v_t           avgm.py:31-32
+      return l + vv;         // w_local + v_t                    avgm.py:34-35
+    } else {
+      const T m = d * d;  // np.multiply(delta, delta)            opt.py:52
+      if constexpr (OP == FA_OP_ADAGRAD) {
+        vv = vv + m;  //                                          opt.py:53-54
+      } else if constexpr (OP == FA_OP_YOGI) {
+        vv = vv - (e.c * m) * sign_of<T>(vv - m);  //             opt.py:55-58
+      } else {
+        vv = e.beta2 * vv + e.c * m;  //                          opt.py:59-60
+      }
+      return l + (e.eta * d) / (sqrt(vv) + e.tau);  //          opt.py:62-63
+    }
+  }
+}
+
+template <typename T, int OP, typename A>
+__device__ __forceinline__ void finish_quad(const Epi<T>& e, int64_t c, int valid,
+                                            typename vec4<A>::type acc) {
+  typename vec4<T>::type w;
+  typename vec4<T>::type vv = {T(0), T(0), T(0), T(0)};
+  typename vec4<float>::type l = {0.f, 0.f, 0.f, 0.f};
+  if constexpr (OP != FA_OP_MEAN) {
+    if (valid == 4) {
+      l = *reinterpret_cast<const typename vec4<float>::type*>(e.prev + c);
+      vv = *reinterpret_cast<const typename vec4<T>::type*>(e.v + c);
+    } else {
+      l = load_quad_guarded(e.prev + c, valid);
+      vv = load_quad_guarded(e.v + c, valid);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const T g = (T)acc[j] / e.denom;  // np.divide(w_glob, np.sum(a))  strategy.py:127-129
+    T vj = vv[j];
+    w[j] = update<T, OP>(e, g, (T)l[j], vj);
+    vv[j] = vj;
+  }
+  if constexpr (OP != FA_OP_MEAN) store_quad<T>(e.v + c, vv, valid);
+  if (e.out32) {
+    typename vec4<float>::type o = {(float)w[0], (float)w[1], (float)w[2], (float)w[3]};
+    store_quad<float>(e.out32 + c, o, valid);
+  }
+  if (e.out64) {
+    typename vec4<double>::type o = {(double)w[0], (double)w[1], (double)w[2], (double)w[3]};
+    store_quad<double>(e.out64 + c, o, valid);
+  }
+}
+
+// Sub-tile kinds for reduce_subtile.
+enum Part : int {
+  kFull = 0,   // all V quads of every thread complete and inside the window (the hot path)
+  kMasked = 1  // only slots v < nv are this block's; nv is WAVE-uniform (scalar branches)
+};
+
+// One sub-tile of the client stack for this thread: quads q0 + v*kThreads (v < V) of every row,
+// all N rows in list order, then the fused epilogue.  Every slot is predicated with a
+// compile-time-unrollable `if` (a `break` would keep the loops rolled and push the register
+// arrays to scratch).
+template <class P, typename T, int OP, int V, int U, bool NT, int PART>
+__device__ __forceinline__ void reduce_subtile(const typename P::x_t* __restrict__ base,
+                                               int64_t stride, int n,
+                                               const typename P::w_t* __restrict__ w, int64_t q0,
+                                               int nv, const Epi<T>& e) {
+  typedef typename P::x_t X;
+  typedef typename P::acc_t A;
+  typedef typename vec4<X>::type XV;
+  typedef typename vec4<A>::type AV;
+  AV acc[V];
+  {
+    const typename P::w_t w0 = w[0];
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      if (PART == kFull || v < nv) {
+        const XV x = load_quad<X, NT>(base + (q0 + (int64_t)v * kThreads) * 4);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[v][j] = P::mul(w0, x[j]);
+      }
+    }
+  }
+  int i = 1;
+  for (; i + U <= n; i += U) {
+    XV x[U][V];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const X* row = base + (int64_t)(i + u) * stride;
+#pragma unroll
+      for (int v = 0; v < V; ++v)
+        if (PART == kFull || v < nv) x[u][v] = load_quad<X, NT>(row + (q0 + (int64_t)v * kThreads) * 4);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const typename P::w_t wu = w[i + u];
+#pragma unroll
+      for (int v = 0; v < V; ++v) {
+        if (PART == kFull || v < nv) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[v][j] = add<A>(acc[v][j], P::mul(wu, x[u][v][j]));
+        }
+      }
+    }
+  }
+  for (; i < n; ++i) {
+    const X* row = base + (int64_t)i * stride;
+    const typename P::w_t wi = w[i];
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      if (PART == kFull || v < nv) {
+        const XV x = load_quad<X, NT>(row + (q0 + (int64_t)v * kThreads) * 4);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[v][j] = add<A>(acc[v][j], P::mul(wi, x[j]));
+      }
+    }
+  }
+#pragma unroll
+  for (int v = 0; v < V; ++v)
+    if (PART == kFull || v < nv) finish_quad<T, OP, A>(e, (q0 + (int64_t)v * kThreads) * 4, 4, acc[v]);
+}
+
+// The window's ragged end (at most one wave per launch): one quad at a time, element-guarded.
+template <class P, typename T, int OP>
+__device__ __attribute__((noinline)) void reduce_ragged(const typename P::x_t* __restrict__ base,
+                                                        int64_t stride, int n,
+                                                        const typename P::w_t* __restrict__ w,
+                                                        int64_t q0, int64_t qlim, int64_t ncols,
+                                                        const Epi<T>& e) {
+  typedef typename P::x_t X;
+  typedef typename vec4<typename P::acc_t>::type AV;
+#pragma unroll 1
+  for (int64_t q = q0; q < qlim; q += kThreads) {
+    const int64_t c = q * 4;
+    const int valid = (int)((ncols - c) < 4 ? (ncols - c) : 4);
+    AV acc;
+    {
+      const typename vec4<X>::type x = load_quad_guarded(base + c, valid);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[j] = P::mul(w[0], x[j]);
+    }
+#pragma unroll 1
+    for (int i = 1; i < n; ++i) {
+      const typename vec4<X>::type x = load_quad_guarded(base + (int64_t)i * stride + c, valid);
+      const typename P::w_t wi = w[i];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[j] = add<typename P::acc_t>(acc[j], P::mul(wi, x[j]));
+    }
+    finish_quad<T, OP, typename P::acc_t>(e, c, valid, acc);
+  }
+}
+
+// Sub-tile starting at quad qt, limited to quads < qlim (the block's range, <= the window).
+template <class P, typename T, int OP, int V, int U, bool NT>
+__device__ __forceinline__ void reduce_range_subtile(const typename P::x_t* __restrict__ base,
+                                                     int64_t stride, int n,
+                                                     const typename P::w_t* __restrict__ w,
+                                                     int64_t qt, int64_t qlim, int64_t ncols,
+                                                     const Epi<T>& e) {
+  constexpr int kSub = kThreads * V;
+  const int64_t q0 = qt + threadIdx.x;
+  const int64_t qfull = ncols / 4;  // complete quads in the window
+  if (qt + kSub <= qlim && qt + kSub <= qfull) {
+    reduce_subtile<P, T, OP, V, U, NT, kFull>(base, stride, n, w, q0, V, e);
+    return;
+  }
+  // slot v of wave wv covers quads [qt + v*kThreads + 64*wv, +64): count the complete ones
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x) / 64;
+  const int64_t wbase = qt + 64 * wv;
+  const int64_t lim = qlim < qfull ? qlim : qfull;
+  int nv = 0;
+  while (nv < V && wbase + (int64_t)nv * kThreads + 64 <= lim) ++nv;
+  if (nv > 0) reduce_subtile<P, T, OP, V, U, NT, kMasked>(base, stride, n, w, q0, nv, e);
+  // the rest of this wave's slots (only at the window's ragged end: lim < qlim)
+  const int64_t qr = q0 + (int64_t)nv * kThreads;
+  if (qr < qlim) reduce_ragged<P, T, OP>(base, stride, n, w, qr, qlim, ncols, e);
+}
+
+// Balanced grid.  Work unit: a CHUNK of 64 quads (1 KiB of one fp32 row = one wave-wide dwordx4
+// instruction).  The host sizes the grid as k full waves of resident blocks (k = rounds) so that
+// every block owns an equal share +-1 chunk of the window, preferably <= one sub-tile: all
+// blocks of a round finish together (no tail of late blocks) and, because neighbouring blocks own
+// neighbouring column ranges and sweep the rows in lockstep, the chip streams each client row
+// almost sequentially — the access pattern of a plain linear read.
+template <class P, typename T, int OP, int V, int U, bool NT>
+__global__ __launch_bounds__(kThreads) void reduce_kernel_balanced(
+    const typename P::x_t* __restrict__ stack, int64_t stride, int n,
+    const typename P::w_t* __restrict__ w, int64_t col0, int64_t ncols, Epi<T> e) {
+  const int64_t nquads = (ncols + 3) / 4;
+  const int64_t nchunks = (nquads + 63) / 64;
+  const int64_t b = blockIdx.x, g = gridDim.x;
+  const int64_t per = nchunks / g, extra = nchunks % g;
+  const int64_t c0 = b * per + (b < extra ? b : extra);
+  const int64_t c1 = c0 + per + (b < extra ? 1 : 0);
+  const int64_t qlim = c1 * 64 < nquads ? c1 * 64 : nquads;
+  const typename P::x_t* base = stack + col0;
+  for (int64_t qt = c0 * 64; qt < qlim; qt += kThreads * V)
+    reduce_range_subtile<P, T, OP, V, U, NT>(base, stride, n, w, qt, qlim, ncols, e);
+}
+
+// One sub-tile per block (grid = number of sub-tiles): the simple mapping.
+template <class P, typename T, int OP, int V, int U, bool NT>
+__global__ __launch_bounds__(kThreads) void reduce_kernel(
+    const typename P::x_t* __restrict__ stack, int64_t stride, int n,
+    const typename P::w_t* __restrict__ w, int64_t col0, int64_t ncols, Epi<T> e) {
+  const int64_t qt = (int64_t)blockIdx.x * (kThreads * V);
+  const int64_t nquads = (ncols + 3) / 4;
+  reduce_range_subtile<P, T, OP, V, U, NT>(stack + col0, stride, n, w, qt,
+                                           qt + kThreads * V < nquads ? qt + kThreads * V : nquads,
+                                           ncols, e);
+}
+
+// Standalone update (client_receive form): g read from memory instead of reduced.
+template <typename T, int OP>
+__global__ __launch_bounds__(kThreads) void apply_kernel(const T* __restrict__ glob, int64_t n,
+                                                         Epi<T> e) {
+  const int64_t c = ((int64_t)blockIdx.x * kThreads + threadIdx.x) * 4;
+  if (c >= n) return;
+  const int valid = (int)((n - c) < 4 ? (n - c) : 4);
+  typename vec4<T>::type g = load_quad_guarded(glob + c, valid);
+  finish_quad<T, OP, T>(e, c, valid, g);  // denom == 1: T(g)/1 == g exactly
+}
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+__global__ __launch_bounds__(kThreads) void fill_uniform_kernel(float* __restrict__ dst,
+                                                                int64_t stride, int64_t ncols,
+                                                                uint64_t seed, int64_t row0,
+                                                                int64_t colg0) {
+  const int64_t r = blockIdx.y;
+  const uint64_t key_row = (seed * 0xD1B54A32D192ED03ull) ^ ((uint64_t)(row0 + r) << 40);
+  float* out = dst + r * stride;
+  for (int64_t c = (int64_t)blockIdx.x * kThreads + threadIdx.x; c < ncols;
+       c += (int64_t)gridDim.x * kThreads) {
+    const uint64_t h = splitmix64(key_row ^ (uint64_t)(colg0 + c));
+    out[c] = (float)(h >> 40) * 0x1.0p-23f - 1.0f;
+  }
+}
+
+}  // namespace fa

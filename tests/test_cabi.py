@@ -1,0 +1,115 @@
+"""The C-ABI library loads here (no GPU) and exports exactly what include/flearn_amd.h declares;
+argument validation fails with the documented codes before anything touches a device."""
+import ctypes
+import re
+import subprocess
+from pathlib import Path
+
+import pytest
+
+from flearn_amd import _native as na
+
+HEADER = Path(__file__).resolve().parent.parent / "include" / "flearn_amd.h"
+
+
+def declared_functions():
+    text = HEADER.read_text()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(fa_[a-z0-9_]+)\s*\(", text)))
+
+
+def header_define(name):
+    m = re.search(rf"#define\s+{name}\s+\(?(-?\d+)\)?", HEADER.read_text())
+    return int(m.group(1))
+
+
+@pytest.fixture(scope="module")
+def L():
+    return na.load()
+
+
+def test_header_matches_binding_table():
+    assert declared_functions() == sorted(na.EXPORTS)
+
+
+def test_library_exports_every_declared_symbol(L):
+    for name in declared_functions():
+        assert hasattr(L, name), name
+    out = subprocess.run(["nm", "-D", "--defined-only", str(na.LIB_PATH)], capture_output=True, text=True).stdout
+    exported = set(re.findall(r"\bT\s+(fa_[a-z0-9_]+)$", out, flags=re.M))
+    assert exported == set(declared_functions()), exported ^ set(declared_functions())
+
+
+def test_abi_version_and_constants(L):
+    assert L.fa_abi_version() == header_define("FA_ABI_VERSION") == na.ABI_VERSION
+    assert header_define("FA_MODE_W32_DIV64") == na.MODE_W32_DIV64
+    assert header_define("FA_MODE_W32_DIV32") == na.MODE_W32_DIV32
+    assert header_define("FA_MODE_W64") == na.MODE_W64
+    for op, v in na.OP_BY_NAME.items():
+        assert header_define(f"FA_OP_{op.upper()}") == v
+
+
+def test_epilogue_struct_layout_matches_c(tmp_path):
+    """ctypes' fa_epilogue must have the C compiler's size and field offsets."""
+    src = tmp_path / "layout.c"
+    src.write_text(
+        '#include <stddef.h>\n#include <stdio.h>\n#include "flearn_amd.h"\n'
+        "int main(void){printf(\"%zu %zu %zu %zu %zu %zu %zu %zu %zu\\n\", sizeof(fa_epilogue),"
+        "offsetof(fa_epilogue,op),offsetof(fa_epilogue,reserved),offsetof(fa_epilogue,prev),"
+        "offsetof(fa_epilogue,v),offsetof(fa_epilogue,beta),offsetof(fa_epilogue,eta),"
+        "offsetof(fa_epilogue,tau),offsetof(fa_epilogue,beta2));return 0;}\n"
+    )
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-I", str(HEADER.parent), str(src), "-o", str(exe)], check=True)
+    c = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True).stdout.split()]
+    E = na.Epilogue
+    py = [ctypes.sizeof(E)] + [getattr(E, f).offset for f in ("op", "reserved", "prev", "v", "beta", "eta", "tau", "beta2")]
+    assert c == py
+
+
+FAKE = 0x100000  # never dereferenced: validation rejects the call first
+
+
+def test_reduce_rejects_bad_arguments(L):
+    rc = L.fa_reduce_f32(FAKE, 64, 0, 0, FAKE, 1.0, 0, 64, None, FAKE, None, None)
+    assert rc == header_define("FA_ERR_ARG")
+    assert b"n_clients" in L.fa_last_error()
+    rc = L.fa_reduce_f32(None, 64, 2, 0, FAKE, 1.0, 0, 64, None, FAKE, None, None)
+    assert rc == header_define("FA_ERR_ARG")
+    rc = L.fa_reduce_f32(FAKE, 64, 2, 0, FAKE, 1.0, 0, 64, None, None, None, None)
+    assert rc == header_define("FA_ERR_ARG") and b"output" in L.fa_last_error()
+    rc = L.fa_reduce_f32(FAKE, 64, 2, 0, FAKE, 1.0, 10, 60, None, FAKE, None, None)  # window > stride
+    assert rc == header_define("FA_ERR_ARG")
+
+
+def test_reduce_rejects_misaligned_windows(L):
+    err_align = header_define("FA_ERR_ALIGN")
+    assert L.fa_reduce_f32(FAKE, 64, 2, 0, FAKE, 1.0, 1, 8, None, FAKE, None, None) == err_align
+    assert L.fa_reduce_f32(FAKE, 66, 2, 0, FAKE, 1.0, 0, 8, None, FAKE, None, None) == err_align
+    assert L.fa_reduce_f32(FAKE + 4, 64, 2, 0, FAKE, 1.0, 0, 8, None, FAKE, None, None) == err_align
+    assert L.fa_reduce_f32(FAKE, 64, 2, 0, FAKE, 1.0, 0, 8, None, FAKE + 4, None, None) == err_align
+    assert L.fa_reduce_f32(FAKE, 64, 2, 0, FAKE, 1.0, 0, 8, None, None, FAKE + 8, None) == err_align
+
+
+def test_unknown_mode_and_op(L):
+    assert L.fa_reduce_f32(FAKE, 64, 2, 7, FAKE, 1.0, 0, 8, None, FAKE, None, None) == header_define("FA_ERR_ARG")
+    epi = na.Epilogue(9, 0, FAKE, FAKE, 0.9, 0.1, 1e-9, 0.99)
+    rc = L.fa_reduce_f32(FAKE, 64, 2, 0, FAKE, 1.0, 0, 8, ctypes.byref(epi), FAKE, None, None)
+    assert rc == header_define("FA_ERR_ARG")
+    epi = na.Epilogue(na.OP_AVGM, 0, None, None, 0.9, 0.1, 1e-9, 0.99)  # op without state
+    rc = L.fa_reduce_f32(FAKE, 64, 2, 0, FAKE, 1.0, 0, 8, ctypes.byref(epi), FAKE, None, None)
+    assert rc == header_define("FA_ERR_ARG")
+
+
+def test_empty_window_is_a_no_op(L):
+    assert L.fa_reduce_f32(FAKE, 64, 2, 0, FAKE, 1.0, 0, 0, None, FAKE, None, None) == 0
+    assert L.fa_reduce_f64(FAKE, 64, 2, FAKE, 1.0, 0, 0, FAKE, None) == 0
+    assert L.fa_reduce_i64(FAKE, 64, 2, FAKE, 1.0, 0, 0, FAKE, None) == 0
+
+
+def test_apply_and_fill_validation(L):
+    epi = na.Epilogue(na.OP_MEAN, 0, None, FAKE, 0.9, 0.1, 1e-9, 0.99)
+    assert L.fa_opt_apply(na.PREC_F64, ctypes.byref(epi), FAKE, FAKE, 8, FAKE, None, None) == header_define("FA_ERR_ARG")
+    assert L.fa_opt_apply(na.PREC_F64, None, FAKE, FAKE, 8, FAKE, None, None) == header_define("FA_ERR_ARG")
+    assert L.fa_fill_uniform_f32(FAKE, 64, 70000, 64, 1, 0, 0, None) == header_define("FA_ERR_ARG")
+    assert L.fa_fill_uniform_f32(FAKE, 8, 1, 64, 1, 0, 0, None) == header_define("FA_ERR_ARG")

@@ -164,6 +164,39 @@ def test_reduce_kernel_bit_exact(n, ncols, cuda):
     assert bitwise_equal(out32.cpu().numpy(), want.astype(np.float32))
 
 
+@pytest.mark.parametrize("n,ncols", [(3, 8388608), (5, 8388608 + 1), (2, 8388608 + 63), (9, 9000003)])
+def test_reduce_kernel_big_tiles_ragged(n, ncols, cuda):
+    """Buckets large enough for the one-tile-per-block 64-KiB geometry, with ragged ends."""
+    stride = -(-ncols // 64) * 64
+    x = _device_stack(n, stride, seed=ncols)
+    w32 = np.linspace(0.5, 2.0, n).astype(np.float32)
+    denom = float(np.sum([float(v) for v in w32]))
+    out64 = torch.empty(ncols, dtype=torch.float64, device=cuda)
+    agg.reduce_stack(x, torch.from_numpy(w32).to(cuda), na.MODE_W32_DIV64, denom, n_cols=ncols, out64=out64)
+    want = oracle.c_reduce(oracle.MODE_W32_DIV64, x[:, :ncols].cpu().numpy(), w32, denom)
+    assert bitwise_equal(out64.cpu().numpy(), want)
+
+
+@pytest.mark.parametrize("op", ["avgm", "adagrad"])
+def test_fused_epilogue_big_tiles(op, cuda):
+    n, p = 4, 8388608 + 5
+    stride = -(-p // 64) * 64
+    x = _device_stack(n, stride, seed=21)
+    w = np.ones(n, np.float32)
+    prev = torch.empty((1, stride), dtype=torch.float32, device=cuda)
+    agg.fill_uniform(prev, seed=5)
+    prev_h = prev[0, :p].cpu().numpy().copy()
+    v = torch.full((p,), 0.25, dtype=torch.float64, device=cuda)
+    v_h = v.cpu().numpy().copy()
+    out64 = torch.empty(p, dtype=torch.float64, device=cuda)
+    agg.reduce_stack(x, torch.from_numpy(w).to(cuda), na.MODE_W32_DIV64, float(n), n_cols=p, out64=out64,
+                     op=na.OP_BY_NAME[op], prev=prev[0], v=v)
+    g = oracle.c_reduce(oracle.MODE_W32_DIV64, x[:, :p].cpu().numpy(), w, float(n))
+    want = oracle.c_update(op, g, prev_h, v_h)
+    assert bitwise_equal(out64.cpu().numpy(), want)
+    assert bitwise_equal(v.cpu().numpy(), v_h)
+
+
 @pytest.mark.parametrize("col_begin", [0, 4, 64, 1000, 4096])
 def test_column_window(col_begin, cuda):
     """A window [col_begin, +n) equals the same columns of the full reduce (sharding property)."""

@@ -1,0 +1,202 @@
+"""Host-side logic of the aggregation boundary (no GPU): numpy-semantics resolution, bucket
+planning, the Strategy registry and conversions, the multi-GPU shard plan, and that the product
+path refuses to run without its HIP library / GPU instead of falling back to the CPU."""
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+import flearn_amd
+from flearn_amd import _native as na
+from flearn_amd import layouts
+from flearn_amd.bucket import ALIGN, make_plan, select_keys
+from flearn_amd.dist import ShardPlan
+from flearn_amd.semantics import KIND_F32, KIND_F64, KIND_I64, resolve
+
+WEIGHT_SETS = {
+    "pyfloat": [1.0, 2.5, 0.25],
+    "pyint": [3, 1, 600],
+    "pybool": [True, True, False],
+    "np32": [np.float32(1.5), np.float32(0.5), np.float32(2)],
+    "np64": [np.float64(1.5), np.float64(0.5), np.float64(2)],
+    "npint64": [np.int64(3), np.int64(1), np.int64(2)],
+    "np16": [np.float16(1.5), np.float16(0.5), np.float16(2)],
+    "mixed_float_int": [1.0, 2, 3],
+}
+
+
+@pytest.mark.parametrize("wname", sorted(WEIGHT_SETS))
+@pytest.mark.parametrize("xdtype", [np.float32, np.float64, np.int64])
+def test_resolve_agrees_with_numpy(wname, xdtype):
+    """resolve() must predict exactly the dtypes numpy gives strategy.py:123-129."""
+    ws = WEIGHT_SETS[wname]
+    if len({np.result_type(w, xdtype) for w in ws}) > 1:
+        with pytest.raises(TypeError):  # per-client precisions differ: rejected, not guessed
+            resolve(ws, xdtype)
+        return
+    xs = [np.array([1, 2, 3], dtype=xdtype) for _ in ws]
+    acc = ws[0] * xs[0]
+    for a, x in zip(ws[1:], xs[1:]):
+        acc = acc + a * x
+    with np.errstate(all="ignore"):
+        out = np.divide(acc, np.sum(ws))
+    nm = resolve(ws, xdtype)
+    assert nm.acc_dtype == acc.dtype
+    assert nm.out_dtype == out.dtype
+    assert nm.weights.dtype == nm.acc_dtype
+    assert nm.denom == float(np.sum(ws))
+    expected_kind = KIND_F32 if xdtype == np.float32 else (KIND_I64 if acc.dtype == np.int64 else KIND_F64)
+    assert nm.kind == expected_kind
+    if nm.kind == KIND_F32:
+        want_mode = {(np.float32, np.float64): na.MODE_W32_DIV64, (np.float32, np.float32): na.MODE_W32_DIV32,
+                     (np.float64, np.float64): na.MODE_W64}[(acc.dtype.type, out.dtype.type)]
+        assert nm.mode == want_mode
+
+
+def test_resolve_rejects_mixed_promotion_and_bad_inputs():
+    with pytest.raises(TypeError):
+        resolve([1.0, np.float64(2.0)], np.float32)  # fp32 and f64 products in one sum
+    with pytest.raises(TypeError):
+        resolve([1.0, "x"], np.float32)
+    with pytest.raises(TypeError):
+        resolve([1.0], np.float16)
+    with pytest.raises(IndexError):
+        resolve([], np.float32)
+
+
+def test_weight_cast_is_numpys():
+    big = 2**24 + 1  # not representable in fp32: numpy rounds it to even
+    nm = resolve([big, 1], np.float32)
+    assert nm.weights[0] == np.float32(big) == (big * np.ones(1, np.float32))[0]
+
+
+def _clients(n=3):
+    out = []
+    for i in range(n):
+        out.append({
+            "conv.weight": np.full((4, 3, 3, 3), i, np.float32),
+            "bn.running_mean": np.full((4,), i, np.float32),
+            "bn.num_batches_tracked": np.array(10 + i, np.int64),
+            "fc.weight": np.full((10, 37), i, np.float32),
+            "fc.bias": np.full((10,), i, np.float32),
+        })
+    return out
+
+
+def test_plan_layout_and_groups():
+    cl = _clients()
+    plan = make_plan([1.0, 1.0, 1.0], cl)
+    assert plan.keys == list(cl[0].keys())
+    f32 = plan.groups[KIND_F32]
+    assert [s.key for s in f32.segments] == ["conv.weight", "bn.running_mean", "fc.weight", "fc.bias"]
+    for s in f32.segments:
+        assert s.offset % ALIGN == 0
+    assert f32.stride % ALIGN == 0 and f32.stride >= sum(s.numel for s in f32.segments)
+    assert plan.key_group["bn.num_batches_tracked"] == KIND_F64  # int64 x Python float -> f64
+    plan_i = make_plan([1, 2, 3], cl)
+    assert plan_i.key_group["bn.num_batches_tracked"] == KIND_I64  # int64 x Python int stays int
+
+
+def test_plan_key_selection_and_errors():
+    cl = _clients()
+    del cl[1]["fc.bias"]
+    assert "fc.bias" not in select_keys(cl)  # intersection, strategy.py:119-121
+    with pytest.raises(KeyError):
+        make_plan([1.0] * 3, cl, key_lst=["fc.bias"])
+    cl = _clients()
+    cl[2]["fc.weight"] = np.zeros((37, 10), np.float32)
+    with pytest.raises(ValueError):
+        make_plan([1.0] * 3, cl)
+    cl = _clients()
+    cl[1]["fc.bias"] = cl[1]["fc.bias"].astype(np.float64)
+    with pytest.raises(ValueError):
+        make_plan([1.0] * 3, cl)
+    with pytest.raises(IndexError):
+        make_plan([], [])
+    cl = _clients(2)
+    cl[1] = {k: torch.from_numpy(np.asarray(v)) for k, v in cl[1].items()}
+    with pytest.raises(TypeError):
+        make_plan([1.0, 1.0], cl)
+
+
+def test_layouts_match_survey_counts():
+    assert layouts.fp32_elems(layouts.get("lenet5")) == 44_426
+    assert layouts.fp32_elems(layouts.get("resnet18")) == 11_699_112
+    assert layouts.fp32_tensors(layouts.get("resnet18")) == 102
+    assert layouts.fp32_elems(layouts.get("resnet50")) == 25_610_152
+    assert layouts.fp32_tensors(layouts.get("resnet50")) == 267
+    assert layouts.fp32_elems(layouts.get("vit_b_16")) == 86_567_656
+    assert layouts.fp32_tensors(layouts.get("vit_b_16")) == 152
+
+
+def test_registry_mirrors_reference():
+    assert type(flearn_amd.setup_strategy("avg", None)).__name__ == "AVG"
+    assert type(flearn_amd.setup_strategy("AVGM", None)).__name__ == "AVGM"
+    s = flearn_amd.setup_strategy("lg", None, shared_key_layers=["fc.weight"])
+    assert s.shared_key_layers == ["fc.weight"]
+    assert flearn_amd.setup_strategy("opt", None, server_side=True).server_side
+    custom = object()
+    assert flearn_amd.setup_strategy("mystrategy", custom) is custom
+    with pytest.raises(SystemError):
+        flearn_amd.setup_strategy("nope", None)
+    for name in ("dyn", "md", "pav", "distill"):
+        with pytest.raises(NotImplementedError):
+            flearn_amd.setup_strategy(name, None)
+
+
+def test_conversions_mirror_reference():
+    d = {"a": torch.ones(3), "b": [1, 2], "c": np.zeros(2)}
+    out = flearn_amd.convert_to_np(d)
+    assert out is d and all(isinstance(v, np.ndarray) for v in d.values())
+    flearn_amd.convert_to_tensor(d)
+    assert all(isinstance(v, torch.Tensor) for v in d.values())
+    with pytest.raises(SystemError):
+        flearn_amd.convert_to_tensor({"n": np.float64(3.0)})  # the 0-d buffer quirk (avg.py:41)
+    with pytest.raises(SystemError):
+        flearn_amd.convert_to_np({"n": 3.0})
+
+
+def test_client_upload_matches_reference_contract():
+    class T:
+        @property
+        def weight(self):
+            return {"w": torch.ones(2, 2), "bn.x": torch.zeros(2)}
+
+    up = flearn_amd.AVG().client(T())
+    assert up["agg_weight"] == 1.0 and isinstance(up["params"]["w"], np.ndarray)
+    up = flearn_amd.BN().client(T(), agg_weight=3)
+    assert list(up["params"]) == ["w"] and up["agg_weight"] == 3
+
+
+@pytest.mark.skipif(torch.cuda.is_available(), reason="checks the no-GPU behaviour")
+def test_product_path_fails_loudly_without_gpu():
+    """No CPU fallback: the server path raises NativeUnavailable (never a silent numpy result)."""
+    ups = [{"agg_weight": 1.0, "params": {"w": np.ones(4, np.float32)}}]
+    with pytest.raises(na.NativeUnavailable):
+        flearn_amd.AVG().server(ups, 0)
+
+
+def test_product_never_imports_the_oracle():
+    code = "import sys, flearn_amd, flearn_amd.aggregator, flearn_amd.dist; print('oracle' in sys.modules)"
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True,
+                         cwd=str(layouts.__file__).rsplit("/flearn_amd/", 1)[0])
+    assert out.stdout.strip() == "False", out.stderr
+    import pathlib
+
+    for f in pathlib.Path(flearn_amd.__file__).parent.rglob("*.py"):
+        assert "import oracle" not in f.read_text(), f
+
+
+@pytest.mark.parametrize("n_cols,world,stripes", [(1, 1, 1), (11_699_112, 8, 4), (44_426, 2, 3), (1000, 4, 4)])
+def test_shard_plan_covers_columns_once(n_cols, world, stripes):
+    seen = np.zeros(ShardPlan.make(n_cols, world, 0, stripes).padded, dtype=np.int32)
+    for r in range(world):
+        p = ShardPlan.make(n_cols, world, r, stripes)
+        assert p.shard % 64 == 0
+        for c in range(stripes):
+            g0 = p.global_begin(c)
+            seen[g0 : g0 + p.shard] += 1
+            assert p.local_to_global(p.local_begin(c)) == g0
+    assert (seen == 1).all()

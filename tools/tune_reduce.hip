@@ -1,0 +1,220 @@
+// tune_reduce.hip — geometry sweep of the fused reduce kernel on the MI355X.
+//
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -Iinclude -Iflearn_amd/csrc \
+//         tools/tune_reduce.hip -o tools/tune_reduce
+//   tools/tune_reduce [n_clients=100] [n_cols=11699136] [rounds=7] [op=mean|avgm]
+//
+// Times every variant (quads/thread V, client unroll U, non-temporal loads, one-shot vs
+// persistent grid) with hipEvents in interleaved rounds (one process, same data), checks each
+// variant's output bitwise against the first, and brackets them with two roofs measured on the
+// same buffers: a pure streaming read of the N x P stack and a float4 copy.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <functional>
+#include <string>
+#include <vector>
+
+#include "fa_device.hpp"
+
+#define CK(x)                                                                        \
+  do {                                                                               \
+    hipError_t e_ = (x);                                                             \
+    if (e_ != hipSuccess) {                                                          \
+      fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
+      exit(1);                                                                       \
+    }                                                                                \
+  } while (0)
+
+using namespace fa;
+
+// read roof: stream the whole stack once, 16-B loads, keep the data alive with one store/thread
+__global__ __launch_bounds__(256) void read_roof(const float* __restrict__ x, int64_t quads,
+                                                 float* __restrict__ sink) {
+  typedef vec4<float>::type f4;
+  f4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < quads; q += (int64_t)gridDim.x * 256) {
+    f4 v = __builtin_nontemporal_load(reinterpret_cast<const f4*>(x) + q);
+    acc += v;
+  }
+  if (acc[0] + acc[1] + acc[2] + acc[3] == 12345.678f) sink[threadIdx.x] = acc[0];
+}
+
+__global__ __launch_bounds__(256) void copy_roof(const float* __restrict__ x, float* __restrict__ y,
+                                                 int64_t quads) {
+  typedef vec4<float>::type f4;
+  for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < quads; q += (int64_t)gridDim.x * 256)
+    reinterpret_cast<f4*>(y)[q] = reinterpret_cast<const f4*>(x)[q];
+}
+
+struct Variant {
+  std::string name;
+  double bytes;
+  std::function<void()> launch;
+  bool checks_output;
+  std::vector<float> times;
+};
+
+template <int V, int U, bool NT, int OP, typename T>
+Variant make_oneshot(const float* stack, int64_t stride, int n, const float* w, int64_t ncols,
+                     Epi<T> e, double bytes) {
+  const int64_t tiles = (ncols + 256 * V * 4 - 1) / (256 * V * 4);
+  char name[96];
+  snprintf(name, sizeof name, "oneshot V%d U%d NT%d", V, U, (int)NT);
+  return {name, bytes,
+          [=] {
+            hipLaunchKernelGGL((reduce_kernel<AccF32, T, OP, V, U, NT>), dim3((unsigned)tiles), dim3(256), 0,
+                               0, stack, stride, n, w, (int64_t)0, ncols, e);
+          },
+          true, {}};
+}
+
+// rounds_extra: grid = (k + rounds_extra) * CUs * occupancy, k = the fewest rounds for which
+// every block's share fits one sub-tile
+template <int V, int U, bool NT, int OP, typename T>
+Variant make_balanced(const float* stack, int64_t stride, int n, const float* w, int64_t ncols,
+                      Epi<T> e, double bytes, int cus, int rounds_extra) {
+  int occ = 0;
+  CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, reduce_kernel_balanced<AccF32, T, OP, V, U, NT>,
+                                                  256, 0));
+  const int64_t slots = (int64_t)cus * occ;
+  const int64_t chunks = ((ncols + 3) / 4 + 63) / 64;
+  const int64_t k = (chunks + slots * 4 * V - 1) / (slots * 4 * V) + rounds_extra;
+  const int grid = (int)std::min<int64_t>(std::max<int64_t>(1, k * slots), chunks);
+  char name[96];
+  snprintf(name, sizeof name, "balanced V%d U%d occ%d g%d", V, U, occ, grid);
+  return {name, bytes,
+          [=] {
+            hipLaunchKernelGGL((reduce_kernel_balanced<AccF32, T, OP, V, U, NT>), dim3(grid), dim3(256), 0, 0,
+                               stack, stride, n, w, (int64_t)0, ncols, e);
+          },
+          true, {}};
+}
+
+int main(int argc, char** argv) {
+  const int n = argc > 1 ? atoi(argv[1]) : 100;
+  const int64_t ncols = argc > 2 ? atoll(argv[2]) : 11699136;
+  const int rounds = argc > 3 ? atoi(argv[3]) : 7;
+  const char* opname = argc > 4 ? argv[4] : "mean";
+  const int op = !strcmp(opname, "avgm") ? FA_OP_AVGM : !strcmp(opname, "adagrad") ? FA_OP_ADAGRAD : FA_OP_MEAN;
+  const bool avgm = op != FA_OP_MEAN;  // any fused epilogue
+  const int64_t pad = argc > 5 ? atoll(argv[5]) : 0;  // extra row-stride elements (bank-conflict probe)
+  const int64_t stride = (ncols + 63) / 64 * 64 + pad;
+
+  hipDeviceProp_t prop;
+  CK(hipGetDeviceProperties(&prop, 0));
+  printf("# device %s  CUs %d  n=%d ncols=%lld op=%s stride=%lld\n", prop.gcnArchName,
+         prop.multiProcessorCount, n, (long long)ncols, opname, (long long)stride);
+
+  float *stack, *w, *out32, *prev, *sink, *copy_dst;
+  double* v;
+  CK(hipMalloc(&stack, (size_t)n * stride * 4));
+  CK(hipMalloc(&w, n * 4));
+  CK(hipMalloc(&out32, stride * 4));
+  CK(hipMalloc(&prev, stride * 4));
+  CK(hipMalloc(&v, stride * 8));
+  CK(hipMalloc(&sink, 4096));
+  const int64_t copy_quads = (int64_t)n * stride / 8;  // copy half the stack into the other half
+  copy_dst = stack + copy_quads * 4;
+  hipLaunchKernelGGL(fill_uniform_kernel, dim3(4096, n), dim3(256), 0, 0, stack, stride, stride, 2024ull,
+                     (int64_t)0, (int64_t)0);
+  hipLaunchKernelGGL(fill_uniform_kernel, dim3(4096, 1), dim3(256), 0, 0, prev, stride, stride, 1ull,
+                     (int64_t)0, (int64_t)0);
+  std::vector<float> ones(n, 1.0f);
+  CK(hipMemcpy(w, ones.data(), n * 4, hipMemcpyHostToDevice));
+  CK(hipMemset(v, 0, stride * 8));
+  CK(hipDeviceSynchronize());
+
+  Epi<double> e{};
+  e.denom = (double)n;
+  e.out32 = out32;
+  e.beta = 0.9;
+  e.eta = 0.1;
+  e.tau = 1e-9;
+  if (avgm) {
+    e.prev = prev;
+    e.v = v;
+  }
+  const double bytes = (double)n * ncols * 4 + ncols * 4 + (avgm ? ncols * (4.0 + 16.0) : 0.0);
+
+  std::vector<Variant> vs;
+  const int cus = prop.multiProcessorCount;
+#define ONESHOT(V, U, NT)                                                                             \
+  vs.push_back(op == FA_OP_AVGM      ? make_oneshot<V, U, NT, FA_OP_AVGM, double>(stack, stride, n, w, ncols, e, bytes) \
+               : op == FA_OP_ADAGRAD ? make_oneshot<V, U, NT, FA_OP_ADAGRAD, double>(stack, stride, n, w, ncols, e, bytes) \
+                                     : make_oneshot<V, U, NT, FA_OP_MEAN, double>(stack, stride, n, w, ncols, e, bytes))
+#define BAL(V, U, G4)                                                                                     \
+  vs.push_back(op == FA_OP_AVGM      ? make_balanced<V, U, true, FA_OP_AVGM, double>(stack, stride, n, w, ncols, e, bytes, cus, G4) \
+               : op == FA_OP_ADAGRAD ? make_balanced<V, U, true, FA_OP_ADAGRAD, double>(stack, stride, n, w, ncols, e, bytes, cus, G4) \
+                                     : make_balanced<V, U, true, FA_OP_MEAN, double>(stack, stride, n, w, ncols, e, bytes, cus, G4))
+  const char* set = getenv("TUNE_SET") ? getenv("TUNE_SET") : "main";
+  ONESHOT(2, 8, true);  // previous product geometry first: the bitwise reference for the others
+  ONESHOT(8, 4, true);
+  if (!strcmp(set, "main")) {
+    ONESHOT(4, 1, true);
+    ONESHOT(8, 1, true);
+    ONESHOT(16, 1, true);
+    BAL(4, 1, 0);
+    BAL(4, 1, 1);
+    BAL(8, 1, 0);
+    BAL(8, 1, 1);
+    BAL(16, 1, 0);
+    BAL(16, 1, 1);
+    BAL(4, 4, 0);
+    BAL(8, 2, 0);
+  }
+  const int64_t quads = (int64_t)n * stride / 4;
+  vs.push_back({"roof: stream read N*P", (double)n * stride * 4,
+                [=] { hipLaunchKernelGGL(read_roof, dim3(cus * 8), dim3(256), 0, 0, stack, quads, sink); },
+                false, {}});
+  vs.push_back({"roof: float4 copy (R+W)", (double)copy_quads * 32,
+                [=] {
+                  hipLaunchKernelGGL(copy_roof, dim3(cus * 8), dim3(256), 0, 0, stack, copy_dst, copy_quads);
+                },
+                false, {}});
+
+  // reference output of the product geometry
+  std::vector<float> ref(ncols), got(ncols);
+  std::vector<double> v_save;
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a));
+  CK(hipEventCreate(&b));
+  // warm up + correctness (state-free for mean; for avgm reset v before each checked launch)
+  for (size_t i = 0; i < vs.size(); ++i) {
+    if (!vs[i].checks_output) continue;
+    CK(hipMemset(v, 0, stride * 8));
+    vs[i].launch();
+    CK(hipDeviceSynchronize());
+    CK(hipMemcpy(i == 0 ? ref.data() : got.data(), out32, ncols * 4, hipMemcpyDeviceToHost));
+    if (i > 0 && memcmp(ref.data(), got.data(), ncols * 4) != 0) {
+      printf("MISMATCH %s\n", vs[i].name.c_str());
+      return 2;
+    }
+  }
+  // copy_roof overwrites the second half of the stack: run the roofs after the checks, and the
+  // reduce variants only read, so timings stay valid.
+  for (int r = 0; r < rounds; ++r) {
+    for (auto& var : vs) {
+      var.launch();  // warm
+      CK(hipEventRecord(a, 0));
+      const int reps = 5;
+      for (int k = 0; k < reps; ++k) var.launch();
+      CK(hipEventRecord(b, 0));
+      CK(hipEventSynchronize(b));
+      float ms;
+      CK(hipEventElapsedTime(&ms, a, b));
+      var.times.push_back(ms / reps);
+    }
+  }
+  printf("%-28s %10s %10s %10s %8s\n", "variant", "med_us", "min_us", "GB/s(med)", "%8TB/s");
+  for (auto& var : vs) {
+    std::sort(var.times.begin(), var.times.end());
+    const double med = var.times[var.times.size() / 2], mn = var.times[0];
+    const double gbs = var.bytes / 1e9 / (med / 1e3);
+    printf("%-28s %10.1f %10.1f %10.1f %8.2f\n", var.name.c_str(), med * 1e3, mn * 1e3, gbs, gbs / 80.0);
+  }
+  return 0;
+}
