@@ -66,6 +66,16 @@ def algorithmic_bytes(n_clients: int, cols: int, op: str) -> int:
     return b
 
 
+def host_cpu_name() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.machine()
+
+
 def cpu_baseline(stack: torch.Tensor, layout, n_sample: int, reps: int = 3):
     """flearn's CPU path: the oracle's numpy restatement of Strategy.server_ensemble
     (strategy.py:102-130, bit-exact to the reference by tests/test_oracle_golden.py), timed on
@@ -90,7 +100,7 @@ def cpu_baseline(stack: torch.Tensor, layout, n_sample: int, reps: int = 3):
         "kind": "port",
         "sample": f"{n_sample} clients x full {len(fp32)}-tensor layout ({p} fp32), numpy op-sequence "
                   f"restatement of server_ensemble, best of {reps} ({best:.3f} s); numpy ufuncs are "
-                  f"single-threaded; host {platform.processor() or platform.machine()} nproc={os.cpu_count()}",
+                  f"single-threaded (1 core used); host {host_cpu_name()}, nproc={os.cpu_count()}",
     }
 
 
@@ -108,8 +118,8 @@ def load_traffic(config: str):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--stripes", type=int, default=None, help="reduce/gather pipeline depth (N>1)")
     ap.add_argument("--cpu-sample", type=int, default=None, help="clients in the CPU-baseline sample")

@@ -1,0 +1,91 @@
+"""End-to-end server aggregation through the Strategy API, uploads in host memory.
+
+    python tools/bench_e2e.py [--config c2] [--rounds 5] [--output reference|float32]
+
+flearn's loopback Server hands `Strategy.server` a list of client uploads whose params are host
+numpy arrays (Communicator.py:127-141 -> Server.py:126-140); the result goes back to the clients
+as host arrays.  This times AVG().server(uploads, r) on that input — plan, pack into pinned
+staging, H2D, the fused HIP reduce, D2H, unpack — and splits the time by phase.  It is the
+PCIe-inclusive rate recorded in DESIGN.md, never bench.py's `value`.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+import torch
+
+REPO = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(REPO))
+
+import flearn_amd  # noqa: E402
+from flearn_amd import aggregator as agg  # noqa: E402
+from flearn_amd import layouts  # noqa: E402
+
+CONFIGS = {"c2": ("resnet18", 100), "c3": ("resnet50", 100), "c1": ("lenet5", 10)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--output", default="reference")
+    a = ap.parse_args()
+    name, n = CONFIGS[a.config]
+    layout = layouts.get(name)
+    p = layouts.fp32_elems(layout)
+    dev = torch.device("cuda", 0)
+    x = torch.empty((n, p), dtype=torch.float32, device=dev)
+    agg.fill_uniform(x, seed=2024)
+    host = x.cpu().numpy()  # the clients' uploads live in host memory
+    del x
+    uploads = [{"agg_weight": 1.0, "params": layouts.synthetic_state_dict(layout, host[i], counter=100 + i)}
+               for i in range(n)]
+    s = flearn_amd.AVG(output=a.output)
+    eng = s.engine
+    # phase timers around the engine's own steps
+    t = {"plan_pack_h2d": [], "reduce": [], "d2h_unpack": [], "total": []}
+    orig_pack, orig_finish = eng.packer.pack, eng._finish
+
+    def pack(plan, w):
+        t0 = time.perf_counter()
+        out = orig_pack(plan, w)
+        torch.cuda.synchronize(dev)
+        t["plan_pack_h2d"].append(time.perf_counter() - t0)
+        t["_red0"] = time.perf_counter()
+        return out
+
+    def finish(plan, results):
+        torch.cuda.synchronize(dev)
+        t["reduce"].append(time.perf_counter() - t["_red0"])
+        t0 = time.perf_counter()
+        out = orig_finish(plan, results)
+        t["d2h_unpack"].append(time.perf_counter() - t0)
+        return out
+
+    eng.packer.pack, eng._finish = pack, finish
+    for r in range(a.rounds + 1):
+        t0 = time.perf_counter()
+        w_glob = s.server(uploads, r)["w_glob"]
+        t["total"].append(time.perf_counter() - t0)
+    assert len(w_glob) == len(layout)
+    med = {k: float(np.median(v[1:])) for k, v in t.items() if not k.startswith("_")}
+    in_bytes = n * p * 4
+    out_bytes = p * (8 if a.output == "reference" else 4)
+    res = {
+        "config": a.config, "layout": name, "clients": n, "params": p, "output": a.output,
+        "median_s": {k: round(v, 5) for k, v in med.items()},
+        "e2e_GiB_s_algorithmic": round((in_bytes + out_bytes) / 2**30 / med["total"], 2),
+        "h2d_input_GB": round(in_bytes / 1e9, 3),
+        "pack_h2d_GB_s": round(in_bytes / 1e9 / med["plan_pack_h2d"], 2),
+        "note": "uploads are host numpy views (flearn loopback); first round (pinned-buffer allocation) excluded",
+    }
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
