@@ -187,9 +187,11 @@ enum Part : int {
 };
 
 // One sub-tile of the client stack for this thread: quads q0 + v*kThreads (v < V) of every row,
-// all N rows in list order, then the fused epilogue.  Every slot is predicated with a
-// compile-time-unrollable `if` (a `break` would keep the loops rolled and push the register
-// arrays to scratch).
+// all N rows in list order, then the fused epilogue.
+// kMasked: slots v >= nv are outside this block's range.  Their loads are NOT skipped (an `if`
+// around a load becomes exec-masked control flow and the compiler drains vmcnt at every join,
+// serialising the row's loads); they re-read slot nv-1's address instead — an L1/L2 hit inside
+// the same wave, no extra HBM traffic — and only the final stores are predicated.
 template <class P, typename T, int OP, int V, int U, bool NT, int PART>
 __device__ __forceinline__ void reduce_subtile(const typename P::x_t* __restrict__ base,
                                                int64_t stride, int n,
@@ -199,16 +201,19 @@ __device__ __forceinline__ void reduce_subtile(const typename P::x_t* __restrict
   typedef typename P::acc_t A;
   typedef typename vec4<X>::type XV;
   typedef typename vec4<A>::type AV;
+  // this lane's quad in slot 0, and each slot's offset from it (wave-uniform: nv is uniform)
+  const X* lane = base + q0 * 4;
+  int off[V];
+#pragma unroll
+  for (int v = 0; v < V; ++v) off[v] = ((PART == kFull || v < nv) ? v : nv - 1) * kThreads * 4;
   AV acc[V];
   {
     const typename P::w_t w0 = w[0];
 #pragma unroll
     for (int v = 0; v < V; ++v) {
-      if (PART == kFull || v < nv) {
-        const XV x = load_quad<X, NT>(base + (q0 + (int64_t)v * kThreads) * 4);
+      const XV x = load_quad<X, NT>(lane + off[v]);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[v][j] = P::mul(w0, x[j]);
-      }
+      for (int j = 0; j < 4; ++j) acc[v][j] = P::mul(w0, x[j]);
     }
   }
   int i = 1;
@@ -216,38 +221,106 @@ __device__ __forceinline__ void reduce_subtile(const typename P::x_t* __restrict
     XV x[U][V];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const X* row = base + (int64_t)(i + u) * stride;
+      const X* row = lane + (int64_t)(i + u) * stride;
 #pragma unroll
-      for (int v = 0; v < V; ++v)
-        if (PART == kFull || v < nv) x[u][v] = load_quad<X, NT>(row + (q0 + (int64_t)v * kThreads) * 4);
+      for (int v = 0; v < V; ++v) x[u][v] = load_quad<X, NT>(row + off[v]);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const typename P::w_t wu = w[i + u];
 #pragma unroll
-      for (int v = 0; v < V; ++v) {
-        if (PART == kFull || v < nv) {
+      for (int v = 0; v < V; ++v)
 #pragma unroll
-          for (int j = 0; j < 4; ++j) acc[v][j] = add<A>(acc[v][j], P::mul(wu, x[u][v][j]));
-        }
-      }
+        for (int j = 0; j < 4; ++j) acc[v][j] = add<A>(acc[v][j], P::mul(wu, x[u][v][j]));
     }
   }
   for (; i < n; ++i) {
-    const X* row = base + (int64_t)i * stride;
+    const X* row = lane + (int64_t)i * stride;
     const typename P::w_t wi = w[i];
 #pragma unroll
     for (int v = 0; v < V; ++v) {
-      if (PART == kFull || v < nv) {
-        const XV x = load_quad<X, NT>(row + (q0 + (int64_t)v * kThreads) * 4);
+      const XV x = load_quad<X, NT>(row + off[v]);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[v][j] = add<A>(acc[v][j], P::mul(wi, x[j]));
-      }
+      for (int j = 0; j < 4; ++j) acc[v][j] = add<A>(acc[v][j], P::mul(wi, x[j]));
     }
   }
 #pragma unroll
   for (int v = 0; v < V; ++v)
     if (PART == kFull || v < nv) finish_quad<T, OP, A>(e, (q0 + (int64_t)v * kThreads) * 4, 4, acc[v]);
+}
+
+// Buffer-descriptor form of a sub-tile (4-byte elements).  Per client row the block builds a
+// buffer resource whose base is the row's first quad of this sub-tile and whose num_records is
+// the sub-tile's valid byte count; lane offsets (VGPR) are the same for every row and slot v's
+// 4-KiB step rides in soffset.  Slots past the valid range are dropped by the hardware range
+// check (they return 0, generate no memory request and need no branch), so a partial sub-tile
+// issues exactly the loads of its valid quads with the same instruction stream as a full one.
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+
+template <bool NT>
+__device__ __forceinline__ vec4<float>::type buf_load_quad(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+  const u32x4 u = __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, NT ? 2 : 0);
+  return __builtin_bit_cast(vec4<float>::type, u);
+}
+
+template <class P, typename T, int OP, int V, int U, bool NT>
+__device__ __forceinline__ void reduce_subtile_buf(const float* __restrict__ base, int64_t stride,
+                                                   int n, const typename P::w_t* __restrict__ w,
+                                                   int64_t qt, int nvalid_quads, const Epi<T>& e) {
+  typedef typename P::acc_t A;
+  typedef typename vec4<float>::type XV;
+  typedef typename vec4<A>::type AV;
+  const char* tile0 = reinterpret_cast<const char*>(base + qt * 4);
+  const uint32_t bytes = (uint32_t)nvalid_quads * 16u;
+  const int64_t row_bytes = stride * 4;
+  const int voff = (int)threadIdx.x * 16;
+  AV acc[V];
+  {
+    const __amdgpu_buffer_rsrc_t r = row_rsrc(tile0, bytes);
+    const typename P::w_t w0 = w[0];
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      const XV x = buf_load_quad<NT>(r, voff, v * kThreads * 16);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[v][j] = P::mul(w0, x[j]);
+    }
+  }
+  int i = 1;
+  for (; i + U <= n; i += U) {
+    XV x[U][V];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const __amdgpu_buffer_rsrc_t r = row_rsrc(tile0 + (int64_t)(i + u) * row_bytes, bytes);
+#pragma unroll
+      for (int v = 0; v < V; ++v) x[u][v] = buf_load_quad<NT>(r, voff, v * kThreads * 16);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const typename P::w_t wu = w[i + u];
+#pragma unroll
+      for (int v = 0; v < V; ++v)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[v][j] = add<A>(acc[v][j], P::mul(wu, x[u][v][j]));
+    }
+  }
+  for (; i < n; ++i) {
+    const __amdgpu_buffer_rsrc_t r = row_rsrc(tile0 + (int64_t)i * row_bytes, bytes);
+    const typename P::w_t wi = w[i];
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      const XV x = buf_load_quad<NT>(r, voff, v * kThreads * 16);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[v][j] = add<A>(acc[v][j], P::mul(wi, x[j]));
+    }
+  }
+#pragma unroll
+  for (int v = 0; v < V; ++v)
+    if (v * kThreads + (int)threadIdx.x < nvalid_quads)
+      finish_quad<T, OP, A>(e, (qt + (int64_t)v * kThreads + threadIdx.x) * 4, 4, acc[v]);
 }
 
 // The window's ragged end (at most one wave per launch): one quad at a time, element-guarded.
@@ -281,7 +354,7 @@ __device__ __attribute__((noinline)) void reduce_ragged(const typename P::x_t* _
 }
 
 // Sub-tile starting at quad qt, limited to quads < qlim (the block's range, <= the window).
-template <class P, typename T, int OP, int V, int U, bool NT>
+template <class P, typename T, int OP, int V, int U, bool NT, bool BUF = false>
 __device__ __forceinline__ void reduce_range_subtile(const typename P::x_t* __restrict__ base,
                                                      int64_t stride, int n,
                                                      const typename P::w_t* __restrict__ w,
@@ -290,6 +363,16 @@ __device__ __forceinline__ void reduce_range_subtile(const typename P::x_t* __re
   constexpr int kSub = kThreads * V;
   const int64_t q0 = qt + threadIdx.x;
   const int64_t qfull = ncols / 4;  // complete quads in the window
+  if constexpr (BUF) {
+    static_assert(sizeof(typename P::x_t) == 4, "buffer path is for 4-byte elements");
+    const int64_t end = qt + kSub < qlim ? qt + kSub : qlim;  // this sub-tile's quads [qt, end)
+    const int64_t full_end = end < qfull ? end : qfull;
+    if (full_end > qt) reduce_subtile_buf<P, T, OP, V, U, NT>(base, stride, n, w, qt, (int)(full_end - qt), e);
+    // the window's ragged last quad (ncols % 4 != 0), if it falls in this sub-tile
+    if (qfull < end && qfull >= qt && q0 == qt + (qfull - qt) % kThreads)
+      reduce_ragged<P, T, OP>(base, stride, n, w, qfull, qfull + 1, ncols, e);
+    return;
+  }
   if (qt + kSub <= qlim && qt + kSub <= qfull) {
     reduce_subtile<P, T, OP, V, U, NT, kFull>(base, stride, n, w, q0, V, e);
     return;
@@ -312,7 +395,7 @@ __device__ __forceinline__ void reduce_range_subtile(const typename P::x_t* __re
 // blocks of a round finish together (no tail of late blocks) and, because neighbouring blocks own
 // neighbouring column ranges and sweep the rows in lockstep, the chip streams each client row
 // almost sequentially — the access pattern of a plain linear read.
-template <class P, typename T, int OP, int V, int U, bool NT>
+template <class P, typename T, int OP, int V, int U, bool NT, bool BUF = false>
 __global__ __launch_bounds__(kThreads) void reduce_kernel_balanced(
     const typename P::x_t* __restrict__ stack, int64_t stride, int n,
     const typename P::w_t* __restrict__ w, int64_t col0, int64_t ncols, Epi<T> e) {
@@ -325,17 +408,17 @@ __global__ __launch_bounds__(kThreads) void reduce_kernel_balanced(
   const int64_t qlim = c1 * 64 < nquads ? c1 * 64 : nquads;
   const typename P::x_t* base = stack + col0;
   for (int64_t qt = c0 * 64; qt < qlim; qt += kThreads * V)
-    reduce_range_subtile<P, T, OP, V, U, NT>(base, stride, n, w, qt, qlim, ncols, e);
+    reduce_range_subtile<P, T, OP, V, U, NT, BUF>(base, stride, n, w, qt, qlim, ncols, e);
 }
 
 // One sub-tile per block (grid = number of sub-tiles): the simple mapping.
-template <class P, typename T, int OP, int V, int U, bool NT>
+template <class P, typename T, int OP, int V, int U, bool NT, bool BUF = false>
 __global__ __launch_bounds__(kThreads) void reduce_kernel(
     const typename P::x_t* __restrict__ stack, int64_t stride, int n,
     const typename P::w_t* __restrict__ w, int64_t col0, int64_t ncols, Epi<T> e) {
   const int64_t qt = (int64_t)blockIdx.x * (kThreads * V);
   const int64_t nquads = (ncols + 3) / 4;
-  reduce_range_subtile<P, T, OP, V, U, NT>(stack + col0, stride, n, w, qt,
+  reduce_range_subtile<P, T, OP, V, U, NT, BUF>(stack + col0, stride, n, w, qt,
                                            qt + kThreads * V < nquads ? qt + kThreads * V : nquads,
                                            ncols, e);
 }

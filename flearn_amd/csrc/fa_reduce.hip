@@ -5,6 +5,8 @@
 // Geometry (measured with tools/tune_reduce.hip on MI355X, see DESIGN.md "Kernel geometry"):
 //   * large buckets: one 64-KiB-per-row tile per block (16 quads per thread, one client row at a
 //     time): neighbouring blocks sweep each client row almost sequentially, like a linear read;
+//     rows are read through per-row buffer descriptors (lane offset in a VGPR, slot step in
+//     soffset, range-checked partial tiles);
 //     if that grid's last round of resident blocks would be < 85% full, the same tiles are
 //     spread evenly over whole rounds (balanced grid) instead;
 //   * buckets too small to give every CU two such tiles: the round-balanced grid (4 quads per
@@ -36,16 +38,19 @@ int fail(int code, const char* what) {
 constexpr bool kNT = true;  // client bytes are read once: non-temporal
 
 template <class P>
-struct Geometry {  // fp32 buckets
+struct Geometry {  // fp32 buckets: big tiles read through per-row buffer descriptors
   static constexpr int kBigV = 16, kBigU = 1, kSmallV = 4, kSmallU = 4;
+  static constexpr bool kBuf = true;
 };
 template <>
 struct Geometry<AccF64> {
   static constexpr int kBigV = 4, kBigU = 1, kSmallV = 4, kSmallU = 1;
+  static constexpr bool kBuf = false;
 };
 template <>
 struct Geometry<AccI64> {
   static constexpr int kBigV = 4, kBigU = 1, kSmallV = 4, kSmallU = 1;
+  static constexpr bool kBuf = false;
 };
 
 int device_cus() {
@@ -94,7 +99,7 @@ int launch_reduce(const typename P::x_t* stack, int64_t stride, int n, const voi
   const int64_t big_tiles = (ncols + per_big - 1) / per_big;
   if (big_tiles > 0x7fffffff) return fail(FA_ERR_ARG, "n_cols too large");
   if (big_tiles >= 2 * (int64_t)cus) {
-    auto one = reduce_kernel<P, T, OP, G::kBigV, G::kBigU, kNT>;
+    auto one = reduce_kernel<P, T, OP, G::kBigV, G::kBigU, kNT, G::kBuf>;
     const int64_t slots = (int64_t)cus * resident_blocks_per_cu(one);
     const int64_t rounds = (big_tiles + slots - 1) / slots;
     if (big_tiles * 100 >= rounds * slots * 85) {  // one-shot rounds >= 85% full: no real tail
@@ -103,7 +108,7 @@ int launch_reduce(const typename P::x_t* stack, int64_t stride, int n, const voi
       return launch_check();
     }
     // a badly filled last round: same tile shape, `rounds` equal waves of resident blocks
-    auto bal = reduce_kernel_balanced<P, T, OP, G::kBigV, G::kBigU, kNT>;
+    auto bal = reduce_kernel_balanced<P, T, OP, G::kBigV, G::kBigU, kNT, G::kBuf>;
     const int64_t bslots = (int64_t)cus * resident_blocks_per_cu(bal);
     const int64_t grid = ((big_tiles + bslots - 1) / bslots) * bslots;
     hipLaunchKernelGGL(bal, dim3((unsigned)(grid < chunks ? grid : chunks)), dim3(kThreads), 0, s, stack,

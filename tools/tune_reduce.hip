@@ -50,6 +50,29 @@ __global__ __launch_bounds__(256) void copy_roof(const float* __restrict__ x, fl
     reinterpret_cast<f4*>(y)[q] = reinterpret_cast<const f4*>(x)[q];
 }
 
+// roof in the reduce's access shape: tiles of 256*B quads read as B 1-KiB-per-wave bursts, tile
+// after tile (grid-stride), LDS used only to cap occupancy; no row jumps, no arithmetic chain
+template <int B>
+__global__ __launch_bounds__(256) void roof_burst(const float* __restrict__ x, int64_t quads,
+                                                  float* __restrict__ sink) {
+  extern __shared__ float lds_cap[];
+  typedef vec4<float>::type f4;
+  f4 acc = {0.f, 0.f, 0.f, 0.f};
+  const int64_t tiles = quads / (256 * B);
+  for (int64_t t = blockIdx.x; t < tiles; t += gridDim.x) {
+    f4 v[B];
+#pragma unroll
+    for (int b = 0; b < B; ++b)
+      v[b] = __builtin_nontemporal_load(reinterpret_cast<const f4*>(x) + t * 256 * B + b * 256 + threadIdx.x);
+#pragma unroll
+    for (int b = 0; b < B; ++b) acc += v[b];
+  }
+  if (acc[0] + acc[1] + acc[2] + acc[3] == 12345.678f) {
+    lds_cap[threadIdx.x] = acc[0];
+    sink[threadIdx.x] = lds_cap[(threadIdx.x + 1) & 255];
+  }
+}
+
 struct Variant {
   std::string name;
   double bytes;
@@ -58,37 +81,37 @@ struct Variant {
   std::vector<float> times;
 };
 
-template <int V, int U, bool NT, int OP, typename T>
+template <int V, int U, bool NT, int OP, typename T, bool BUF = false>
 Variant make_oneshot(const float* stack, int64_t stride, int n, const float* w, int64_t ncols,
                      Epi<T> e, double bytes) {
   const int64_t tiles = (ncols + 256 * V * 4 - 1) / (256 * V * 4);
   char name[96];
-  snprintf(name, sizeof name, "oneshot V%d U%d NT%d", V, U, (int)NT);
+  snprintf(name, sizeof name, "oneshot%s V%d U%d NT%d", BUF ? "-buf" : "", V, U, (int)NT);
   return {name, bytes,
           [=] {
-            hipLaunchKernelGGL((reduce_kernel<AccF32, T, OP, V, U, NT>), dim3((unsigned)tiles), dim3(256), 0,
-                               0, stack, stride, n, w, (int64_t)0, ncols, e);
+            hipLaunchKernelGGL((reduce_kernel<AccF32, T, OP, V, U, NT, BUF>), dim3((unsigned)tiles), dim3(256),
+                               0, 0, stack, stride, n, w, (int64_t)0, ncols, e);
           },
           true, {}};
 }
 
 // rounds_extra: grid = (k + rounds_extra) * CUs * occupancy, k = the fewest rounds for which
 // every block's share fits one sub-tile
-template <int V, int U, bool NT, int OP, typename T>
+template <int V, int U, bool NT, int OP, typename T, bool BUF = false>
 Variant make_balanced(const float* stack, int64_t stride, int n, const float* w, int64_t ncols,
                       Epi<T> e, double bytes, int cus, int rounds_extra) {
   int occ = 0;
-  CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, reduce_kernel_balanced<AccF32, T, OP, V, U, NT>,
+  CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, reduce_kernel_balanced<AccF32, T, OP, V, U, NT, BUF>,
                                                   256, 0));
   const int64_t slots = (int64_t)cus * occ;
   const int64_t chunks = ((ncols + 3) / 4 + 63) / 64;
   const int64_t k = (chunks + slots * 4 * V - 1) / (slots * 4 * V) + rounds_extra;
   const int grid = (int)std::min<int64_t>(std::max<int64_t>(1, k * slots), chunks);
   char name[96];
-  snprintf(name, sizeof name, "balanced V%d U%d occ%d g%d", V, U, occ, grid);
+  snprintf(name, sizeof name, "balanced%s V%d U%d occ%d g%d", BUF ? "-buf" : "", V, U, occ, grid);
   return {name, bytes,
           [=] {
-            hipLaunchKernelGGL((reduce_kernel_balanced<AccF32, T, OP, V, U, NT>), dim3(grid), dim3(256), 0, 0,
+            hipLaunchKernelGGL((reduce_kernel_balanced<AccF32, T, OP, V, U, NT, BUF>), dim3(grid), dim3(256), 0, 0,
                                stack, stride, n, w, (int64_t)0, ncols, e);
           },
           true, {}};
@@ -153,6 +176,53 @@ int main(int argc, char** argv) {
   const char* set = getenv("TUNE_SET") ? getenv("TUNE_SET") : "main";
   ONESHOT(2, 8, true);  // previous product geometry first: the bitwise reference for the others
   ONESHOT(8, 4, true);
+  if (!strcmp(set, "roof")) {
+    const int64_t q = (int64_t)n * stride / 4;
+    auto add_roof = [&](auto kern, int B, int waves_per_simd) {
+      // blocks per CU = waves_per_simd (4 waves per 256-thread block, one per SIMD)
+      const int lds = waves_per_simd >= 8 ? 0 : (160 * 1024) / waves_per_simd - 64;
+      const int grid = cus * waves_per_simd;
+      char name[96];
+      snprintf(name, sizeof name, "roof burst B%d occ%d", B, waves_per_simd);
+      vs.push_back({name, (double)(q / (256 * B)) * 256 * B * 16,
+                    [=] { hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, 0, stack, q, sink); }, false, {}});
+    };
+    for (int occ : {8, 4, 3, 2}) {
+      add_roof(roof_burst<1>, 1, occ);
+      add_roof(roof_burst<4>, 4, occ);
+      add_roof(roof_burst<16>, 16, occ);
+    }
+  }
+#define ONESHOTB(V, U)                                                                                       \
+  vs.push_back(op == FA_OP_AVGM      ? make_oneshot<V, U, true, FA_OP_AVGM, double, true>(stack, stride, n, w, ncols, e, bytes) \
+               : op == FA_OP_ADAGRAD ? make_oneshot<V, U, true, FA_OP_ADAGRAD, double, true>(stack, stride, n, w, ncols, e, bytes) \
+                                     : make_oneshot<V, U, true, FA_OP_MEAN, double, true>(stack, stride, n, w, ncols, e, bytes))
+#define BALB(V, U, G4)                                                                                    \
+  vs.push_back(op == FA_OP_AVGM      ? make_balanced<V, U, true, FA_OP_AVGM, double, true>(stack, stride, n, w, ncols, e, bytes, cus, G4) \
+               : op == FA_OP_ADAGRAD ? make_balanced<V, U, true, FA_OP_ADAGRAD, double, true>(stack, stride, n, w, ncols, e, bytes, cus, G4) \
+                                     : make_balanced<V, U, true, FA_OP_MEAN, double, true>(stack, stride, n, w, ncols, e, bytes, cus, G4))
+  if (!strcmp(set, "buf")) {
+    ONESHOT(16, 1, true);
+    ONESHOTB(16, 1);
+    ONESHOTB(12, 1);
+    ONESHOTB(8, 1);
+    BAL(16, 1, 0);
+    BALB(16, 1, 0);
+    BALB(16, 1, 1);
+    BALB(12, 1, 0);
+    BALB(8, 1, 0);
+    BALB(8, 2, 0);
+    BALB(4, 4, 0);
+  }
+  if (!strcmp(set, "balance")) {
+    ONESHOT(16, 1, true);
+    ONESHOT(15, 1, true);
+    ONESHOT(14, 1, true);
+    ONESHOT(12, 1, true);
+    ONESHOT(10, 1, true);
+    BAL(16, 1, 0);
+    BAL(12, 1, 0);
+  }
   if (!strcmp(set, "main")) {
     ONESHOT(4, 1, true);
     ONESHOT(8, 1, true);
