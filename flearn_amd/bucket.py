@@ -173,41 +173,69 @@ class Packer:
                 out[kind] = dev
                 continue
             host = self._buf(self._pinned, kind, (plan.n_clients, g.stride), tdt, pin_memory=True)
-            host_np = host.numpy()
-
-            def fill(n, g=g, host_np=host_np):
-                row = host_np[n]
-                w = w_local_lst[n]
-                for s in g.segments:
-                    v = w[s.key]
-                    if isinstance(v, torch.Tensor):
-                        v = v.detach().cpu().numpy()
-                    row[s.offset : s.offset + s.numel] = np.asarray(v).reshape(-1)
-
-            if plan.n_clients > 1 and self.workers > 1:
-                with concurrent.futures.ThreadPoolExecutor(min(self.workers, plan.n_clients)) as ex:
-                    list(ex.map(fill, range(plan.n_clients)))
-            else:
-                for n in range(plan.n_clients):
-                    fill(n)
-            dev.copy_(host, non_blocking=True)
+            self._pack_pipelined(plan, g, w_local_lst, host, dev)
             out[kind] = dev
         return out
 
+    def _pack_pipelined(self, plan: BucketPlan, g: Group, w_local_lst, host, dev):
+        """Host ingest: client rows are packed into pinned staging by a thread pool, chunk by
+        chunk, and each finished chunk's H2D copy is queued at once, so the DMA of chunk k runs
+        while the CPU packs chunk k+1 (flearn's uploads are pageable host arrays: they must be
+        copied once into pinned memory before the DMA engine can read them)."""
+        host_np = host.numpy()
+
+        def fill(n):
+            row = host_np[n]
+            w = w_local_lst[n]
+            for s in g.segments:
+                v = w[s.key]
+                if isinstance(v, torch.Tensor):
+                    v = v.detach().cpu().numpy()
+                row[s.offset : s.offset + s.numel] = np.asarray(v).reshape(-1)
+
+        n = plan.n_clients
+        workers = max(1, min(self.workers, n))
+        chunk = max(workers, -(-n // 8))  # ~8 chunks, at least one row per worker
+        if workers == 1:
+            for r in range(n):
+                fill(r)
+            dev.copy_(host, non_blocking=True)
+            return
+        with concurrent.futures.ThreadPoolExecutor(workers) as ex:
+            for lo in range(0, n, chunk):
+                hi = min(n, lo + chunk)
+                list(ex.map(fill, range(lo, hi)))
+                dev[lo:hi].copy_(host[lo:hi], non_blocking=True)
+
     def unpack(self, plan: BucketPlan, results: dict, as_torch: bool, out_dtype_override=None) -> dict:
         """results: kind -> device tensor [stride].  Returns {key: fresh value} in plan order,
-        with the reference's types: ndarray (numpy scalar for 0-d keys) or torch CPU tensor."""
+        with the reference's types: ndarray (numpy scalar for 0-d keys) or torch CPU tensor.
+        D2H goes to reusable pinned staging (full PCIe rate); the result is then copied, by a
+        thread pool in slices, into ONE freshly allocated buffer per call whose views are handed
+        out — nothing returned is shared with staging or with later calls."""
         host = {}
         for kind, t in results.items():
             h = self._buf(self._pinned, ("out", kind, t.dtype), tuple(t.shape), t.dtype, pin_memory=True)
             h.copy_(t, non_blocking=True)
             host[kind] = h
         torch.cuda.current_stream(self.device).synchronize()
+        fresh = {}
+        for kind, h in host.items():
+            src = h.numpy()
+            dst = np.empty_like(src)
+            step = 1 << 22  # 4M elements per slice
+            if src.size > step and self.workers > 1:
+                with concurrent.futures.ThreadPoolExecutor(self.workers) as ex:
+                    list(ex.map(lambda lo: np.copyto(dst[lo : lo + step], src[lo : lo + step]),
+                                range(0, src.size, step)))
+            else:
+                np.copyto(dst, src)
+            fresh[kind] = dst
         glob = {}
         for k in plan.keys:
             kind = plan.key_group[k]
             s = plan.key_segment[k]
-            arr = host[kind].numpy()[s.offset : s.offset + s.numel].reshape(s.shape).copy()
+            arr = fresh[kind][s.offset : s.offset + s.numel].reshape(s.shape)
             if out_dtype_override is not None:
                 arr = arr.astype(out_dtype_override, copy=False)
             if as_torch:
