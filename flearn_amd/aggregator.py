@@ -171,8 +171,9 @@ class ServerOptimizer:
     """FedAVGM / FedOPT state for the fused server step.
 
     op     : "avgm" | "adagrad" | "yogi" | "adam"
-    state  : prev (fp32 previous global, flattened like the f32 bucket) and v_t (f64, or fp32 when
-             the weights make the reference's w_glob float32), both resident in HBM.
+    state  : per column shard (one per device), prev (fp32 previous global, flattened like the
+             f32 bucket) and v_t (f64, or fp32 when the weights make the reference's w_glob
+             float32), resident in HBM and never communicated.
     First round without `init_global`: the update is skipped (the mean is returned), prev is set
     to the fp32 mean and v_t to zeros — the reference has no previous global model either.
     """
@@ -183,35 +184,39 @@ class ServerOptimizer:
         self.op = na.OP_BY_NAME[op]
         self.name = op
         self.beta, self.eta, self.tau, self.beta2 = beta, eta, tau, beta2
-        self.prev = None
-        self.v = None
+        self.state = {}  # shard index -> (prev, v)
         self._sig = None
         self._pending_init = None
 
     def init_global(self, glob: dict):
         """Set the previous global model (dict of arrays/tensors); v_t is reset to zeros."""
         self._pending_init = {k: np.asarray(v.cpu() if isinstance(v, torch.Tensor) else v) for k, v in glob.items()}
-        self.prev = self.v = self._sig = None
+        self.state, self._sig = {}, None
 
     @staticmethod
-    def _signature(plan: BucketPlan, numerics: Numerics):
+    def _signature(plan: BucketPlan, shards):
         g = plan.f32
-        return tuple((s.key, s.shape) for s in g.segments), numerics.out_dtype.str
+        return (tuple((s.key, s.shape) for s in g.segments), g.numerics.out_dtype.str,
+                tuple((sh.device, sh.c0, sh.c1) for sh in shards))
 
-    def prepare(self, plan: BucketPlan, device) -> bool:
+    @staticmethod
+    def _vdtype(plan):
+        return torch.float32 if plan.f32.numerics.out_dtype == np.float32 else torch.float64
+
+    def prepare(self, plan: BucketPlan, shards) -> bool:
         """Bind the state to this plan's f32 bucket.  Returns False when there is no previous
         model yet (first round): the caller then runs a plain mean and calls `adopt`."""
         g = plan.f32
-        sig = self._signature(plan, g.numerics)
-        vdt = torch.float32 if g.numerics.out_dtype == np.float32 else torch.float64
+        sig = self._signature(plan, shards)
         if self._pending_init is not None:
-            prev = torch.zeros(g.stride, dtype=torch.float32)
+            prev = np.zeros(g.stride, dtype=np.float32)
             for s in g.segments:
-                prev[s.offset : s.offset + s.numel] = torch.from_numpy(
-                    np.asarray(self._pending_init[s.key], dtype=np.float32).reshape(-1).copy()
-                )
-            self.prev = prev.to(device)
-            self.v = torch.zeros(g.stride, dtype=vdt, device=device)
+                prev[s.offset : s.offset + s.numel] = np.asarray(self._pending_init[s.key], np.float32).reshape(-1)
+            self.state = {
+                sh.index: (torch.from_numpy(prev[sh.c0 : sh.c1].copy()).to(sh.device),
+                           torch.zeros(sh.width, dtype=self._vdtype(plan), device=sh.device))
+                for sh in shards
+            }
             self._sig = sig
             self._pending_init = None
             return True
@@ -221,16 +226,16 @@ class ServerOptimizer:
             raise ValueError("model layout changed between rounds; call init_global() again")
         return True
 
-    def adopt(self, plan: BucketPlan, mean32: torch.Tensor):
-        g = plan.f32
-        vdt = torch.float32 if g.numerics.out_dtype == np.float32 else torch.float64
-        self.prev = mean32.clone()
-        self.v = torch.zeros(g.stride, dtype=vdt, device=mean32.device)
-        self._sig = self._signature(plan, g.numerics)
+    def adopt(self, plan: BucketPlan, shards, means: dict):
+        """First round: the fp32 mean becomes prev, v_t = 0.  means: shard index -> fp32 tensor."""
+        self.state = {sh.index: (means[sh.index][: sh.width].clone(),
+                                 torch.zeros(sh.width, dtype=self._vdtype(plan), device=sh.device))
+                      for sh in shards}
+        self._sig = self._signature(plan, shards)
 
     def v_t(self, plan: BucketPlan) -> dict:
         """The state as the reference exposes it (self.v_t dict of arrays)."""
-        host = self.v.cpu().numpy()
+        host = np.concatenate([self.state[i][1].cpu().numpy() for i in sorted(self.state)])
         return {s.key: host[s.offset : s.offset + s.numel].reshape(s.shape).copy() for s in plan.f32.segments}
 
 
@@ -245,65 +250,78 @@ class Aggregator:
     """output: "reference" — values with the reference's types and dtypes (float64 ndarrays, numpy
     scalars for 0-d buffers, torch CPU tensors when the uploads were tensors);
     "float32" — fp32 ndarrays for fp32 keys (the values load_state_dict ends up with);
-    "device" — fresh torch CUDA tensors, fp32 for fp32 keys (no D2H)."""
+    "device" — fresh torch CUDA tensors on the first device, fp32 for fp32 keys (no D2H).
 
-    def __init__(self, device=None, output: str = "reference", workers: int = 8):
+    devices: the HIP devices the f32 bucket is split over (column shards); each ingests its
+    columns through its own PCIe link.  Default: torch's current device only."""
+
+    def __init__(self, device=None, output: str = "reference", workers: int = 8, devices=None):
         na.lib()  # fail loudly right away if the HIP path is unavailable
         if output not in OUTPUTS:
             raise ValueError(f"output must be one of {OUTPUTS}")
-        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        if devices is None:
+            devices = [torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())]
+        self.devices = [torch.device(d) for d in devices]
+        self.device = self.devices[0]
         self.output = output
-        self.packer = Packer(self.device, workers)
+        self.packer = Packer(self.devices, workers)
         self.last_plan: BucketPlan | None = None
-
-    def _weights(self, nm: Numerics) -> torch.Tensor:
-        return torch.from_numpy(nm.weights).to(self.device)
 
     def ensemble(self, agg_weight_lst, w_local_lst, key_lst=None, server_opt: ServerOptimizer | None = None):
         plan = make_plan(agg_weight_lst, w_local_lst, key_lst)
         self.last_plan = plan
-        with torch.cuda.device(self.device):
-            stacks = self.packer.pack(plan, w_local_lst)
-            results = {}
-            for kind, g in plan.groups.items():
-                nm = g.numerics
-                w = self._weights(nm)
-                if kind == KIND_F32:
-                    results[kind] = self._reduce_f32(plan, g, stacks[kind], w, server_opt)
-                elif kind == KIND_F64:
-                    out = self.packer.device_bucket(("out64", kind), (g.stride,), torch.float64)
-                    reduce_stack_f64(stacks[kind], w, nm.denom, out)
-                    results[kind] = out
-                elif kind == KIND_I64:
-                    out = self.packer.device_bucket(("out64", kind), (g.stride,), torch.float64)
-                    reduce_stack_i64(stacks[kind], w, nm.denom, out)
-                    results[kind] = out
-            return self._finish(plan, results)
+        stacks = self.packer.pack(plan, w_local_lst)
+        fused = False
+        if server_opt is not None and KIND_F32 in plan.groups:
+            fused = server_opt.prepare(plan, [sh for sh, _ in stacks[KIND_F32]])
+        results = {}
+        first_means = {}
+        for kind, parts in stacks.items():
+            g = plan.groups[kind]
+            nm = g.numerics
+            res = []
+            for sh, stack in parts:
+                with torch.cuda.device(sh.device):
+                    w = torch.from_numpy(nm.weights).to(sh.device)
+                    if kind == KIND_F32:
+                        out = self._reduce_f32(g, sh, stack, w, server_opt, fused, first_means)
+                    else:
+                        out = self.packer.device_bucket(("out64", kind, sh.index), (sh.width,), torch.float64, sh.device)
+                        (reduce_stack_f64 if kind == KIND_F64 else reduce_stack_i64)(stack, w, nm.denom, out)
+                res.append((sh, out))
+            results[kind] = res
+        if server_opt is not None and first_means:
+            server_opt.adopt(plan, [sh for sh, _ in stacks[KIND_F32]], first_means)
+        return self._finish(plan, results)
 
-    def _reduce_f32(self, plan, g, stack, w, server_opt):
+    def _reduce_f32(self, g, sh, stack, w, server_opt, fused, first_means):
         nm = g.numerics
         want64 = self.output == "reference" and nm.out_dtype == _F64
-        out64 = self.packer.device_bucket(("out64", KIND_F32), (g.stride,), torch.float64) if want64 else None
-        out32 = None if want64 else self.packer.device_bucket(("out32", KIND_F32), (g.stride,), torch.float32)
-        if server_opt is None:
-            reduce_stack(stack, w, nm.mode, nm.denom, out32=out32, out64=out64)
-            return out64 if want64 else out32
-        if not server_opt.prepare(plan, self.device):
-            mean32 = self.packer.device_bucket(("mean32", KIND_F32), (g.stride,), torch.float32)
-            reduce_stack(stack, w, nm.mode, nm.denom, out32=mean32, out64=out64)
-            server_opt.adopt(plan, mean32)
-            return out64 if want64 else mean32
-        # fused: prev is updated in place to fl32(w) — the model clients load next round
-        reduce_stack(stack, w, nm.mode, nm.denom, out32=server_opt.prev, out64=out64, op=server_opt.op,
-                     prev=server_opt.prev, v=server_opt.v, beta=server_opt.beta, eta=server_opt.eta,
-                     tau=server_opt.tau, beta2=server_opt.beta2)
-        return out64 if want64 else server_opt.prev
+        out64 = (self.packer.device_bucket(("out64", KIND_F32, sh.index), (sh.width,), torch.float64, sh.device)
+                 if want64 else None)
+        if server_opt is not None and fused:
+            # fused: prev is updated in place to fl32(w) — the model clients load next round
+            prev, v = server_opt.state[sh.index]
+            reduce_stack(stack, w, nm.mode, nm.denom, out32=prev, out64=out64, op=server_opt.op, prev=prev, v=v,
+                         beta=server_opt.beta, eta=server_opt.eta, tau=server_opt.tau, beta2=server_opt.beta2)
+            return out64 if want64 else prev
+        out32 = None
+        if not want64 or server_opt is not None:
+            out32 = self.packer.device_bucket(("out32", KIND_F32, sh.index), (sh.width,), torch.float32, sh.device)
+        reduce_stack(stack, w, nm.mode, nm.denom, out32=out32, out64=out64)
+        if server_opt is not None:
+            first_means[sh.index] = out32
+        return out64 if want64 else out32
 
     def _finish(self, plan: BucketPlan, results: dict):
         if self.output == "device":
             glob = {}
             for k in plan.keys:
                 s = plan.key_segment[k]
-                glob[k] = results[plan.key_group[k]][s.offset : s.offset + s.numel].view(s.shape).clone()
+                lo, hi = s.offset, s.offset + s.numel
+                pieces = [t[max(lo, sh.c0) - sh.c0 : min(hi, sh.c1) - sh.c0].to(self.device)
+                          for sh, t in results[plan.key_group[k]] if max(lo, sh.c0) < min(hi, sh.c1)]
+                flat = pieces[0].clone() if len(pieces) == 1 else torch.cat(pieces)
+                glob[k] = flat.view(s.shape)
             return glob
         return self.packer.unpack(plan, results, as_torch=plan.input_kind == "torch")

@@ -30,6 +30,7 @@ ALIGN = 64  # elements: 256 B for fp32, 512 B for 8-byte kinds
 
 _STORE = {KIND_F32: np.float32, KIND_F64: np.float64, KIND_I64: np.int64}
 _TORCH = {np.float32: torch.float32, np.float64: torch.float64, np.int64: torch.int64}
+_NP = {torch.float32: np.float32, torch.float64: np.float64, torch.int64: np.int64}
 
 
 @dataclass
@@ -137,14 +138,44 @@ def _same_numerics(a: Numerics, b: Numerics) -> bool:
     )
 
 
-class Packer:
-    """Owns reusable pinned staging and device buckets; packs uploads, unpacks results."""
+@dataclass(frozen=True)
+class Shard:
+    """A column range [c0, c1) of the f32 bucket that lives on one device (multi-GPU ingest).
+    Non-f32 buckets (f64 / i64: BN counters, a few bytes) always live on shard 0."""
 
-    def __init__(self, device, workers: int = 8):
-        self.device = torch.device(device)
+    index: int
+    device: torch.device
+    c0: int
+    c1: int
+
+    @property
+    def width(self) -> int:
+        return self.c1 - self.c0
+
+
+def split_columns(stride: int, devices) -> list:
+    """Near-equal ALIGN-aligned column ranges of a stride-wide bucket, one per device."""
+    k = len(devices)
+    units = stride // ALIGN
+    bounds = [ALIGN * (units * i // k) for i in range(k + 1)]
+    bounds[-1] = stride
+    return [Shard(i, torch.device(d), bounds[i], bounds[i + 1]) for i, d in enumerate(devices)]
+
+
+class Packer:
+    """Owns reusable pinned staging and device buckets; packs uploads, unpacks results.
+
+    The f32 bucket is split by columns over `devices` (one Shard each): every device receives
+    its columns of every client through its own PCIe link, reduces them, and sends its slice of
+    the global model back — per-GPU parallel H2D/D2H.  With one device this is the plain path."""
+
+    def __init__(self, devices, workers: int = 8):
+        self.devices = [torch.device(d) for d in devices]
+        self.device = self.devices[0]
         self.workers = workers
         self._pinned = {}
         self._dev = {}
+        self._shards = {}
 
     def _buf(self, cache, key, shape, dtype, **kw):
         t = cache.get(key)
@@ -154,83 +185,128 @@ class Packer:
             cache[key] = t
         return t[: math.prod(shape)].view(shape)
 
-    def device_bucket(self, tag, shape, dtype):
+    def device_bucket(self, tag, shape, dtype, device=None):
         """A reusable device buffer (contents undefined)."""
-        return self._buf(self._dev, tag, shape, dtype, device=self.device)
+        dev = self.device if device is None else torch.device(device)
+        return self._buf(self._dev, (tag, str(dev)), shape, dtype, device=dev)
+
+    def shards(self, plan: BucketPlan, kind: str) -> list:
+        g = plan.groups[kind]
+        if kind != KIND_F32:
+            return [Shard(0, self.device, 0, g.stride)]
+        key = (g.stride, tuple(str(d) for d in self.devices))
+        if key not in self._shards:
+            self._shards[key] = split_columns(g.stride, self.devices)
+        return self._shards[key]
+
+    @staticmethod
+    def _pieces(g: Group, shards) -> list:
+        """(segment, src_lo, src_hi, shard, dst_lo): each key segment cut at shard boundaries."""
+        out = []
+        for s in g.segments:
+            lo, hi = s.offset, s.offset + s.numel
+            for sh in shards:
+                a, b = max(lo, sh.c0), min(hi, sh.c1)
+                if a < b:
+                    out.append((s, a - lo, b - lo, sh, a - sh.c0))
+        return out
 
     def pack(self, plan: BucketPlan, w_local_lst) -> dict:
-        """Copy every client's selected tensors into the device buckets: kind -> [N, stride]."""
+        """Copy every client's selected tensors into the device buckets.
+        Returns kind -> [(shard, device stack [N, shard.width])]."""
         out = {}
         for kind, g in plan.groups.items():
             tdt = _TORCH[g.store_dtype]
-            dev = self.device_bucket(("in", kind), (plan.n_clients, g.stride), tdt)
-            if plan.input_kind == "torch" and all(
-                w_local_lst[0][s.key].device.type == "cuda" for s in g.segments
-            ):
+            shards = self.shards(plan, kind)
+            devs = [self.device_bucket(("in", kind, sh.index), (plan.n_clients, sh.width), tdt, sh.device)
+                    for sh in shards]
+            pieces = self._pieces(g, shards)
+            if plan.input_kind == "torch" and all(w_local_lst[0][s.key].device.type == "cuda" for s in g.segments):
                 for n, w in enumerate(w_local_lst):
-                    for s in g.segments:
-                        dev[n, s.offset : s.offset + s.numel].copy_(w[s.key].reshape(-1))
-                out[kind] = dev
-                continue
-            host = self._buf(self._pinned, kind, (plan.n_clients, g.stride), tdt, pin_memory=True)
-            self._pack_pipelined(plan, g, w_local_lst, host, dev)
-            out[kind] = dev
+                    for s, a, b, sh, d in pieces:
+                        devs[sh.index][n, d : d + (b - a)].copy_(w[s.key].reshape(-1)[a:b])
+            else:
+                hosts = [self._buf(self._pinned, ("in", kind, sh.index), (plan.n_clients, sh.width), tdt,
+                                   pin_memory=True) for sh in shards]
+                self._pack_pipelined(plan, pieces, w_local_lst, shards, hosts, devs)
+            out[kind] = list(zip(shards, devs))
         return out
 
-    def _pack_pipelined(self, plan: BucketPlan, g: Group, w_local_lst, host, dev):
+    def _pack_pipelined(self, plan: BucketPlan, pieces, w_local_lst, shards, hosts, devs):
         """Host ingest: client rows are packed into pinned staging by a thread pool, chunk by
-        chunk, and each finished chunk's H2D copy is queued at once, so the DMA of chunk k runs
-        while the CPU packs chunk k+1 (flearn's uploads are pageable host arrays: they must be
-        copied once into pinned memory before the DMA engine can read them)."""
-        host_np = host.numpy()
+        chunk, and each finished chunk's H2D copies (one per shard, on that device's stream) are
+        queued at once, so the DMA of chunk k runs while the CPU packs chunk k+1 (flearn's
+        uploads are pageable host arrays: they must be copied once into pinned memory before a
+        DMA engine can read them)."""
+        host_np = [h.numpy() for h in hosts]
 
         def fill(n):
-            row = host_np[n]
             w = w_local_lst[n]
-            for s in g.segments:
-                v = w[s.key]
-                if isinstance(v, torch.Tensor):
-                    v = v.detach().cpu().numpy()
-                row[s.offset : s.offset + s.numel] = np.asarray(v).reshape(-1)
+            cache = {}
+            for s, a, b, sh, d in pieces:
+                src = cache.get(s.key)
+                if src is None:
+                    v = w[s.key]
+                    if isinstance(v, torch.Tensor):
+                        v = v.detach().cpu().numpy()
+                    src = cache[s.key] = np.asarray(v).reshape(-1)
+                host_np[sh.index][n, d : d + (b - a)] = src[a:b]
+
+        def ship(lo, hi):
+            for sh, h, dv in zip(shards, hosts, devs):
+                with torch.cuda.device(sh.device):
+                    dv[lo:hi].copy_(h[lo:hi], non_blocking=True)
 
         n = plan.n_clients
         workers = max(1, min(self.workers, n))
-        chunk = max(workers, -(-n // 8))  # ~8 chunks, at least one row per worker
         if workers == 1:
             for r in range(n):
                 fill(r)
-            dev.copy_(host, non_blocking=True)
+            ship(0, n)
             return
+        chunk = max(workers, -(-n // 8))  # ~8 chunks, at least one row per worker
         with concurrent.futures.ThreadPoolExecutor(workers) as ex:
             for lo in range(0, n, chunk):
                 hi = min(n, lo + chunk)
                 list(ex.map(fill, range(lo, hi)))
-                dev[lo:hi].copy_(host[lo:hi], non_blocking=True)
+                ship(lo, hi)
 
     def unpack(self, plan: BucketPlan, results: dict, as_torch: bool, out_dtype_override=None) -> dict:
-        """results: kind -> device tensor [stride].  Returns {key: fresh value} in plan order,
-        with the reference's types: ndarray (numpy scalar for 0-d keys) or torch CPU tensor.
-        D2H goes to reusable pinned staging (full PCIe rate); the result is then copied, by a
-        thread pool in slices, into ONE freshly allocated buffer per call whose views are handed
-        out — nothing returned is shared with staging or with later calls."""
-        host = {}
-        for kind, t in results.items():
-            h = self._buf(self._pinned, ("out", kind, t.dtype), tuple(t.shape), t.dtype, pin_memory=True)
-            h.copy_(t, non_blocking=True)
-            host[kind] = h
-        torch.cuda.current_stream(self.device).synchronize()
-        fresh = {}
-        for kind, h in host.items():
+        """results: kind -> [(shard, device tensor [shard.width])].  Returns {key: fresh value} in
+        plan order with the reference's types: ndarray (numpy scalar for 0-d keys) or torch CPU
+        tensor.  Each shard's D2H goes to reusable pinned staging on its device's stream (all
+        links in parallel); the slices are then copied, by a thread pool, into ONE freshly
+        allocated buffer per kind whose views are handed out — nothing returned is shared with
+        staging or with later calls."""
+        staged = []
+        for kind, parts in results.items():
+            for sh, t in parts:
+                h = self._buf(self._pinned, ("out", kind, sh.index, t.dtype), (sh.width,), t.dtype, pin_memory=True)
+                with torch.cuda.device(sh.device):
+                    h.copy_(t[: sh.width], non_blocking=True)
+                staged.append((kind, sh, h))
+        for d in {sh.device for _, sh, _ in staged}:
+            torch.cuda.current_stream(d).synchronize()
+        fresh = {kind: np.empty(plan.groups[kind].stride, dtype=_NP[parts[0][1].dtype])
+                 for kind, parts in results.items()}
+        step = 1 << 22  # 4M elements per copy task
+        tasks = []
+        for kind, sh, h in staged:
             src = h.numpy()
-            dst = np.empty_like(src)
-            step = 1 << 22  # 4M elements per slice
-            if src.size > step and self.workers > 1:
-                with concurrent.futures.ThreadPoolExecutor(self.workers) as ex:
-                    list(ex.map(lambda lo: np.copyto(dst[lo : lo + step], src[lo : lo + step]),
-                                range(0, src.size, step)))
-            else:
-                np.copyto(dst, src)
-            fresh[kind] = dst
+            for lo in range(0, sh.width, step):
+                hi = min(sh.width, lo + step)
+                tasks.append((fresh[kind], sh.c0 + lo, src, lo, hi))
+
+        def copy(t):
+            dst, d0, src, lo, hi = t
+            np.copyto(dst[d0 : d0 + (hi - lo)], src[lo:hi])
+
+        if len(tasks) > 1 and self.workers > 1:
+            with concurrent.futures.ThreadPoolExecutor(self.workers) as ex:
+                list(ex.map(copy, tasks))
+        else:
+            for t in tasks:
+                copy(t)
         glob = {}
         for k in plan.keys:
             kind = plan.key_group[k]

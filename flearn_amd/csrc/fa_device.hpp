@@ -423,6 +423,29 @@ __global__ __launch_bounds__(kThreads) void reduce_kernel(
                                            ncols, e);
 }
 
+// Column-blocked client stack: element (n, c) lives at ((c / B) * N + n) * B + c % B with
+// B = kThreads*V*4 columns (one tile).  Tile b's N rows are one contiguous N*B*4-byte region, so
+// a block streams its whole tile linearly (rows B*4 bytes apart) — the access pattern of a plain
+// streaming read.  One tile per block; the window is the whole (padded) bucket.
+template <class P, typename T, int OP, int V, int U, bool NT>
+__global__ __launch_bounds__(kThreads) void reduce_kernel_blocked(
+    const typename P::x_t* __restrict__ stack, int n, const typename P::w_t* __restrict__ w,
+    int64_t ncols, Epi<T> e) {
+  constexpr int64_t B = (int64_t)kThreads * V * 4;
+  const int64_t tile = blockIdx.x;
+  const typename P::x_t* base = stack + tile * (int64_t)n * B;
+  Epi<T> et = e;
+  if (et.out32) et.out32 += tile * B;
+  if (et.out64) et.out64 += tile * B;
+  if constexpr (OP != FA_OP_MEAN) {
+    et.prev += tile * B;
+    et.v += tile * B;
+  }
+  const int64_t cols = ncols - tile * B < B ? ncols - tile * B : B;
+  reduce_range_subtile<P, T, OP, V, U, NT, (sizeof(typename P::x_t) == 4)>(
+      base, B, n, w, 0, (cols + 3) / 4, cols, et);
+}
+
 // Standalone update (client_receive form): g read from memory instead of reduced.
 template <typename T, int OP>
 __global__ __launch_bounds__(kThreads) void apply_kernel(const T* __restrict__ glob, int64_t n,

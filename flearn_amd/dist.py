@@ -74,17 +74,20 @@ class ShardedReducer:
     the oracle to check the sharding and gather logic with gloo.
     """
 
-    def __init__(self, plan: ShardPlan, reduce_fn, device, group=None, local_out=None):
+    def __init__(self, plan: ShardPlan, reduce_fn, device, group=None, local_out=None, gather=None):
         self.plan = plan
         self.reduce_fn = reduce_fn
         self.device = torch.device(device)
         self.group = group
+        # gather=None: all-gather only when there is more than one rank; True forces the
+        # collective path (a 1-rank RCCL group exercises the exact multi-GPU call sequence)
+        self.gather = plan.world > 1 if gather is None else gather
         # local_out may alias the sharded `prev` of a fused optimizer (updated in place)
         self.local_out = (torch.empty(plan.local_cols, dtype=torch.float32, device=self.device)
                           if local_out is None else local_out)
         # one rank: local columns ARE the global columns, nothing to reassemble
-        self.full = (self.local_out if plan.world == 1
-                     else torch.empty(plan.padded, dtype=torch.float32, device=self.device))
+        self.full = (torch.empty(plan.padded, dtype=torch.float32, device=self.device) if self.gather
+                     else self.local_out)
 
     def step(self) -> torch.Tensor:
         p = self.plan
@@ -92,7 +95,7 @@ class ShardedReducer:
         for c in range(p.stripes):
             lo = p.local_begin(c)
             self.reduce_fn(lo, p.shard, self.local_out[lo : lo + p.shard])
-            if p.world > 1:
+            if self.gather:
                 dst = self.full[c * p.world * p.shard : (c + 1) * p.world * p.shard]
                 works.append(dist.all_gather_into_tensor(dst, self.local_out[lo : lo + p.shard],
                                                          group=self.group, async_op=True))

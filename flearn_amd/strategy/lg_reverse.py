@@ -7,8 +7,8 @@ from .utils import convert_to_tensor
 
 
 class LG_R(AVG):
-    def __init__(self, shared_key_layers=None, encrypt=None, output="reference", device=None):
-        super().__init__(encrypt, output, device)
+    def __init__(self, shared_key_layers=None, encrypt=None, output="reference", device=None, devices=None):
+        super().__init__(encrypt, output, device, devices)
         self.shared_key_layers = shared_key_layers
 
     def client(self, trainer, agg_weight=1.0):

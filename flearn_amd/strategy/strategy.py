@@ -7,8 +7,10 @@ Callers (flearn's Server.ensemble, Server.py:140) use exactly the reference's me
 engine (flearn_amd.aggregator), with results bit-identical to the reference's numpy arithmetic.
 
 Extra keyword arguments (all optional, defaults keep the reference's behaviour):
-    output : "reference" (default) | "float32" | "device"  — see Aggregator
-    device : HIP device for the engine (default: torch's current device)
+    output  : "reference" (default) | "float32" | "device"  — see Aggregator
+    device  : HIP device for the engine (default: torch's current device)
+    devices : several HIP devices: the bucket's columns are split over them, each ingesting and
+              reducing its share through its own PCIe link (per-GPU parallel H2D/D2H)
 """
 from __future__ import annotations
 
@@ -28,10 +30,11 @@ class BaseEncrypt:
 
 
 class Strategy(ABC):
-    def __init__(self, encrypt=None, output: str = "reference", device=None):
+    def __init__(self, encrypt=None, output: str = "reference", device=None, devices=None):
         self.encrypt = BaseEncrypt() if encrypt is None else encrypt
         self.output = output
         self.device = device
+        self.devices = devices
         self._engine = None
 
     # -- engine -----------------------------------------------------------------------------
@@ -41,7 +44,9 @@ class Strategy(ABC):
         if self.__dict__.get("_engine") is None:
             from ..aggregator import Aggregator
 
-            self._engine = Aggregator(device=self.__dict__.get("device"), output=self.__dict__.get("output", "reference"))
+            d = self.__dict__
+            self._engine = Aggregator(device=d.get("device"), output=d.get("output", "reference"),
+                                      devices=d.get("devices"))
         return self._engine
 
     # -- reference surface ------------------------------------------------------------------

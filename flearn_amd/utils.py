@@ -20,9 +20,9 @@ OUT_OF_SCOPE = ("distill", "dyn", "md", "pav", "df")
 def setup_strategy(strategy_name, custom_strategy, **strategy_p):
     """Name -> strategy instance, as common/utils.py:16-58.  Unknown names fall back to
     `custom_strategy`, else SystemError.  Extra keyword arguments understood here:
-    shared_key_layers (LG / LG_R), output / device (engine), server_side (AVGM / OPT)."""
+    shared_key_layers (LG / LG_R), output / device / devices (engine), server_side (AVGM / OPT)."""
     shared_key_layers = strategy_p.get("shared_key_layers", None)
-    eng = {k: strategy_p[k] for k in ("output", "device") if k in strategy_p}
+    eng = {k: strategy_p[k] for k in ("output", "device", "devices") if k in strategy_p}
     server_side = strategy_p.get("server_side", False)
     name = strategy_name.lower()
     factories = {

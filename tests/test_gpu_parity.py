@@ -353,3 +353,85 @@ def test_baseline_config_spot_parity(layout, n, op, cuda):
             g = oracle.c_update(op, g, prev_h[c0 : c0 + width], np.zeros(width))
         assert bitwise_equal(got[c0 : c0 + width], g.astype(np.float32)), (layout, c0)
     assert np.isfinite(got).all()
+
+
+# ---------------------------------------------------------------------------------------------
+# multi-GPU code path on one GPU: a 1-rank RCCL group runs the exact all-gather call sequence
+# ---------------------------------------------------------------------------------------------
+
+
+@pytest.mark.parametrize("op", ["mean", "avgm"])
+def test_sharded_reducer_rccl_one_rank(op, cuda, tmp_path):
+    import torch.distributed as dist
+
+    from flearn_amd.dist import ShardedReducer, ShardPlan, hip_reduce_fn
+
+    created = False
+    if not dist.is_initialized():
+        dist.init_process_group("nccl", init_method=f"file://{tmp_path}/pg", rank=0, world_size=1,
+                                device_id=cuda)
+        created = True
+    try:
+        n, p = 9, 1_000_003
+        plan = ShardPlan.make(p, 1, 0, stripes=4)
+        stack = torch.empty((n, plan.local_cols), dtype=torch.float32, device=cuda)
+        for c in range(plan.stripes):
+            agg.fill_uniform(stack[:, plan.local_begin(c):], seed=3, col_begin=plan.global_begin(c),
+                             n_cols=plan.shard)
+        w = torch.ones(n, dtype=torch.float32, device=cuda)
+        epi, local_out = {}, None
+        if op != "mean":
+            prev = torch.empty((1, plan.local_cols), dtype=torch.float32, device=cuda)
+            agg.fill_uniform(prev, seed=4)
+            prev_h = prev[0, :p].cpu().numpy().copy()
+            epi = dict(op=na.OP_BY_NAME[op], prev=prev[0], v=torch.zeros(plan.local_cols, dtype=torch.float64, device=cuda))
+            local_out = prev[0]
+        red = ShardedReducer(plan, hip_reduce_fn(stack, w, na.MODE_W32_DIV64, float(n), **epi), cuda,
+                             local_out=local_out, gather=True)
+        full = red.step().cpu().numpy()
+        want = oracle.c_reduce(oracle.MODE_W32_DIV64, oracle.fill_uniform(n, p, 3), np.ones(n, np.float32), float(n))
+        if op != "mean":
+            want = oracle.c_update(op, want, prev_h, np.zeros(p))
+        assert bitwise_equal(full, want.astype(np.float32))
+    finally:
+        if created:
+            dist.destroy_process_group()
+
+
+# ---------------------------------------------------------------------------------------------
+# column shards over several devices (per-GPU parallel ingest); here 2-3 shards on one GPU
+# ---------------------------------------------------------------------------------------------
+
+
+@pytest.mark.parametrize("name", ["avg_w1_n10", "avg_bnmodel_pyint_n4", "avg_special_n5", "trace_lenet5_round0",
+                                  "avg_np32_n10", "avg_torch_n3"])
+@pytest.mark.parametrize("k", [2, 3])
+def test_sharded_ingest_matches_reference(name, k, cuda):
+    g = Golden(name)
+    s = strategy_for(g)
+    s.devices = [cuda] * k
+    got = s.server(upload(g.clients(), g.weights()), 0)["w_glob"]
+    assert_dict_bitwise(got, g.output(), f"{name} x{k}")
+    assert len(s.engine.packer.shards(s.engine.last_plan, "f32")) == k
+
+
+@pytest.mark.parametrize("name", ["avgm_pyfloat_rounds3", "adagrad_np32_rounds3"])
+def test_sharded_fused_optimizer_matches_reference(name, cuda):
+    g = Golden(name)
+    op = g.meta["op"]
+    s = (AVGM(server_side=True, devices=[cuda] * 3) if op == "avgm"
+         else OPT(server_side=True, method=op, devices=[cuda] * 3))
+    s.server_opt.init_global({k[6:]: v for k, v in g.arrays.items() if k.startswith("prev0:")})
+    for r in range(g.meta["rounds"]):
+        clients, weights = _round_inputs(g, r)
+        got = s.server(upload(clients, weights), r)["w_glob"]
+        assert_dict_bitwise(got, g.output(f"w{r}"), f"{name} w{r}")
+        assert_dict_bitwise(s.server_opt.v_t(s.engine.last_plan), g.output(f"v{r}"), f"{name} v{r}")
+
+
+def test_sharded_device_output(cuda):
+    g = Golden("avg_w1_n10")
+    s = AVG(output="device", devices=[cuda, cuda])
+    got = s.server(upload(g.clients(), g.weights()), 0)["w_glob"]
+    for k, w in g.output().items():
+        assert bitwise_equal(got[k].cpu().numpy(), np.asarray(w).astype(np.float32)), k

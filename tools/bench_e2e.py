@@ -34,6 +34,7 @@ def main():
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--output", default="reference")
+    ap.add_argument("--devices", type=int, default=1, help="split columns over the first K GPUs")
     a = ap.parse_args()
     name, n = CONFIGS[a.config]
     layout = layouts.get(name)
@@ -45,22 +46,28 @@ def main():
     del x
     uploads = [{"agg_weight": 1.0, "params": layouts.synthetic_state_dict(layout, host[i], counter=100 + i)}
                for i in range(n)]
-    s = flearn_amd.AVG(output=a.output)
+    if a.devices > torch.cuda.device_count():
+        raise SystemExit(f"--devices {a.devices} but only {torch.cuda.device_count()} GPU(s) visible")
+    s = flearn_amd.AVG(output=a.output, devices=[torch.device("cuda", i) for i in range(a.devices)])
     eng = s.engine
     # phase timers around the engine's own steps
     t = {"plan_pack_h2d": [], "reduce": [], "d2h_unpack": [], "total": []}
     orig_pack, orig_finish = eng.packer.pack, eng._finish
 
+    def sync_all():
+        for d in eng.devices:
+            torch.cuda.synchronize(d)
+
     def pack(plan, w):
         t0 = time.perf_counter()
         out = orig_pack(plan, w)
-        torch.cuda.synchronize(dev)
+        sync_all()
         t["plan_pack_h2d"].append(time.perf_counter() - t0)
         t["_red0"] = time.perf_counter()
         return out
 
     def finish(plan, results):
-        torch.cuda.synchronize(dev)
+        sync_all()
         t["reduce"].append(time.perf_counter() - t["_red0"])
         t0 = time.perf_counter()
         out = orig_finish(plan, results)
@@ -77,7 +84,7 @@ def main():
     in_bytes = n * p * 4
     out_bytes = p * (8 if a.output == "reference" else 4)
     res = {
-        "config": a.config, "layout": name, "clients": n, "params": p, "output": a.output,
+        "config": a.config, "layout": name, "clients": n, "params": p, "output": a.output, "devices": a.devices,
         "median_s": {k: round(v, 5) for k, v in med.items()},
         "e2e_GiB_s_algorithmic": round((in_bytes + out_bytes) / 2**30 / med["total"], 2),
         "h2d_input_GB": round(in_bytes / 1e9, 3),

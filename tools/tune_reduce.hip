@@ -117,6 +117,20 @@ Variant make_balanced(const float* stack, int64_t stride, int n, const float* w,
           true, {}};
 }
 
+template <int V, int U, int OP, typename T>
+Variant make_blocked(const float* stack, int n, const float* w, int64_t ncols, Epi<T> e, double bytes) {
+  const int64_t B = 256 * V * 4;
+  const int64_t tiles = (ncols + B - 1) / B;
+  char name[96];
+  snprintf(name, sizeof name, "blocked-buf V%d U%d", V, U);
+  return {name, bytes,
+          [=] {
+            hipLaunchKernelGGL((reduce_kernel_blocked<AccF32, T, OP, V, U, true>), dim3((unsigned)tiles), dim3(256),
+                               0, 0, stack, n, w, ncols, e);
+          },
+          false, {}};
+}
+
 int main(int argc, char** argv) {
   const int n = argc > 1 ? atoi(argv[1]) : 100;
   const int64_t ncols = argc > 2 ? atoll(argv[2]) : 11699136;
@@ -134,7 +148,11 @@ int main(int argc, char** argv) {
 
   float *stack, *w, *out32, *prev, *sink, *copy_dst;
   double* v;
-  CK(hipMalloc(&stack, (size_t)n * stride * 4));
+  // room for the column-blocked layout too: every tile (up to 16384 columns) holds N full rows
+  const int64_t blocked_cols = (ncols + 16383) / 16384 * 16384;
+  const size_t stack_elems = (size_t)n * (size_t)(stride > blocked_cols ? stride : blocked_cols);
+  CK(hipMalloc(&stack, stack_elems * 4));
+  CK(hipMemset(stack, 0, stack_elems * 4));
   CK(hipMalloc(&w, n * 4));
   CK(hipMalloc(&out32, stride * 4));
   CK(hipMalloc(&prev, stride * 4));
@@ -201,6 +219,23 @@ int main(int argc, char** argv) {
   vs.push_back(op == FA_OP_AVGM      ? make_balanced<V, U, true, FA_OP_AVGM, double, true>(stack, stride, n, w, ncols, e, bytes, cus, G4) \
                : op == FA_OP_ADAGRAD ? make_balanced<V, U, true, FA_OP_ADAGRAD, double, true>(stack, stride, n, w, ncols, e, bytes, cus, G4) \
                                      : make_balanced<V, U, true, FA_OP_MEAN, double, true>(stack, stride, n, w, ncols, e, bytes, cus, G4))
+#define BLOCKED(V, U)                                                                                    \
+  vs.push_back(op == FA_OP_AVGM      ? make_blocked<V, U, FA_OP_AVGM, double>(stack, n, w, ncols, e, bytes)   \
+               : op == FA_OP_ADAGRAD ? make_blocked<V, U, FA_OP_ADAGRAD, double>(stack, n, w, ncols, e, bytes) \
+                                     : make_blocked<V, U, FA_OP_MEAN, double>(stack, n, w, ncols, e, bytes))
+  if (!strcmp(set, "blocked")) {
+    ONESHOT(16, 1, true);
+    ONESHOTB(16, 1);
+    BALB(16, 1, 0);
+    BLOCKED(16, 1);
+    BLOCKED(16, 2);
+    BLOCKED(8, 1);
+    BLOCKED(8, 2);
+    BLOCKED(4, 4);
+    BLOCKED(4, 8);
+    BLOCKED(2, 8);
+    BLOCKED(1, 16);
+  }
   if (!strcmp(set, "buf")) {
     ONESHOT(16, 1, true);
     ONESHOTB(16, 1);
