@@ -95,6 +95,25 @@ def adaptive_opt(w_local, w_glob, v_t, method, eta=1e-1, tau=1e-9, beta2=0.99):
     return w_local, v_t
 
 
+def dyn_f(w_glob, h, theta, n_clients, alpha=0.01):
+    """dyn.py:17-36 with the state passed explicitly: h is updated IN PLACE (keys whose in-place
+    float update numpy refuses, e.g. int64 BN counters, are skipped, dyn.py:24-29); returns
+    (new w_glob, new theta) — theta becomes w_glob (dyn.py:35)."""
+    delta = {k: w_glob[k] * n_clients - theta[k] for k in h.keys()}
+    skipped = []
+    for k in h.keys():
+        try:
+            h[k] -= alpha / n_clients * delta[k]
+        except Exception:
+            skipped.append(k)
+    w_glob = dict(w_glob)
+    for k in h.keys():
+        if k in skipped:
+            continue
+        w_glob[k] = w_glob[k] - alpha * h[k]
+    return w_glob, w_glob
+
+
 # ---------------------------------------------------------------------------------------------
 # C restatement (liboracle.so)
 # ---------------------------------------------------------------------------------------------
@@ -128,6 +147,8 @@ def lib():
             "ora_update_f64": [I32, P, P, P, D, D, D, D, I64, P],
             "ora_update_f32": [I32, P, P, P, D, D, D, D, I64, P],
             "ora_fill_uniform": [P, I64, I32, I64, ctypes.c_uint64, I64, I64],
+            "ora_update_dyn_f64": [P, P, P, D, D, I64, P],
+            "ora_update_dyn_f32": [P, P, P, D, D, I64, P],
         }.items():
             fn = getattr(L, name)
             fn.argtypes = args
@@ -191,6 +212,22 @@ def c_update(op, g, local32, v, beta=0.9, eta=1e-1, tau=1e-9, beta2=0.99):
         g = np.ascontiguousarray(g)
         out = np.empty(n, np.float32)
         L.ora_update_f32(opi, _ptr(g), _ptr(local32), _ptr(v), beta, eta, tau, beta2, n, _ptr(out))
+    return out
+
+
+def c_update_dyn(g, h32, theta, n_clients, alpha=0.01):
+    """FedDyn update per element (dyn.py:17-36): h32 (fp32) and theta (dtype of g) are updated in
+    place; returns the new w_glob (dtype of g)."""
+    L = lib()
+    assert h32.dtype == np.float32 and h32.flags.c_contiguous and theta.flags.c_contiguous
+    g = np.ascontiguousarray(g)
+    out = np.empty_like(g)
+    if g.dtype == np.float64:
+        assert theta.dtype == np.float64
+        L.ora_update_dyn_f64(_ptr(g), _ptr(h32), _ptr(theta), float(n_clients), alpha, g.size, _ptr(out))
+    else:
+        assert g.dtype == np.float32 and theta.dtype == np.float32
+        L.ora_update_dyn_f32(_ptr(g), _ptr(h32), _ptr(theta), float(n_clients), alpha, g.size, _ptr(out))
     return out
 
 

@@ -172,6 +172,42 @@ void ora_update_f32(int32_t op, const float* g, const float* l, float* v, double
   }
 }
 
+/* FedDyn (dyn.py:17-36), f64 w_glob: d = g*N - theta; h = fl32(h - (alpha/N)*d) computed in f64;
+ * w = g - fl32(fl32(alpha)*h); theta = w.  h and theta are updated in place. */
+void ora_update_dyn_f64(const double* g, float* h, double* theta, double nclients, double alpha,
+                        int64_t n, double* out) {
+  const double c = alpha / nclients;
+  const float a32 = (float)alpha;
+  for (int64_t p = 0; p < n; ++p) {
+    const double gn = g[p] * nclients;
+    const double d = gn - theta[p];
+    const double cd = c * d;
+    const float hn = (float)((double)h[p] - cd);
+    const float ah = a32 * hn;
+    const double w = g[p] - (double)ah;
+    h[p] = hn;
+    theta[p] = w;
+    out[p] = w;
+  }
+}
+
+/* Same with float32 w_glob (np.float32 weights): everything in fp32, c = fl32(alpha/N). */
+void ora_update_dyn_f32(const float* g, float* h, float* theta, double nclients_d, double alpha_d,
+                        int64_t n, float* out) {
+  const float nclients = (float)nclients_d, c = (float)(alpha_d / nclients_d), a32 = (float)alpha_d;
+  for (int64_t p = 0; p < n; ++p) {
+    const float gn = g[p] * nclients;
+    const float d = gn - theta[p];
+    const float cd = c * d;
+    const float hn = h[p] - cd;
+    const float ah = a32 * hn;
+    const float w = g[p] - ah;
+    h[p] = hn;
+    theta[p] = w;
+    out[p] = w;
+  }
+}
+
 /* ---- synthetic generator, identical to the device fill (flearn_amd/csrc/fa_reduce.hip) ---- */
 static uint64_t splitmix64(uint64_t z) {
   z += 0x9E3779B97F4A7C15ull;

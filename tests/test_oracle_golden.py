@@ -10,7 +10,7 @@ from flearn_amd.semantics import KIND_F32, KIND_F64, KIND_I64, resolve
 from golden_io import Golden, assert_dict_bitwise, bitwise_equal, cases
 
 REDUCE_CASES = [c for c in cases() if c.startswith(("avg_", "bn_", "lg_", "trace_"))]
-ROUND_CASES = [c for c in cases() if c.endswith("_rounds3")]
+ROUND_CASES = [c for c in cases() if c.endswith("_rounds3") and not c.startswith("dyn_")]
 
 
 def strategy_keys(g: Golden, clients):
@@ -136,3 +136,51 @@ def test_fixture_inventory():
         assert must in names, must
     for op in ("avgm", "adagrad", "yogi", "adam"):
         assert f"{op}_pyfloat_rounds3" in names and f"{op}_np32_rounds3" in names
+
+
+DYN_CASES = [c for c in cases() if c.startswith("dyn_")]
+
+
+def dyn_round_inputs(g: Golden, r):
+    from golden_io import decode_weight
+
+    keys = g.meta["client_keys"]
+    clients = [{k: g.arrays[f"r{r}x{i}:{k}"].copy() for k in keys} for i in range(g.meta["n_clients"])]
+    return clients, [decode_weight(e) for e in g.meta["round_weights"][r]]
+
+
+@pytest.mark.parametrize("name", DYN_CASES)
+def test_numpy_oracle_dyn_rounds(name):
+    g = Golden(name)
+    h = {k[6:]: v.copy() for k, v in g.arrays.items() if k.startswith("hinit:")}
+    theta = {k: v.copy() for k, v in h.items()}  # Dyn.__init__: theta = deepcopy(h)
+    for r in range(g.meta["rounds"]):
+        clients, weights = dyn_round_inputs(g, r)
+        avg = oracle.server_ensemble(weights, clients)
+        w, theta = oracle.dyn_f(avg, h, theta, len(clients))
+        assert_dict_bitwise(w, g.output(f"w{r}"), f"{name} w{r}")
+        assert_dict_bitwise(h, g.output(f"h{r}"), f"{name} h{r}")
+        assert_dict_bitwise(theta, g.output(f"theta{r}"), f"{name} theta{r}")
+
+
+@pytest.mark.parametrize("name", DYN_CASES)
+def test_c_oracle_dyn_rounds(name, oracle_lib):
+    g = Golden(name)
+    h0 = {k[6:]: v for k, v in g.arrays.items() if k.startswith("hinit:")}
+    fkeys = [k for k, v in h0.items() if v.dtype == np.float32]
+    h = np.concatenate([h0[k].reshape(-1) for k in fkeys]).astype(np.float32)
+    theta = None
+    for r in range(g.meta["rounds"]):
+        clients, weights = dyn_round_inputs(g, r)
+        avg = c_oracle_ensemble(weights, clients, fkeys)
+        gflat = np.concatenate([np.asarray(avg[k]).reshape(-1) for k in fkeys])
+        if theta is None:
+            theta = h.astype(gflat.dtype)
+        w = oracle.c_update_dyn(gflat, h, theta, len(clients))
+        want_w, want_h = g.output(f"w{r}"), g.output(f"h{r}")
+        off = 0
+        for k in fkeys:
+            n = h0[k].size
+            assert bitwise_equal(w[off : off + n].reshape(h0[k].shape), want_w[k]), f"{name} w{r} {k}"
+            assert bitwise_equal(h[off : off + n].reshape(h0[k].shape), want_h[k]), f"{name} h{r} {k}"
+            off += n
