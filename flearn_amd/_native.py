@@ -17,13 +17,13 @@ from pathlib import Path
 import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 
 LIB_PATH = Path(__file__).resolve().parent / "lib" / "libflearn_amd.so"
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 FA_OK = 0
 MODE_W32_DIV64, MODE_W32_DIV32, MODE_W64 = 0, 1, 2
-OP_MEAN, OP_AVGM, OP_ADAGRAD, OP_YOGI, OP_ADAM = 0, 1, 2, 3, 4
+OP_MEAN, OP_AVGM, OP_ADAGRAD, OP_YOGI, OP_ADAM, OP_DYN = 0, 1, 2, 3, 4, 5
 PREC_F32, PREC_F64 = 0, 1
-OP_BY_NAME = {"mean": OP_MEAN, "avgm": OP_AVGM, "adagrad": OP_ADAGRAD, "yogi": OP_YOGI, "adam": OP_ADAM}
+OP_BY_NAME = {"mean": OP_MEAN, "avgm": OP_AVGM, "adagrad": OP_ADAGRAD, "yogi": OP_YOGI, "adam": OP_ADAM, "dyn": OP_DYN}
 
 #: every symbol include/flearn_amd.h declares (checked by tests/test_cabi.py)
 EXPORTS = (
@@ -57,6 +57,9 @@ class Epilogue(ctypes.Structure):
         ("eta", ctypes.c_double),
         ("tau", ctypes.c_double),
         ("beta2", ctypes.c_double),
+        ("h", ctypes.c_void_p),
+        ("alpha", ctypes.c_double),
+        ("n_clients", ctypes.c_double),
     ]
 
 

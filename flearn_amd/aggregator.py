@@ -41,8 +41,8 @@ def _check_cuda(t: torch.Tensor, name: str, dtype: torch.dtype, ndim: int | None
         raise ValueError(f"{name} must be {ndim}-D, got shape {tuple(t.shape)}")
 
 
-def _epilogue(op: int, prev, v, beta=0.9, eta=1e-1, tau=1e-9, beta2=0.99):
-    return na.Epilogue(op, 0, _ptr(prev), _ptr(v), beta, eta, tau, beta2)
+def _epilogue(op: int, prev, v, beta=0.9, eta=1e-1, tau=1e-9, beta2=0.99, h=None, alpha=0.0, n_dyn=0):
+    return na.Epilogue(op, 0, _ptr(prev), _ptr(v), beta, eta, tau, beta2, _ptr(h), alpha, float(n_dyn))
 
 
 # ---------------------------------------------------------------------------------------------
@@ -68,10 +68,13 @@ def reduce_stack(
     eta: float = 1e-1,
     tau: float = 1e-9,
     beta2: float = 0.99,
+    h: torch.Tensor | None = None,
+    alpha: float = 0.01,
 ) -> None:
     """Weighted mean of the fp32 client stack [N, stride] over columns [col_begin, +n_cols)
-    (+ fused update), queued on torch's current stream.  out32/out64/prev/v are indexed from
-    col_begin.  weights: fp32 for MODE_W32_*, f64 for MODE_W64 (device tensors)."""
+    (+ fused update), queued on torch's current stream.  out32/out64/prev/v/h are indexed from
+    col_begin.  weights: fp32 for MODE_W32_*, f64 for MODE_W64 (device tensors).
+    op=OP_DYN: FedDyn with h (fp32, in place) and v = theta (in place); prev unused."""
     L = na.lib()
     _check_cuda(stack, "stack", torch.float32, 2)
     if stack.stride(1) != 1:
@@ -93,7 +96,14 @@ def reduce_stack(
             if t.numel() < ncols or not t.is_contiguous():
                 raise ValueError(f"{name} too small or not contiguous")
     epi = None
-    if op != na.OP_MEAN:
+    if op == na.OP_DYN:
+        vdt = torch.float32 if mode == na.MODE_W32_DIV32 else torch.float64
+        _check_cuda(h, "h", torch.float32)
+        _check_cuda(v, "theta", vdt)
+        if h.numel() < ncols or v.numel() < ncols:
+            raise ValueError("h / theta too small")
+        epi = _epilogue(op, None, v, h=h, alpha=alpha, n_dyn=n)
+    elif op != na.OP_MEAN:
         vdt = torch.float32 if mode == na.MODE_W32_DIV32 else torch.float64
         _check_cuda(prev, "prev", torch.float32)
         _check_cuda(v, "v", vdt)
@@ -144,6 +154,23 @@ def apply_update(op: int, local32, glob, v, *, out32=None, out64=None, beta=0.9,
     epi = _epilogue(op, local32, v, beta, eta, tau, beta2)
     rc = L.fa_opt_apply(prec, ctypes.byref(epi), local32.data_ptr(), glob.data_ptr(), n, _ptr(out32),
                         _ptr(out64), na.stream_handle(local32.device))
+    na.check(rc, "fa_opt_apply")
+
+
+def apply_dyn(glob, h, theta, n_clients: int, alpha: float = 0.01, *, out32=None, out64=None) -> None:
+    """Standalone FedDyn step on a computed mean (dyn.py:17-36): h and theta in place,
+    w -> out32/out64 (which may alias glob / theta)."""
+    L = na.lib()
+    prec = na.PREC_F64 if glob.dtype == torch.float64 else na.PREC_F32
+    _check_cuda(glob, "glob", torch.float64 if prec == na.PREC_F64 else torch.float32)
+    _check_cuda(h, "h", torch.float32)
+    _check_cuda(theta, "theta", glob.dtype)
+    n = glob.numel()
+    if h.numel() != n or theta.numel() != n:
+        raise ValueError("glob / h / theta sizes differ")
+    epi = _epilogue(na.OP_DYN, None, theta, h=h, alpha=alpha, n_dyn=n_clients)
+    rc = L.fa_opt_apply(prec, ctypes.byref(epi), None, glob.data_ptr(), n, _ptr(out32), _ptr(out64),
+                        na.stream_handle(glob.device))
     na.check(rc, "fa_opt_apply")
 
 
@@ -239,6 +266,177 @@ class ServerOptimizer:
         return {s.key: host[s.offset : s.offset + s.numel].reshape(s.shape).copy() for s in plan.f32.segments}
 
 
+def _as_host(v):
+    return v.detach().cpu().numpy() if isinstance(v, torch.Tensor) else v
+
+
+class DynState:
+    """FedDyn server state (flearn/common/strategy/dyn.py:10-36), resident in HBM.
+
+    h      : the caller's dict (a model state_dict).  fp32 entries for fp32 model keys live on the
+             device as one flat fp32 array per column shard, laid out like the f32 bucket, and are
+             updated in place by the fused epilogue; `sync_h()` copies them back into the
+             caller's arrays (the reference mutates them in place, dyn.py:26).  Integer entries
+             (BN counters) are the keys whose in-place float update numpy refuses: the reference
+             skips them (dyn.py:24-31) and so do we — w_glob keeps the plain mean there.
+    theta  : per shard, in the precision numpy gives w_glob (f64 for Python-float weights, fp32
+             for np.float32 weights); starts as a copy of h (dyn.py:14) and becomes w_glob each
+             round (dyn.py:34).
+    One launch per round: mean, delta_theta, h, w and theta for every fp32 column.  When h does
+    not cover every fp32 key, the mean is computed first and the update is applied to the
+    covered column runs only.
+    """
+
+    op = na.OP_DYN
+    name = "dyn"
+
+    def __init__(self, h, alpha: float = 0.01):
+        self.alpha = alpha
+        self.h_host = h
+        self._theta_init = None if h is None else {k: np.array(_as_host(v), copy=True) for k, v in h.items()}
+        self.state = {}  # shard index -> (h fp32, theta)
+        self._sig = None
+        self._tdt = None
+        self._dirty = False
+        self._covered = True
+        self.dev_keys = ()
+        self.skipped = ()
+
+    # -- state management -------------------------------------------------------------------
+    def set_h(self, h):
+        """Replace h (uploaded at the next round); theta is kept."""
+        self.sync_h()
+        if self.state:
+            self._theta_init = self.theta_host()
+        self.h_host, self.state, self._sig = h, {}, None
+
+    def set_theta(self, theta):
+        self.sync_h()
+        self._theta_init = {k: np.array(_as_host(v), copy=True) for k, v in theta.items()}
+        self.state, self._sig = {}, None
+
+    def classify(self, plan: BucketPlan):
+        """(device keys, skipped keys) of h for this plan; raises like the reference would."""
+        if self.h_host is None:
+            raise AttributeError("FedDyn h is None (dyn.py:20 iterates self.h.keys())")
+        dev, skip = [], []
+        for k, hv in self.h_host.items():
+            if k not in plan.key_group:
+                raise KeyError(k)  # dyn.py:21: w_glob[k]
+            a = _as_host(hv)
+            if not isinstance(a, np.ndarray):
+                raise NotImplementedError(f"FedDyn h[{k!r}] is a {type(a).__name__}, expected an array")
+            if np.issubdtype(a.dtype, np.integer) or a.dtype == np.bool_:
+                skip.append(k)  # h[k] -= float array raises in numpy: skipped  dyn.py:24-29
+                continue
+            seg = plan.key_segment[k]
+            if plan.key_group[k] != KIND_F32 or a.dtype != np.float32:
+                raise NotImplementedError(
+                    f"FedDyn h[{k!r}] ({a.dtype}) on a {plan.key_group[k]} key: only fp32 h on fp32 keys runs on the device")
+            if tuple(a.shape) != tuple(seg.shape):
+                raise ValueError(f"FedDyn h[{k!r}] shape {a.shape} != model shape {seg.shape}")
+            dev.append(k)
+        return dev, skip
+
+    def prepare(self, plan: BucketPlan, shards) -> bool:
+        g = plan.f32
+        dev, skip = self.classify(plan)
+        tdt = torch.float32 if g.numerics.out_dtype == np.float32 else torch.float64
+        sig = (tuple((s.key, s.shape) for s in g.segments), tuple(dev),
+               tuple((sh.device, sh.c0, sh.c1) for sh in shards))
+        if not self.state:
+            hflat = np.zeros(g.stride, dtype=np.float32)
+            tflat = np.zeros(g.stride, dtype=np.float64)
+            for k in dev:
+                s = plan.key_segment[k]
+                hflat[s.offset : s.offset + s.numel] = np.asarray(_as_host(self.h_host[k])).reshape(-1)
+                t0 = np.asarray(self._theta_init[k], dtype=np.float64).reshape(-1)
+                tflat[s.offset : s.offset + s.numel] = t0
+            self.state = {
+                sh.index: (torch.from_numpy(hflat[sh.c0 : sh.c1].copy()).to(sh.device),
+                           torch.from_numpy(tflat[sh.c0 : sh.c1].copy()).to(sh.device, tdt))
+                for sh in shards
+            }
+            self._sig, self._tdt = sig, tdt
+        elif sig != self._sig:
+            raise ValueError("model layout changed between FedDyn rounds; set h again")
+        elif tdt != self._tdt:
+            raise TypeError("FedDyn: the weights' type changed between rounds (theta precision)")
+        self.dev_keys, self.skipped = tuple(dev), tuple(skip)
+        self._covered = len(dev) == len(g.segments)
+        self._plan_f32 = g
+        return True
+
+    def step(self, agg: "Aggregator", sh, stack, w, nm: Numerics, want64: bool):
+        """The fused round for one shard: returns the output tensor (theta itself for f64)."""
+        hs, th = self.state[sh.index]
+        f64 = th.dtype == torch.float64
+        self._dirty = True
+        if self._covered:
+            out32 = None if want64 else agg.packer.device_bucket(("out32", KIND_F32, sh.index), (sh.width,),
+                                                                   torch.float32, sh.device)
+            reduce_stack(stack, w, nm.mode, nm.denom, out32=out32, out64=th if want64 else None, op=na.OP_DYN,
+                         v=th, h=hs, alpha=self.alpha)
+            return th if want64 else out32
+        # partial coverage: mean in theta's precision, then the update on the covered runs
+        gbuf = agg.packer.device_bucket(("dyn_g", KIND_F32, sh.index), (sh.width,), th.dtype, sh.device)
+        reduce_stack(stack, w, nm.mode, nm.denom, out32=None if f64 else gbuf, out64=gbuf if f64 else None)
+        for a, b in self._runs(sh):
+            gs = gbuf[a:b]
+            apply_dyn(gs, hs[a:b], th[a:b], stack.shape[0], self.alpha,
+                      out64=gs if f64 else None, out32=None if f64 else gs)
+        if want64 or not f64:
+            return gbuf
+        return gbuf.to(torch.float32)
+
+    def _runs(self, sh):
+        """Maximal column runs [a, b) of device keys within the shard, shard-relative."""
+        segs = sorted((s.offset, s.offset + s.numel) for s in self._plan_f32.segments if s.key in set(self.dev_keys))
+        runs = []
+        for lo, hi in segs:
+            lo, hi = max(lo, sh.c0), min(hi, sh.c1)
+            if lo >= hi:
+                continue
+            if runs and runs[-1][1] == lo - sh.c0:
+                runs[-1][1] = hi - sh.c0
+            else:
+                runs.append([lo - sh.c0, hi - sh.c0])
+        return runs
+
+    # -- host views ---------------------------------------------------------------------------
+    def _host_flat(self, i):
+        return np.concatenate([self.state[j][i].cpu().numpy() for j in sorted(self.state)])
+
+    def sync_h(self):
+        """Copy the device h into the caller's arrays (in place) and return the dict."""
+        if self._dirty and self.state:
+            flat = self._host_flat(0)
+            for k in self.dev_keys:
+                s = self._plan_f32_segment(k)
+                val = flat[s.offset : s.offset + s.numel].reshape(s.shape)
+                dst = self.h_host[k]
+                if isinstance(dst, torch.Tensor):
+                    dst.copy_(torch.from_numpy(val))
+                else:
+                    np.copyto(dst, val)
+            self._dirty = False
+        return self.h_host
+
+    def theta_host(self) -> dict:
+        flat = self._host_flat(1)
+        out = dict(self._theta_init)
+        for k in self.dev_keys:
+            s = self._plan_f32_segment(k)
+            out[k] = flat[s.offset : s.offset + s.numel].reshape(s.shape).copy()
+        return out
+
+    def _plan_f32_segment(self, k):
+        for s in self._plan_f32.segments:
+            if s.key == k:
+                return s
+        raise KeyError(k)
+
+
 # ---------------------------------------------------------------------------------------------
 # the engine behind Strategy.server_ensemble
 # ---------------------------------------------------------------------------------------------
@@ -299,6 +497,8 @@ class Aggregator:
         want64 = self.output == "reference" and nm.out_dtype == _F64
         out64 = (self.packer.device_bucket(("out64", KIND_F32, sh.index), (sh.width,), torch.float64, sh.device)
                  if want64 else None)
+        if isinstance(server_opt, DynState):
+            return server_opt.step(self, sh, stack, w, nm, want64)
         if server_opt is not None and fused:
             # fused: prev is updated in place to fl32(w) — the model clients load next round
             prev, v = server_opt.state[sh.index]

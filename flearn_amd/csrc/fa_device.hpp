@@ -113,7 +113,11 @@ struct Epi {
   T denom;
   const float* prev;
   T* v;
-  T beta, eta, tau, beta2, c;  // c = 1 - beta2 (evaluated in double on the host, as Python does)
+  T beta, eta, tau, beta2, c;  // c = 1 - beta2 (evaluated in double on the host, as Python does);
+                               // FA_OP_DYN: c = alpha / N (a Python float, cast to T by numpy)
+  float* h;                    // FA_OP_DYN: fp32 h; v holds theta
+  T n;                         // FA_OP_DYN: len(w_local_lst)
+  float alpha32;               // FA_OP_DYN: fl32(alpha) — alpha * (fp32 h) stays fp32
   float* out32;
   double* out64;
 };
@@ -154,20 +158,35 @@ __device__ __forceinline__ void finish_quad(const Epi<T>& e, int64_t c, int vali
   typename vec4<T>::type vv = {T(0), T(0), T(0), T(0)};
   typename vec4<float>::type l = {0.f, 0.f, 0.f, 0.f};
   if constexpr (OP != FA_OP_MEAN) {
+    const float* ls = OP == FA_OP_DYN ? e.h : e.prev;  // the fp32 per-column operand
     if (valid == 4) {
-      l = *reinterpret_cast<const typename vec4<float>::type*>(e.prev + c);
+      l = *reinterpret_cast<const typename vec4<float>::type*>(ls + c);
       vv = *reinterpret_cast<const typename vec4<T>::type*>(e.v + c);
     } else {
-      l = load_quad_guarded(e.prev + c, valid);
+      l = load_quad_guarded(ls + c, valid);
       vv = load_quad_guarded(e.v + c, valid);
     }
   }
+  if constexpr (OP == FA_OP_DYN) {
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const T g = (T)acc[j] / e.denom;  // np.divide(w_glob, np.sum(a))  strategy.py:127-129
-    T vj = vv[j];
-    w[j] = update<T, OP>(e, g, (T)l[j], vj);
-    vv[j] = vj;
+    for (int j = 0; j < 4; ++j) {
+      const T g = (T)acc[j] / e.denom;
+      const T d = g * e.n - vv[j];                // delta_theta = w_glob*N - theta   dyn.py:20-21
+      const float hn = (float)((T)l[j] - e.c * d);  // h -= alpha/N * delta (fp32 h)    dyn.py:26
+      const float ah = e.alpha32 * hn;            // alpha * h stays fp32              dyn.py:33
+      w[j] = g - (T)ah;                           // w_glob - alpha*h                  dyn.py:33
+      l[j] = hn;
+      vv[j] = w[j];                               // theta = w_glob                    dyn.py:34
+    }
+    store_quad<float>(e.h + c, l, valid);
+  } else {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const T g = (T)acc[j] / e.denom;  // np.divide(w_glob, np.sum(a))  strategy.py:127-129
+      T vj = vv[j];
+      w[j] = update<T, OP>(e, g, (T)l[j], vj);
+      vv[j] = vj;
+    }
   }
   if constexpr (OP != FA_OP_MEAN) store_quad<T>(e.v + c, vv, valid);
   if (e.out32) {
@@ -438,7 +457,8 @@ __global__ __launch_bounds__(kThreads) void reduce_kernel_blocked(
   if (et.out32) et.out32 += tile * B;
   if (et.out64) et.out64 += tile * B;
   if constexpr (OP != FA_OP_MEAN) {
-    et.prev += tile * B;
+    if (et.prev) et.prev += tile * B;
+    if (et.h) et.h += tile * B;
     et.v += tile * B;
   }
   const int64_t cols = ncols - tile * B < B ? ncols - tile * B : B;

@@ -133,29 +133,42 @@ int dispatch_op(int op, const typename P::x_t* stack, int64_t stride, int n, con
       return launch_reduce<P, T, FA_OP_ADAGRAD>(stack, stride, n, w, col0, ncols, e, s);
     case FA_OP_YOGI: return launch_reduce<P, T, FA_OP_YOGI>(stack, stride, n, w, col0, ncols, e, s);
     case FA_OP_ADAM: return launch_reduce<P, T, FA_OP_ADAM>(stack, stride, n, w, col0, ncols, e, s);
+    case FA_OP_DYN: return launch_reduce<P, T, FA_OP_DYN>(stack, stride, n, w, col0, ncols, e, s);
     default: return fail(FA_ERR_ARG, "unknown epilogue op");
   }
 }
 
 template <typename T>
-int make_epi(const fa_epilogue* in, double denom, float* out32, double* out64, Epi<T>* e) {
+int make_epi(const fa_epilogue* in, double denom, int n_reduced, float* out32, double* out64, Epi<T>* e) {
   e->denom = (T)denom;
   e->prev = nullptr;
   e->v = nullptr;
-  e->beta = e->eta = e->tau = e->beta2 = e->c = T(0);
+  e->h = nullptr;
+  e->beta = e->eta = e->tau = e->beta2 = e->c = e->n = T(0);
+  e->alpha32 = 0.f;
   e->out32 = out32;
   e->out64 = out64;
-  if (in && in->op != FA_OP_MEAN) {
-    if (in->op < FA_OP_AVGM || in->op > FA_OP_ADAM) return fail(FA_ERR_ARG, "unknown epilogue op");
-    if (!in->prev || !in->v) return fail(FA_ERR_ARG, "epilogue needs prev and v");
-    e->prev = in->prev;
-    e->v = static_cast<T*>(in->v);
-    e->beta = (T)in->beta;
-    e->eta = (T)in->eta;
-    e->tau = (T)in->tau;
-    e->beta2 = (T)in->beta2;
-    e->c = (T)(1.0 - in->beta2);  // Python evaluates (1 - self.beta2) in double
+  if (!in || in->op == FA_OP_MEAN) return FA_OK;
+  if (in->op < FA_OP_AVGM || in->op > FA_OP_DYN) return fail(FA_ERR_ARG, "unknown epilogue op");
+  if (!in->v) return fail(FA_ERR_ARG, "epilogue needs v");
+  e->v = static_cast<T*>(in->v);
+  if (in->op == FA_OP_DYN) {
+    if (!in->h) return fail(FA_ERR_ARG, "FedDyn epilogue needs h");
+    const double nc = in->n_clients > 0 ? in->n_clients : (double)n_reduced;
+    if (!(nc >= 1)) return fail(FA_ERR_ARG, "FedDyn epilogue needs n_clients >= 1");
+    e->h = in->h;
+    e->n = (T)nc;
+    e->c = (T)(in->alpha / nc);  // self.alpha / len(w_local_lst): a Python float   dyn.py:26
+    e->alpha32 = (float)in->alpha;
+    return FA_OK;
   }
+  if (!in->prev) return fail(FA_ERR_ARG, "epilogue needs prev and v");
+  e->prev = in->prev;
+  e->beta = (T)in->beta;
+  e->eta = (T)in->eta;
+  e->tau = (T)in->tau;
+  e->beta2 = (T)in->beta2;
+  e->c = (T)(1.0 - in->beta2);  // Python evaluates (1 - self.beta2) in double
   return FA_OK;
 }
 
@@ -163,10 +176,10 @@ bool aligned_to(const void* p, size_t a) { return ((uintptr_t)p % a) == 0; }
 
 // per-column arrays are accessed with 4-element vector loads/stores
 int check_columns(const float* out32, const double* out64, const void* prev, const void* v,
-                  size_t v_elem) {
+                  size_t v_elem, const float* h = nullptr) {
   if (!aligned_to(out32, 16) || !aligned_to(out64, 32) || !aligned_to(prev, 16) ||
-      !aligned_to(v, 4 * v_elem))
-    return fail(FA_ERR_ALIGN, "output / prev / v arrays must be 4-element aligned");
+      !aligned_to(v, 4 * v_elem) || !aligned_to(h, 16))
+    return fail(FA_ERR_ALIGN, "output / prev / v / h arrays must be 4-element aligned");
   return FA_OK;
 }
 
@@ -197,24 +210,25 @@ int fa_reduce_f32(const float* stack, int64_t row_stride, int32_t n_clients, int
   if (n_cols == 0) return FA_OK;
   const int op = epi ? epi->op : FA_OP_MEAN;
   if ((rc = check_columns(out32, out64, epi ? epi->prev : nullptr, epi ? epi->v : nullptr,
-                          mode == FA_MODE_W32_DIV32 ? sizeof(float) : sizeof(double))))
+                          mode == FA_MODE_W32_DIV32 ? sizeof(float) : sizeof(double),
+                          epi ? epi->h : nullptr)))
     return rc;
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (mode == FA_MODE_W32_DIV64) {
     Epi<double> e;
-    if ((rc = make_epi<double>(epi, denom, out32, out64, &e))) return rc;
+    if ((rc = make_epi<double>(epi, denom, n_clients, out32, out64, &e))) return rc;
     return dispatch_op<AccF32, double>(op, stack, row_stride, n_clients, weights, col_begin, n_cols,
                                        e, s);
   }
   if (mode == FA_MODE_W32_DIV32) {
     Epi<float> e;
-    if ((rc = make_epi<float>(epi, denom, out32, out64, &e))) return rc;
+    if ((rc = make_epi<float>(epi, denom, n_clients, out32, out64, &e))) return rc;
     return dispatch_op<AccF32, float>(op, stack, row_stride, n_clients, weights, col_begin, n_cols,
                                       e, s);
   }
   if (mode == FA_MODE_W64) {
     Epi<double> e;
-    if ((rc = make_epi<double>(epi, denom, out32, out64, &e))) return rc;
+    if ((rc = make_epi<double>(epi, denom, n_clients, out32, out64, &e))) return rc;
     return dispatch_op<AccF32W64, double>(op, stack, row_stride, n_clients, weights, col_begin,
                                           n_cols, e, s);
   }
@@ -229,7 +243,7 @@ int fa_reduce_f64(const double* stack, int64_t row_stride, int32_t n_clients,
   if (n_cols == 0) return FA_OK;
   if ((rc = check_columns(nullptr, out64, nullptr, nullptr, 8))) return rc;
   Epi<double> e;
-  make_epi<double>(nullptr, denom, nullptr, out64, &e);
+  make_epi<double>(nullptr, denom, n_clients, nullptr, out64, &e);
   return launch_reduce<AccF64, double, FA_OP_MEAN>(stack, row_stride, n_clients, weights, col_begin,
                                                    n_cols, e, static_cast<hipStream_t>(stream));
 }
@@ -242,23 +256,26 @@ int fa_reduce_i64(const int64_t* stack, int64_t row_stride, int32_t n_clients,
   if (n_cols == 0) return FA_OK;
   if ((rc = check_columns(nullptr, out64, nullptr, nullptr, 8))) return rc;
   Epi<double> e;
-  make_epi<double>(nullptr, denom, nullptr, out64, &e);
+  make_epi<double>(nullptr, denom, n_clients, nullptr, out64, &e);
   return launch_reduce<AccI64, double, FA_OP_MEAN>(stack, row_stride, n_clients, weights, col_begin,
                                                    n_cols, e, static_cast<hipStream_t>(stream));
 }
 
 int fa_opt_apply(int32_t prec, const fa_epilogue* epi, const float* local, const void* glob,
                  int64_t n, float* out32, double* out64, void* stream) {
-  if (!epi || !local || !glob || n < 0) return fail(FA_ERR_ARG, "bad apply arguments");
+  if (!epi || !glob || n < 0) return fail(FA_ERR_ARG, "bad apply arguments");
+  if (!local && epi->op != FA_OP_DYN) return fail(FA_ERR_ARG, "apply needs local");
   if (!out32 && !out64) return fail(FA_ERR_ARG, "no output");
   if (n == 0) return FA_OK;
   if (epi->op == FA_OP_MEAN) return fail(FA_ERR_ARG, "apply needs an optimizer op");
+  if (epi->op == FA_OP_DYN && !(epi->n_clients >= 1))
+    return fail(FA_ERR_ARG, "FedDyn apply needs n_clients >= 1");
   const size_t ve = prec == FA_PREC_F32 ? sizeof(float) : sizeof(double);
-  int rc0 = check_columns(out32, out64, local, epi->v, ve);
+  int rc0 = check_columns(out32, out64, local, epi->v, ve, epi->h);
   if (rc0) return rc0;
   if (!epi->v) return fail(FA_ERR_ARG, "apply needs v");
   fa_epilogue local_epi = *epi;
-  local_epi.prev = local;
+  if (epi->op != FA_OP_DYN) local_epi.prev = local;
   const int64_t blocks = (n + kThreads * 4 - 1) / (kThreads * 4);
   hipStream_t s = static_cast<hipStream_t>(stream);
   int rc;
@@ -267,20 +284,22 @@ int fa_opt_apply(int32_t prec, const fa_epilogue* epi, const float* local, const
                      static_cast<const T*>(glob), n, e)
   if (prec == FA_PREC_F64) {
     Epi<double> e;
-    if ((rc = make_epi<double>(&local_epi, 1.0, out32, out64, &e))) return rc;
+    if ((rc = make_epi<double>(&local_epi, 1.0, 1, out32, out64, &e))) return rc;
     switch (epi->op) {
       case FA_OP_AVGM: FA_APPLY(double, FA_OP_AVGM); break;
       case FA_OP_ADAGRAD: FA_APPLY(double, FA_OP_ADAGRAD); break;
       case FA_OP_YOGI: FA_APPLY(double, FA_OP_YOGI); break;
+      case FA_OP_DYN: FA_APPLY(double, FA_OP_DYN); break;
       default: FA_APPLY(double, FA_OP_ADAM); break;
     }
   } else if (prec == FA_PREC_F32) {
     Epi<float> e;
-    if ((rc = make_epi<float>(&local_epi, 1.0, out32, out64, &e))) return rc;
+    if ((rc = make_epi<float>(&local_epi, 1.0, 1, out32, out64, &e))) return rc;
     switch (epi->op) {
       case FA_OP_AVGM: FA_APPLY(float, FA_OP_AVGM); break;
       case FA_OP_ADAGRAD: FA_APPLY(float, FA_OP_ADAGRAD); break;
       case FA_OP_YOGI: FA_APPLY(float, FA_OP_YOGI); break;
+      case FA_OP_DYN: FA_APPLY(float, FA_OP_DYN); break;
       default: FA_APPLY(float, FA_OP_ADAM); break;
     }
   } else {

@@ -1,12 +1,13 @@
 """Strategy plugins with the reference's names (flearn/common/strategy/__init__.py:1-34).
 
-In scope (server reduce on the MI355X engine): AVG, AVGM, OPT, SGD, Prox, BN, LG, LG_R.
-Out of scope (server-side distillation / different epilogues): DF,
-Distill, Dyn, MD, PAV — not provided; keep using flearn's for those.
+In scope (server reduce on the MI355X engine): AVG, AVGM, OPT, SGD, Prox, BN, LG, LG_R, Dyn.
+Out of scope (server-side distillation / model training): DF, Distill,
+MD, PAV — not provided; keep using flearn's for those.
 """
 from .avg import AVG
 from .avgm import AVGM
 from .bn import BN
+from .dyn import Dyn
 from .lg import LG
 from .lg_reverse import LG_R
 from .opt import OPT
@@ -19,6 +20,7 @@ __all__ = [
     "AVG",
     "AVGM",
     "BN",
+    "Dyn",
     "LG",
     "LG_R",
     "OPT",

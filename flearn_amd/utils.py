@@ -6,7 +6,7 @@ import random
 import numpy as np
 import torch
 
-from .strategy import AVG, AVGM, BN, LG, LG_R, OPT, SGD, Prox
+from .strategy import AVG, AVGM, BN, LG, LG_R, OPT, SGD, Dyn, Prox
 
 __all__ = ["setup_strategy", "setup_seed", "base_strategy_lst", "OUT_OF_SCOPE"]
 
@@ -14,21 +14,24 @@ __all__ = ["setup_strategy", "setup_seed", "base_strategy_lst", "OUT_OF_SCOPE"]
 #: out-of-scope server-side distillation strategies
 base_strategy_lst = ["avg", "avgm", "bn", "lg", "lg_r", "opt", "sgd"]
 #: registry names of the reference that this engine deliberately does not provide
-OUT_OF_SCOPE = ("distill", "dyn", "md", "pav", "df")
+OUT_OF_SCOPE = ("distill", "md", "pav", "df")
 
 
 def setup_strategy(strategy_name, custom_strategy, **strategy_p):
     """Name -> strategy instance, as common/utils.py:16-58.  Unknown names fall back to
     `custom_strategy`, else SystemError.  Extra keyword arguments understood here:
-    shared_key_layers (LG / LG_R), output / device / devices (engine), server_side (AVGM / OPT)."""
+    shared_key_layers (LG / LG_R), h (Dyn), output / device / devices (engine),
+    server_side (AVGM / OPT)."""
     shared_key_layers = strategy_p.get("shared_key_layers", None)
     eng = {k: strategy_p[k] for k in ("output", "device", "devices") if k in strategy_p}
     server_side = strategy_p.get("server_side", False)
+    h = strategy_p.get("h", None)
     name = strategy_name.lower()
     factories = {
         "avg": lambda: AVG(**eng),
         "avgm": lambda: AVGM(server_side=server_side, **eng),
         "bn": lambda: BN(**eng),
+        "dyn": lambda: Dyn(h, **eng),
         "lg": lambda: LG(shared_key_layers, **eng),
         "lg_r": lambda: LG_R(shared_key_layers, **eng),
         "opt": lambda: OPT(server_side=server_side, **eng),

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define FA_ABI_VERSION 1
+#define FA_ABI_VERSION 2
 
 /* return codes */
 #define FA_OK 0
@@ -54,6 +54,10 @@ extern "C" {
 #define FA_OP_ADAGRAD 2 /* d = g - l; v = v + d*d; w = l + (eta*d)/(sqrt(v)+tau)   opt.py:52-63 */
 #define FA_OP_YOGI 3    /* v = v - (c*d*d)*sign(v - d*d), c = 1-beta2               opt.py:54-58 */
 #define FA_OP_ADAM 4    /* v = beta2*v + c*d*d                                      opt.py:59-60 */
+#define FA_OP_DYN 5     /* FedDyn, state h (fp32) and theta (in v):                dyn.py:17-36
+                           d = g*N - theta; h = fl32(h - (alpha/N)*d); w = g - fl32(alpha)*h;
+                           theta = w.  In precision T (F64/F32 below) except h and alpha*h,
+                           which numpy keeps fp32 (h is the model's fp32 state_dict).        */
 
 /* Precision of the epilogue state / the mean (FA_PREC_F64 for modes DIV64 and W64,
  * FA_PREC_F32 for mode DIV32 — the dtype numpy gives w_glob in that mode).                      */
@@ -69,7 +73,12 @@ typedef struct fa_epilogue {
   double eta;        /* OPT step size 1e-1 (opt.py:24)                                  */
   double tau;        /* OPT epsilon 1e-9 (opt.py:25)                                    */
   double beta2;      /* OPT beta2 0.99 (opt.py:27); kernels use c = 1 - beta2 and beta2 */
+  float* h;          /* FA_OP_DYN: [n_cols] fp32 h, updated in place; else NULL          */
+  double alpha;      /* FA_OP_DYN alpha (dyn.py:15, 0.01)                                */
+  double n_clients;  /* FA_OP_DYN len(w_local_lst) (dyn.py:21,26); 0 = the reduce's N    */
 } fa_epilogue;
+/* FA_OP_DYN: v is theta (double* / float*, updated in place to w); prev is unused.  out32 /
+ * out64 may alias v when they have its element type (each element is read before written). */
 
 int fa_abi_version(void);
 const char* fa_last_error(void);

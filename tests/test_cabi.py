@@ -54,16 +54,18 @@ def test_epilogue_struct_layout_matches_c(tmp_path):
     src = tmp_path / "layout.c"
     src.write_text(
         '#include <stddef.h>\n#include <stdio.h>\n#include "flearn_amd.h"\n'
-        "int main(void){printf(\"%zu %zu %zu %zu %zu %zu %zu %zu %zu\\n\", sizeof(fa_epilogue),"
+        "int main(void){printf(\"%zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu\\n\", sizeof(fa_epilogue),"
         "offsetof(fa_epilogue,op),offsetof(fa_epilogue,reserved),offsetof(fa_epilogue,prev),"
         "offsetof(fa_epilogue,v),offsetof(fa_epilogue,beta),offsetof(fa_epilogue,eta),"
-        "offsetof(fa_epilogue,tau),offsetof(fa_epilogue,beta2));return 0;}\n"
+        "offsetof(fa_epilogue,tau),offsetof(fa_epilogue,beta2),offsetof(fa_epilogue,h),"
+        "offsetof(fa_epilogue,alpha),offsetof(fa_epilogue,n_clients));return 0;}\n"
     )
     exe = tmp_path / "layout"
     subprocess.run(["gcc", "-I", str(HEADER.parent), str(src), "-o", str(exe)], check=True)
     c = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True).stdout.split()]
     E = na.Epilogue
-    py = [ctypes.sizeof(E)] + [getattr(E, f).offset for f in ("op", "reserved", "prev", "v", "beta", "eta", "tau", "beta2")]
+    py = [ctypes.sizeof(E)] + [getattr(E, f).offset for f in ("op", "reserved", "prev", "v", "beta", "eta", "tau", "beta2",
+                                                           "h", "alpha", "n_clients")]
     assert c == py
 
 
@@ -98,6 +100,15 @@ def test_unknown_mode_and_op(L):
     assert rc == header_define("FA_ERR_ARG")
     epi = na.Epilogue(na.OP_AVGM, 0, None, None, 0.9, 0.1, 1e-9, 0.99)  # op without state
     rc = L.fa_reduce_f32(FAKE, 64, 2, 0, FAKE, 1.0, 0, 8, ctypes.byref(epi), FAKE, None, None)
+    assert rc == header_define("FA_ERR_ARG")
+    epi = na.Epilogue(na.OP_DYN, 0, None, FAKE, 0, 0, 0, 0, None, 0.01, 0)  # FedDyn without h
+    rc = L.fa_reduce_f32(FAKE, 64, 2, 0, FAKE, 1.0, 0, 8, ctypes.byref(epi), FAKE, None, None)
+    assert rc == header_define("FA_ERR_ARG") and b"h" in L.fa_last_error()
+    epi = na.Epilogue(na.OP_DYN, 0, None, FAKE, 0, 0, 0, 0, FAKE + 4, 0.01, 0)  # misaligned h
+    rc = L.fa_reduce_f32(FAKE, 64, 2, 0, FAKE, 1.0, 0, 8, ctypes.byref(epi), FAKE, None, None)
+    assert rc == header_define("FA_ERR_ALIGN")
+    epi = na.Epilogue(na.OP_DYN, 0, None, FAKE, 0, 0, 0, 0, FAKE, 0.01, 0)  # apply needs N
+    rc = L.fa_opt_apply(na.PREC_F64, ctypes.byref(epi), None, FAKE, 8, None, FAKE, None)
     assert rc == header_define("FA_ERR_ARG")
 
 

@@ -435,3 +435,140 @@ def test_sharded_device_output(cuda):
     got = s.server(upload(g.clients(), g.weights()), 0)["w_glob"]
     for k, w in g.output().items():
         assert bitwise_equal(got[k].cpu().numpy(), np.asarray(w).astype(np.float32)), k
+
+
+# ---------------------------------------------------------------------------------------------
+# FedDyn (dyn.py:10-49): fused h / theta epilogue
+# ---------------------------------------------------------------------------------------------
+DYN_CASES = [c for c in cases() if c.startswith("dyn_")]
+
+
+def _dyn_inputs(g, r):
+    from golden_io import decode_weight
+
+    keys = g.meta["client_keys"]
+    clients = [{k: g.arrays[f"r{r}x{i}:{k}"].copy() for k in keys} for i in range(g.meta["n_clients"])]
+    return clients, [decode_weight(e) for e in g.meta["round_weights"][r]]
+
+
+def _dyn_h0(g):
+    return {k[6:]: v.copy() for k, v in g.arrays.items() if k.startswith("hinit:")}
+
+
+@pytest.mark.parametrize("name", DYN_CASES)
+@pytest.mark.parametrize("shards", [1, 3])
+def test_dyn_strategy_matches_reference(name, shards, cuda):
+    """Dyn(h).server over 3 rounds: w_glob, h (synced back into the caller's arrays) and theta
+    bit-identical to the reference's; integer h entries skipped as dyn.py:24-31 does."""
+    from flearn_amd import Dyn
+
+    g = Golden(name)
+    h = _dyn_h0(g)
+    h_ids = {k: id(v) for k, v in h.items()}
+    s = Dyn(h, devices=[cuda] * shards)
+    for r in range(g.meta["rounds"]):
+        clients, weights = _dyn_inputs(g, r)
+        got = s.server(upload(clients, weights), r)["w_glob"]
+        assert_dict_bitwise(got, g.output(f"w{r}"), f"{name} w{r}")
+        assert s.theta is got  # dyn.py:34
+        hh = s.h
+        assert hh is h and all(id(hh[k]) == h_ids[k] for k in h)  # updated in place
+        assert_dict_bitwise(hh, g.output(f"h{r}"), f"{name} h{r}")
+        dev = s._dyn.dev_keys
+        assert_dict_bitwise({k: v for k, v in s._dyn.theta_host().items() if k in dev},
+                            {k: np.asarray(v) for k, v in g.output(f"theta{r}").items() if k in dev}, f"{name} theta{r}")
+
+
+@pytest.mark.parametrize("name", DYN_CASES)
+def test_dyn_float32_output(name, cuda):
+    from flearn_amd import Dyn
+
+    g = Golden(name)
+    s = Dyn(_dyn_h0(g), output="float32")
+    for r in range(g.meta["rounds"]):
+        clients, weights = _dyn_inputs(g, r)
+        got = s.server(upload(clients, weights), r)["w_glob"]
+        for k, w in g.output(f"w{r}").items():
+            w = np.asarray(w)
+            if k in s._dyn.dev_keys:
+                assert bitwise_equal(np.asarray(got[k]), w.astype(np.float32)), (r, k)
+
+
+def test_dyn_partial_h_matches_numpy_oracle(cuda):
+    """h without some fp32 keys: those keep the plain mean (mean + update on covered runs)."""
+    from flearn_amd import Dyn
+
+    g = Golden("dyn_pyfloat_rounds3")
+    h0 = _dyn_h0(g)
+    for drop in ("bn1.weight", "fc.bias"):
+        h0.pop(drop)
+    h_ora = {k: v.copy() for k, v in h0.items()}
+    theta = {k: v.copy() for k, v in h0.items()}
+    s = Dyn({k: v.copy() for k, v in h0.items()})
+    for r in range(3):
+        clients, weights = _dyn_inputs(g, r)
+        got = s.server(upload(clients, weights), r)["w_glob"]
+        with np.errstate(all="ignore"):
+            avg = oracle.server_ensemble(weights, [{k: v.copy() for k, v in c.items()} for c in clients])
+            want, theta = oracle.dyn_f(avg, h_ora, theta, len(clients))
+        assert_dict_bitwise(got, want, f"partial w{r}")
+        assert_dict_bitwise(s.h, h_ora, f"partial h{r}")
+
+
+def test_dyn_errors_like_reference(cuda):
+    from flearn_amd import Dyn
+
+    g = Golden("dyn_pyfloat_rounds3")
+    clients, weights = _dyn_inputs(g, 0)
+    h = _dyn_h0(g)
+    h["not.a.key"] = np.zeros(3, np.float32)
+    with pytest.raises(KeyError):
+        Dyn(h).server(upload(clients, weights), 0)
+    with pytest.raises(AttributeError):
+        Dyn(None).server(upload(clients, weights), 0)
+    s = Dyn(_dyn_h0(g))
+    s.server(upload(clients, weights), 0)
+    with pytest.raises(SystemExit):  # theta precision would change (f64 -> fp32): refused
+        s.server(upload(clients, [np.float32(w) for w in weights]), 1)
+
+
+@pytest.mark.parametrize("prec", ["f64", "f32", "w64"])
+@pytest.mark.parametrize("p", [1, 4093, 5001, 8388608 + 5])
+def test_dyn_epilogue_vs_c_oracle(prec, p, cuda):
+    """Kernel level, 2 rounds with state carried: fused reduce+FedDyn vs the C restatement,
+    small (balanced grid) and big-tile (buffer-descriptor path, ragged tail) buckets."""
+    n = 7 if p < 10**6 else 3
+    stride = -(-p // 64) * 64
+    mode = {"f64": na.MODE_W32_DIV64, "f32": na.MODE_W32_DIV32, "w64": na.MODE_W64}[prec]
+    tdt = torch.float32 if prec == "f32" else torch.float64
+    h = torch.empty((1, stride), dtype=torch.float32, device=cuda)
+    agg.fill_uniform(h, seed=41)
+    h = h[0] * 0.01
+    h_ora = h[:p].cpu().numpy().copy()
+    theta = h.to(tdt, copy=True)
+    th_ora = theta[:p].cpu().numpy().copy()
+    for r in range(2):
+        x = _device_stack(n, stride, seed=100 + r)
+        wv = np.linspace(0.5, 2.0, n)
+        w = wv.astype(np.float64 if prec == "w64" else np.float32)
+        denom = float(np.sum([float(v) for v in wv])) if prec == "f64" else float(np.sum(w))
+        out = torch.empty(p, dtype=tdt, device=cuda)
+        kw = {"out64": out} if tdt == torch.float64 else {"out32": out}
+        agg.reduce_stack(x, torch.from_numpy(w).to(cuda), mode, denom, n_cols=p, op=na.OP_DYN, h=h, v=theta, **kw)
+        gm = oracle.c_reduce(mode, x[:, :p].cpu().numpy(), w, denom)
+        want = oracle.c_update_dyn(gm, h_ora, th_ora, n)
+        assert bitwise_equal(out.cpu().numpy(), want), r
+        assert bitwise_equal(h[:p].cpu().numpy(), h_ora), r
+        assert bitwise_equal(theta[:p].cpu().numpy(), th_ora), r
+
+
+def test_dyn_apply_vs_c_oracle(cuda):
+    p = 10007
+    g = torch.rand(p, dtype=torch.float64, device=cuda)
+    h = (torch.rand(p, device=cuda) * 0.1).float()
+    th = torch.rand(p, dtype=torch.float64, device=cuda)
+    g_h, h_h, th_h = g.cpu().numpy(), h.cpu().numpy().copy(), th.cpu().numpy().copy()
+    agg.apply_dyn(g, h, th, 9, 0.05, out64=g)  # in place on the mean
+    want = oracle.c_update_dyn(g_h, h_h, th_h, 9, alpha=0.05)
+    assert bitwise_equal(g.cpu().numpy(), want)
+    assert bitwise_equal(h.cpu().numpy(), h_h) and bitwise_equal(th.cpu().numpy(), th_h)

@@ -141,9 +141,13 @@ def test_registry_mirrors_reference():
     assert flearn_amd.setup_strategy("mystrategy", custom) is custom
     with pytest.raises(SystemError):
         flearn_amd.setup_strategy("nope", None)
-    for name in ("dyn", "md", "pav", "distill"):
+    for name in ("md", "pav", "distill"):
         with pytest.raises(NotImplementedError):
             flearn_amd.setup_strategy(name, None)
+    h = {"w": np.zeros(3, np.float32)}
+    d = flearn_amd.setup_strategy("dyn", None, h=h)
+    assert type(d).__name__ == "Dyn" and d.alpha == 0.01 and d.h is h
+    assert d.theta is not h and np.array_equal(d.theta["w"], h["w"])  # dyn.py:14 deepcopy
 
 
 def test_conversions_mirror_reference():
