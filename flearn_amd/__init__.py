@@ -9,7 +9,7 @@ Drop-in use with an unchanged flearn server:
 The hot path (Strategy.server -> server_ensemble) runs hand-written HIP kernels for gfx950
 through the C ABI in include/flearn_amd.h; there is no CPU fallback.
 """
-from .strategy import AVG, AVGM, BN, LG, LG_R, OPT, SGD, BaseEncrypt, Dyn, ParentStrategy, Prox, Strategy
+from .strategy import AVG, AVGM, BN, LG, LG_R, OPT, SGD, BaseEncrypt, Distill, Dyn, ParentStrategy, Prox, Strategy
 from .strategy import convert_to_np, convert_to_tensor
 from .utils import base_strategy_lst, setup_seed, setup_strategy
 
@@ -19,6 +19,7 @@ __all__ = [
     "AVG",
     "AVGM",
     "BN",
+    "Distill",
     "Dyn",
     "LG",
     "LG_R",

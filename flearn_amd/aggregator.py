@@ -189,6 +189,44 @@ def fill_uniform(dst: torch.Tensor, seed: int, row_begin: int = 0, col_begin: in
         na.check(rc, "fa_fill_uniform_f32")
 
 
+def mean_tables(tables, device=None):
+    """FedDistill's logits mean (distill.py:42-46) on the device: user_logits = 0, += each table
+    in list order, / len(tables), in the tables' dtype (fp32 or f64), bit-identical to torch /
+    numpy on the host.  One reduce launch over a [N+1, C*C] stack whose row 0 is zeros with
+    weight 1 (so the sum starts from +0.0 exactly as `0 + t0` does) and weights 1 elsewhere.
+    Returns the container type of tables[0] (torch tensor on its device, or ndarray)."""
+    if len(tables) == 0:
+        raise ZeroDivisionError("division by zero")  # 0 / len([])  distill.py:46
+    first = tables[0]
+    as_torch = isinstance(first, torch.Tensor)
+    host = [t.detach().cpu().numpy() if isinstance(t, torch.Tensor) else np.asarray(t) for t in tables]
+    dt, shape = host[0].dtype, host[0].shape
+    for a in host[1:]:
+        if a.dtype != dt or a.shape != shape:
+            raise ValueError(f"logits tables differ: {a.dtype}{a.shape} vs {dt}{shape}")
+    if dt not in (np.float32, np.float64):
+        raise NotImplementedError(f"logits dtype {dt}: the device mean handles float32 / float64 tables")
+    dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    n, m = len(host), int(np.prod(shape, dtype=np.int64))
+    stride = max(64, -(-m // 64) * 64)
+    stack = np.zeros((n + 1, stride), dtype=dt)
+    for i, a in enumerate(host):
+        stack[i + 1, :m] = a.reshape(-1)
+    tdt = torch.float32 if dt == np.float32 else torch.float64
+    with torch.cuda.device(dev):
+        sd = torch.from_numpy(stack).to(dev)
+        w = torch.ones(n + 1, dtype=tdt, device=dev)
+        out = torch.empty(stride, dtype=tdt, device=dev)
+        if tdt == torch.float32:
+            reduce_stack(sd, w, na.MODE_W32_DIV32, float(n), out32=out)  # fp32 sum, fp32 / fl32(N)
+        else:
+            reduce_stack_f64(sd, w, float(n), out)
+        res = out[:m].view(shape)
+        if as_torch:
+            return res.to(first.device).clone() if first.device != dev else res.clone()
+        return res.cpu().numpy()
+
+
 # ---------------------------------------------------------------------------------------------
 # server-side optimizer state
 # ---------------------------------------------------------------------------------------------

@@ -1,12 +1,13 @@
 """Strategy plugins with the reference's names (flearn/common/strategy/__init__.py:1-34).
 
-In scope (server reduce on the MI355X engine): AVG, AVGM, OPT, SGD, Prox, BN, LG, LG_R, Dyn.
-Out of scope (server-side distillation / model training): DF, Distill,
-MD, PAV — not provided; keep using flearn's for those.
+In scope (server reduce on the MI355X engine): AVG, AVGM, OPT, SGD, Prox, BN, LG, LG_R, Dyn,
+Distill.  Out of scope (server-side model training): DF, MD, PAV — not
+provided; keep using flearn's for those.
 """
 from .avg import AVG
 from .avgm import AVGM
 from .bn import BN
+from .distill import Distill
 from .dyn import Dyn
 from .lg import LG
 from .lg_reverse import LG_R
@@ -20,6 +21,7 @@ __all__ = [
     "AVG",
     "AVGM",
     "BN",
+    "Distill",
     "Dyn",
     "LG",
     "LG_R",

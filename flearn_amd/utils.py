@@ -6,7 +6,7 @@ import random
 import numpy as np
 import torch
 
-from .strategy import AVG, AVGM, BN, LG, LG_R, OPT, SGD, Dyn, Prox
+from .strategy import AVG, AVGM, BN, LG, LG_R, OPT, SGD, Distill, Dyn, Prox
 
 __all__ = ["setup_strategy", "setup_seed", "base_strategy_lst", "OUT_OF_SCOPE"]
 
@@ -14,7 +14,7 @@ __all__ = ["setup_strategy", "setup_seed", "base_strategy_lst", "OUT_OF_SCOPE"]
 #: out-of-scope server-side distillation strategies
 base_strategy_lst = ["avg", "avgm", "bn", "lg", "lg_r", "opt", "sgd"]
 #: registry names of the reference that this engine deliberately does not provide
-OUT_OF_SCOPE = ("distill", "md", "pav", "df")
+OUT_OF_SCOPE = ("md", "pav")
 
 
 def setup_strategy(strategy_name, custom_strategy, **strategy_p):
@@ -31,6 +31,7 @@ def setup_strategy(strategy_name, custom_strategy, **strategy_p):
         "avg": lambda: AVG(**eng),
         "avgm": lambda: AVGM(server_side=server_side, **eng),
         "bn": lambda: BN(**eng),
+        "distill": lambda: Distill(**eng),
         "dyn": lambda: Dyn(h, **eng),
         "lg": lambda: LG(shared_key_layers, **eng),
         "lg_r": lambda: LG_R(shared_key_layers, **eng),

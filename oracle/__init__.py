@@ -6,8 +6,9 @@ never imports it; the product fails loudly when its HIP library is missing.
 
 Two restatements of the reference (wnma3mz/flearn v0.0.5) arithmetic:
 
-* ``server_ensemble`` / ``mean_momentum`` / ``adaptive_opt`` — numpy op-sequence restatements
-  of ``flearn/common/strategy/strategy.py:102-130``, ``avgm.py:19-36`` and ``opt.py:23-65``: the
+* ``server_ensemble`` / ``mean_momentum`` / ``adaptive_opt`` / ``dyn_f`` / ``logits_mean`` — numpy
+  op-sequence restatements of ``flearn/common/strategy/strategy.py:102-130``, ``avgm.py:19-36``,
+  ``opt.py:23-65``, ``dyn.py:17-36`` and ``distill.py:42-46``: the
   same ufunc calls in the same order, so numpy applies the same (NEP 50) promotions.  This is
   "flearn's CPU path" timed by bench.py.
 * ``c_reduce`` / ``c_update`` — the per-element C restatement (``fa_oracle.c``, strict IEEE, no
@@ -112,6 +113,18 @@ def dyn_f(w_glob, h, theta, n_clients, alpha=0.01):
             continue
         w_glob[k] = w_glob[k] - alpha * h[k]
     return w_glob, w_glob
+
+
+def logits_mean(logits_lst):
+    """Distill.aggregate_logits (distill.py:42-46): user_logits = 0; user_logits += item for each
+    table in list order (0 + t0 makes a fresh array: -0.0 becomes +0.0); / len(logits_lst) in the
+    tables' dtype.  torch tensors are restated through numpy (same IEEE fp32/f64 ops, and torch's
+    CPU true-divide by a Python int is the correctly rounded division, checked by the fixtures)."""
+    arrs = [np.asarray(t.numpy() if hasattr(t, "numpy") else t) for t in logits_lst]
+    acc = 0
+    for a in arrs:
+        acc += a
+    return acc / len(arrs)
 
 
 # ---------------------------------------------------------------------------------------------

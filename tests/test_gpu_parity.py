@@ -572,3 +572,40 @@ def test_dyn_apply_vs_c_oracle(cuda):
     want = oracle.c_update_dyn(g_h, h_h, th_h, 9, alpha=0.05)
     assert bitwise_equal(g.cpu().numpy(), want)
     assert bitwise_equal(h.cpu().numpy(), h_h) and bitwise_equal(th.cpu().numpy(), th_h)
+
+
+# ---------------------------------------------------------------------------------------------
+# FedDistill (distill.py:26-46): logits mean on the device
+# ---------------------------------------------------------------------------------------------
+DISTILL_CASES = [c for c in cases() if c.startswith("distill_logits_")]
+
+
+@pytest.mark.parametrize("name", DISTILL_CASES)
+def test_distill_logits_mean_matches_reference(name, cuda):
+    from flearn_amd import Distill
+
+    g = Golden(name)
+    tabs = [g.arrays[f"logits{i}"] for i in range(g.meta["n_clients"])]
+    if g.meta["logits_kind"].startswith("torch"):
+        tabs = [torch.from_numpy(t.copy()) for t in tabs]
+    got = Distill.aggregate_logits(tabs)
+    if g.meta["logits_kind"].startswith("torch"):
+        assert isinstance(got, torch.Tensor) and got.device.type == "cpu"
+        got = got.numpy()
+    else:
+        assert isinstance(got, np.ndarray)
+    assert_dict_bitwise({"glob_logits": got}, g.output(), name)
+
+
+def test_distill_server_matches_reference(cuda):
+    from flearn_amd import Distill
+
+    g = Golden("distill_server_n4")
+    ups = upload(g.clients(), g.weights())
+    for i, u in enumerate(ups):
+        u["logits"] = torch.from_numpy(g.arrays[f"logits{i}"].copy())
+    res = Distill().server(ups, 0)
+    assert_dict_bitwise(res["w_glob"], g.output(), "distill w_glob")
+    assert_dict_bitwise({"glob_logits": res["glob_logits"].numpy()}, g.output("glob"), "distill glob_logits")
+    with pytest.raises(ZeroDivisionError):
+        Distill.aggregate_logits([])

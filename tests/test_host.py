@@ -141,7 +141,8 @@ def test_registry_mirrors_reference():
     assert flearn_amd.setup_strategy("mystrategy", custom) is custom
     with pytest.raises(SystemError):
         flearn_amd.setup_strategy("nope", None)
-    for name in ("md", "pav", "distill"):
+    assert type(flearn_amd.setup_strategy("distill", None)).__name__ == "Distill"
+    for name in ("md", "pav"):
         with pytest.raises(NotImplementedError):
             flearn_amd.setup_strategy(name, None)
     h = {"w": np.zeros(3, np.float32)}

@@ -184,3 +184,23 @@ def test_c_oracle_dyn_rounds(name, oracle_lib):
             assert bitwise_equal(w[off : off + n].reshape(h0[k].shape), want_w[k]), f"{name} w{r} {k}"
             assert bitwise_equal(h[off : off + n].reshape(h0[k].shape), want_h[k]), f"{name} h{r} {k}"
             off += n
+
+
+DISTILL_CASES = [c for c in cases() if c.startswith("distill_logits_")]
+
+
+@pytest.mark.parametrize("name", DISTILL_CASES)
+def test_numpy_oracle_logits_mean(name):
+    g = Golden(name)
+    tabs = [g.arrays[f"logits{i}"] for i in range(g.meta["n_clients"])]
+    with np.errstate(all="ignore"):
+        got = oracle.logits_mean(tabs)
+    assert_dict_bitwise({"glob_logits": got}, g.output(), name)
+
+
+def test_numpy_oracle_distill_server():
+    g = Golden("distill_server_n4")
+    clients, weights = g.clients(), g.weights()
+    assert_dict_bitwise(oracle.server_ensemble(weights, clients), g.output(), "distill w_glob")
+    tabs = [g.arrays[f"logits{i}"] for i in range(4)]
+    assert_dict_bitwise({"glob_logits": oracle.logits_mean(tabs)}, g.output("glob"), "distill logits")
