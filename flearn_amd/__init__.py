@@ -12,6 +12,7 @@ through the C ABI in include/flearn_amd.h; there is no CPU fallback.
 from .strategy import AVG, AVGM, BN, LG, LG_R, OPT, SGD, BaseEncrypt, Distill, Dyn, ParentStrategy, Prox, Strategy
 from .strategy import convert_to_np, convert_to_tensor
 from .utils import base_strategy_lst, setup_seed, setup_strategy
+from .wire import Encrypt
 
 __version__ = "0.1.0"
 
@@ -29,6 +30,7 @@ __all__ = [
     "Strategy",
     "ParentStrategy",
     "BaseEncrypt",
+    "Encrypt",
     "convert_to_np",
     "convert_to_tensor",
     "setup_strategy",

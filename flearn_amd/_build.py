@@ -9,6 +9,7 @@ from pathlib import Path
 HERE = Path(__file__).resolve().parent
 REPO = HERE.parent
 SOURCES = [HERE / "csrc" / "fa_reduce.hip"]
+HOST_SOURCES = [HERE / "csrc" / "fa_wire.cpp"]  # plain host C++ (g++), linked into the same .so
 DEPS = [HERE / "csrc" / "fa_device.hpp"]
 HEADERS = [REPO / "include" / "flearn_amd.h"]
 OUT = HERE / "lib" / "libflearn_amd.so"
@@ -23,28 +24,45 @@ def hipcc() -> str:
 
 
 def build_native(force: bool = False, verbose: bool = False) -> Path:
-    newest = max(p.stat().st_mtime for p in SOURCES + DEPS + HEADERS + [Path(__file__)])
+    newest = max(p.stat().st_mtime for p in SOURCES + HOST_SOURCES + DEPS + HEADERS + [Path(__file__)])
     if OUT.exists() and not force and OUT.stat().st_mtime >= newest:
         return OUT
     OUT.parent.mkdir(parents=True, exist_ok=True)
     tmp = OUT.with_suffix(".so.tmp")
-    cmd = [
-        hipcc(),
-        f"--offload-arch={ARCH}",
-        "-O3",
-        "-std=c++17",
-        "-fPIC",
-        "-shared",
-        "-ffp-contract=off",  # bit-parity: no fused multiply-add anywhere in the reduce
-        "-Wall",
-        f"-I{REPO / 'include'}",
-        "-o",
-        str(tmp),
-        *map(str, SOURCES),
-    ]
+    objs = []
+    for src in HOST_SOURCES:
+        obj = OUT.parent / (src.stem + ".o")
+        hcmd = [os.environ.get("CXX", "g++"), "-O3", "-std=c++17", "-fPIC", "-pthread", "-Wall",
+                f"-I{REPO / 'include'}", "-c", str(src), "-o", str(obj)]
+        if verbose:
+            print(" ".join(hcmd))
+        subprocess.run(hcmd, check=True)
+        objs.append(str(obj))
+    dev_objs = []
+    for src in SOURCES:  # device code: compile, then link with the host objects
+        obj = OUT.parent / (src.stem + ".o")
+        cmd = [
+            hipcc(),
+            f"--offload-arch={ARCH}",
+            "-O3",
+            "-std=c++17",
+            "-fPIC",
+            "-ffp-contract=off",  # bit-parity: no fused multiply-add anywhere in the reduce
+            "-Wall",
+            f"-I{REPO / 'include'}",
+            "-c",
+            str(src),
+            "-o",
+            str(obj),
+        ]
+        if verbose:
+            print(" ".join(cmd))
+        subprocess.run(cmd, check=True)
+        dev_objs.append(str(obj))
+    link = [hipcc(), f"--offload-arch={ARCH}", "-fPIC", "-shared", "-pthread", "-o", str(tmp), *dev_objs, *objs]
     if verbose:
-        print(" ".join(cmd))
-    subprocess.run(cmd, check=True)
+        print(" ".join(link))
+    subprocess.run(link, check=True)
     tmp.replace(OUT)
     return OUT
 

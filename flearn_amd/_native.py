@@ -17,9 +17,11 @@ from pathlib import Path
 import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 
 LIB_PATH = Path(__file__).resolve().parent / "lib" / "libflearn_amd.so"
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 FA_OK = 0
+FA_ERR_ARG, FA_ERR_ALIGN, FA_ERR_LAUNCH = -1, -2, -3
+FA_ERR_SIZE, FA_ERR_UNSUPPORTED, FA_ERR_DATA = -4, -5, -6
 MODE_W32_DIV64, MODE_W32_DIV32, MODE_W64 = 0, 1, 2
 OP_MEAN, OP_AVGM, OP_ADAGRAD, OP_YOGI, OP_ADAM, OP_DYN = 0, 1, 2, 3, 4, 5
 PREC_F32, PREC_F64 = 0, 1
@@ -34,6 +36,13 @@ EXPORTS = (
     "fa_reduce_i64",
     "fa_opt_apply",
     "fa_fill_uniform_f32",
+    "fa_b64_decoded_size",
+    "fa_b64_decode",
+    "fa_b64_decode_ranges",
+    "fa_b64_encode",
+    "fa_pickle_scan_b64",
+    "fa_pickle_scan",
+    "fa_wire_last_error",
 )
 
 
@@ -87,6 +96,13 @@ def load(require_gpu: bool = False):
                 "fa_reduce_i64": ([P, I64, I32, P, D, I64, I64, P, P], ctypes.c_int),
                 "fa_opt_apply": ([I32, ctypes.POINTER(Epilogue), P, P, I64, P, P, P], ctypes.c_int),
                 "fa_fill_uniform_f32": ([P, I64, I32, I64, ctypes.c_uint64, I64, I64, P], ctypes.c_int),
+                "fa_b64_decoded_size": ([P, I64], I64),
+                "fa_b64_decode": ([P, I64, P, I64, I32], ctypes.c_int),
+                "fa_b64_decode_ranges": ([P, I64, I32, P, P, P, I32], ctypes.c_int),
+                "fa_b64_encode": ([P, I64, P, I64, I32], ctypes.c_int),
+                "fa_pickle_scan_b64": ([P, I64, P, I64, ctypes.POINTER(I64)], ctypes.c_int),
+                "fa_pickle_scan": ([P, I64, P, I64, ctypes.POINTER(I64)], ctypes.c_int),
+                "fa_wire_last_error": ([], ctypes.c_char_p),
             }
             for name, (args, res) in sig.items():
                 fn = getattr(L, name)

@@ -176,6 +176,7 @@ class Packer:
         self._pinned = {}
         self._dev = {}
         self._shards = {}
+        self.last_wire_rows = 0
 
     def _buf(self, cache, key, shape, dtype, **kw):
         t = cache.get(key)
@@ -226,21 +227,39 @@ class Packer:
                     for s, a, b, sh, d in pieces:
                         devs[sh.index][n, d : d + (b - a)].copy_(w[s.key].reshape(-1)[a:b])
             else:
-                hosts = [self._buf(self._pinned, ("in", kind, sh.index), (plan.n_clients, sh.width), tdt,
-                                   pin_memory=True) for sh in shards]
-                self._pack_pipelined(plan, pieces, w_local_lst, shards, hosts, devs)
+                rows = self._wire_rows(g, w_local_lst) if kind == KIND_F32 else [None] * plan.n_clients
+                if all(r is not None for r in rows):
+                    hosts = [None] * len(shards)  # every row already sits in pinned memory
+                else:
+                    hosts = [self._buf(self._pinned, ("in", kind, sh.index), (plan.n_clients, sh.width), tdt,
+                                       pin_memory=True) for sh in shards]
+                self._pack_pipelined(plan, pieces, w_local_lst, shards, hosts, devs, rows)
             out[kind] = list(zip(shards, devs))
         return out
 
-    def _pack_pipelined(self, plan: BucketPlan, pieces, w_local_lst, shards, hosts, devs):
+    def _wire_rows(self, g: Group, w_local_lst) -> list:
+        """Per client: the pinned row the wire codec decoded its fp32 params into, when that row
+        is laid out exactly as this bucket (flearn_amd.wire.decode) — else None."""
+        from .wire import wire_row
+
+        sig = tuple((s.key, s.shape, s.offset) for s in g.segments) + (g.stride,)
+        rows = [wire_row(w, sig) for w in w_local_lst]
+        self.last_wire_rows = sum(r is not None for r in rows)
+        return rows
+
+    def _pack_pipelined(self, plan: BucketPlan, pieces, w_local_lst, shards, hosts, devs, rows=None):
         """Host ingest: client rows are packed into pinned staging by a thread pool, chunk by
         chunk, and each finished chunk's H2D copies (one per shard, on that device's stream) are
         queued at once, so the DMA of chunk k runs while the CPU packs chunk k+1 (flearn's
         uploads are pageable host arrays: they must be copied once into pinned memory before a
-        DMA engine can read them)."""
-        host_np = [h.numpy() for h in hosts]
+        DMA engine can read them).  Clients whose fp32 params the wire codec decoded straight
+        into a pinned row of this layout (`rows[n]`) skip the pack and are DMA'd from there."""
+        rows = rows if rows is not None else [None] * plan.n_clients
+        host_np = [h.numpy() if h is not None else None for h in hosts]
 
         def fill(n):
+            if rows[n] is not None:
+                return
             w = w_local_lst[n]
             cache = {}
             for s, a, b, sh, d in pieces:
@@ -255,11 +274,21 @@ class Packer:
         def ship(lo, hi):
             for sh, h, dv in zip(shards, hosts, devs):
                 with torch.cuda.device(sh.device):
-                    dv[lo:hi].copy_(h[lo:hi], non_blocking=True)
+                    r = lo
+                    while r < hi:
+                        if rows[r] is not None:
+                            dv[r].copy_(rows[r][sh.c0 : sh.c1], non_blocking=True)
+                            r += 1
+                            continue
+                        e = r
+                        while e < hi and rows[e] is None:
+                            e += 1
+                        dv[r:e].copy_(h[r:e], non_blocking=True)
+                        r = e
 
         n = plan.n_clients
         workers = max(1, min(self.workers, n))
-        if workers == 1:
+        if workers == 1 or all(r is not None for r in rows):
             for r in range(n):
                 fill(r)
             ship(0, n)

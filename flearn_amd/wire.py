@@ -1,0 +1,440 @@
+"""Wire codec — drop-in for flearn's ``Encrypt`` (flearn/common/Encrypt.py:17-44).
+
+flearn's HTTP mode moves every upload and every global model as ``base64(pickle.dumps(obj))``:
+clients encode in ``Client.upload`` (Client.py:201), the server decodes each upload in
+``Server.ensemble`` (Server.py:126-131) and encodes the result (Server.py:142).  The reference
+does this with ``base64.b64decode`` + ``pickle.loads`` on one core, after which the numpy arrays
+are copied once more into the aggregation input.
+
+``Encrypt`` here keeps the format byte for byte and makes the server side one pass:
+
+* ``decode`` — a native restricted pickle scanner (flearn_amd/csrc/fa_wire.cpp) walks the pickle
+  *through* the base64 text, decoding only its small header pieces, and reports every array
+  payload as a (decoded offset, length) range.  The fp32 arrays of an upload's ``params`` are
+  then decoded by a thread pool straight into ONE pinned row laid out exactly as the
+  aggregation bucket (bucket.make_plan: key order, 64-element alignment), and handed back as
+  numpy views of it — a plain dict of plain ndarrays, equal to what ``pickle.loads`` returns.
+  When the engine later aggregates those uploads, the Packer recognises the rows and DMAs them
+  to the GPU as they are (no pack copy).
+* ``encode`` — ``pickle.dumps`` (the reference's bytes) + a multi-threaded base64 encoder
+  writing directly into the result ``str``.
+
+Safety: pickle content outside the scanner's subset (e.g. torch tensors) goes through a
+*restricted* unpickler that only resolves numpy / torch / collections reconstructors; any other
+global raises ``pickle.UnpicklingError`` — the reference's ``pickle.loads`` would execute it.
+"""
+from __future__ import annotations
+
+import base64
+import codecs
+import collections
+import ctypes
+import io
+import json
+import os
+import pickle
+import threading
+import weakref
+
+import numpy as np
+import torch
+
+from . import _native as na
+from .bucket import ALIGN
+
+__all__ = ["BaseEncrypt", "Encrypt", "b64encode", "b64decode", "wire_row"]
+
+_F32 = np.dtype("<f4")
+
+# CPython C API: zero-copy access to the bytes of an ASCII str, and str allocation
+_AsUTF8AndSize = ctypes.pythonapi.PyUnicode_AsUTF8AndSize
+_AsUTF8AndSize.restype = ctypes.c_void_p
+_AsUTF8AndSize.argtypes = [ctypes.py_object, ctypes.POINTER(ctypes.c_ssize_t)]
+_PyUnicode_New = ctypes.pythonapi.PyUnicode_New
+_PyUnicode_New.restype = ctypes.py_object
+_PyUnicode_New.argtypes = [ctypes.c_ssize_t, ctypes.c_uint32]
+
+
+def _threads() -> int:
+    return max(1, min(16, os.cpu_count() or 1))
+
+
+def _ascii_ptr(s: str) -> tuple[int, int]:
+    """(address, length) of the internal buffer of an ASCII str (no copy)."""
+    size = ctypes.c_ssize_t()
+    p = _AsUTF8AndSize(s, ctypes.byref(size))
+    if not p:
+        raise ValueError("string has no UTF-8 view")
+    return p, size.value
+
+
+def _check(L, rc, what):
+    if rc != na.FA_OK:
+        msg = L.fa_wire_last_error().decode(errors="replace")
+        raise _WireError(rc, f"{what}: {msg}")
+
+
+class _WireError(ValueError):
+    def __init__(self, code, msg):
+        super().__init__(msg)
+        self.code = code
+
+
+# ---------------------------------------------------------------------------------------------
+# base64
+# ---------------------------------------------------------------------------------------------
+
+
+def b64encode(raw) -> str:
+    """base64.b64encode(raw).decode() with the native encoder, written into the new str."""
+    L = na.load()
+    mv = memoryview(raw).cast("B")
+    n = mv.nbytes
+    m = 4 * ((n + 2) // 3)
+    out = _PyUnicode_New(m, 127)
+    if m == 0:
+        return out
+    dst, _ = _ascii_ptr(out)
+    src = np.frombuffer(mv, dtype=np.uint8)
+    _check(L, L.fa_b64_encode(src.ctypes.data, n, dst, m, _threads()), "base64 encode")
+    return out
+
+
+def b64decode(s: str) -> bytearray:
+    """base64.b64decode(s) for canonical input (what b64encode produces), natively."""
+    L = na.load()
+    p, n = _ascii_ptr(s)
+    total = L.fa_b64_decoded_size(p, n)
+    if total < 0:
+        raise _WireError(total, "not canonical base64")
+    out = bytearray(total)
+    if total:
+        dst = (ctypes.c_char * total).from_buffer(out)
+        _check(L, L.fa_b64_decode(p, n, ctypes.addressof(dst), total, _threads()), "base64 decode")
+    return out
+
+
+# ---------------------------------------------------------------------------------------------
+# restricted unpickler (fallback for content outside the scanner's subset)
+# ---------------------------------------------------------------------------------------------
+
+
+def _load_storage_bytes(b):
+    """torch.storage._load_from_bytes, but through torch.load(weights_only=True)."""
+    return torch.load(io.BytesIO(b), weights_only=True)
+
+
+class _RestrictedUnpickler(pickle.Unpickler):
+    _NUMPY = {
+        ("numpy._core.multiarray", "_reconstruct"), ("numpy.core.multiarray", "_reconstruct"),
+        ("numpy._core.multiarray", "scalar"), ("numpy.core.multiarray", "scalar"),
+        ("numpy._core.numeric", "_frombuffer"), ("numpy.core.numeric", "_frombuffer"),
+        ("numpy", "ndarray"), ("numpy", "dtype"),
+    }
+    _OTHER = {
+        ("collections", "OrderedDict"): collections.OrderedDict,
+        ("_codecs", "encode"): codecs.encode,  # protocol-2 bytes
+        ("builtins", "bytearray"): bytearray,
+        ("builtins", "set"): set,
+        ("builtins", "frozenset"): frozenset,
+        ("builtins", "complex"): complex,
+        ("builtins", "slice"): slice,
+        ("torch.storage", "_load_from_bytes"): _load_storage_bytes,
+    }
+    _TORCH = {"_rebuild_tensor_v2", "_rebuild_parameter", "_rebuild_parameter_with_state"}
+
+    def find_class(self, module, name):
+        if module == "__builtin__":  # protocol <= 2 spelling (fix_imports)
+            module = "builtins"
+        if (module, name) == ("builtins", "bytes"):
+            return bytes
+        if (module, name) in self._NUMPY or (module.startswith("numpy.dtypes") and name.endswith("DType")):
+            return super().find_class(module, name)
+        if (module, name) in self._OTHER:
+            return self._OTHER[(module, name)]
+        if module == "torch._utils" and name in self._TORCH:
+            return super().find_class(module, name)
+        if module == "torch" and (name == "Size" or name.endswith("Storage") or
+                                  isinstance(getattr(torch, name, None), torch.dtype)):
+            return super().find_class(module, name)
+        raise pickle.UnpicklingError(f"global '{module}.{name}' is not allowed by the flearn_amd wire codec")
+
+
+def restricted_loads(data) -> object:
+    return _RestrictedUnpickler(io.BytesIO(data)).load()
+
+
+# ---------------------------------------------------------------------------------------------
+# pinned rows handed out by decode (weakly tracked, verified by address before reuse)
+# ---------------------------------------------------------------------------------------------
+_ROWS: dict[int, tuple] = {}
+_ROWS_LOCK = threading.Lock()
+
+
+class _RowArray(np.ndarray):
+    """The numpy face of a pinned row; carries the torch tensor (`_fa_tensor`).  The arrays
+    handed out are plain ndarray views whose base chain ends here, so the row lives exactly as
+    long as any of them (the registry below only holds a weak reference)."""
+
+
+def _register(params: dict, row_np: _RowArray, layout: tuple):
+    with _ROWS_LOCK:
+        if len(_ROWS) > 4096:
+            for k in [k for k, (ref, _) in _ROWS.items() if ref() is None]:
+                del _ROWS[k]
+        _ROWS[id(params)] = (weakref.ref(row_np), layout)
+
+
+def wire_row(params: dict, layout: tuple):
+    """The pinned row behind a decoded upload's params when its fp32 arrays are still the
+    decoder's views laid out as `layout` ((key, shape, offset), ..., stride) — else None."""
+    ent = _ROWS.get(id(params))
+    if ent is None:
+        return None
+    row_np = ent[0]()
+    if row_np is None or ent[1] != layout:
+        return None
+    row = row_np._fa_tensor
+    base = row.data_ptr()
+    for key, shape, off in layout[:-1]:
+        a = params.get(key)
+        if not isinstance(a, np.ndarray) or a.dtype != _F32 or a.shape != shape or not a.flags.c_contiguous:
+            return None
+        if a.__array_interface__["data"][0] != base + 4 * off:
+            return None
+    return row
+
+
+# ---------------------------------------------------------------------------------------------
+# decode: manifest -> objects
+# ---------------------------------------------------------------------------------------------
+
+
+def _numel(shape):
+    n = 1
+    for s in shape:
+        n *= s
+    return n
+
+
+class _Decoder:
+    def __init__(self, L, ptr, n):
+        self.L, self.ptr, self.n = L, ptr, n
+        self.ranges = []  # (off, len, dst address)
+        self.aux_size = 0
+        self.row_plan = {}  # id(node) -> row offset (elements)
+
+    # pass 1: find the upload's params dict and lay out its fp32 C-order arrays
+    def plan_row(self, tree):
+        if not (isinstance(tree, dict) and "__d" in tree):
+            return None
+        params = None
+        for k, v in tree["__d"]:
+            if k == "params" and isinstance(v, dict) and ("__d" in v or "__od" in v):
+                params = v
+        if params is None:
+            return None
+        layout, stride = [], 0
+        for k, v in params.get("__d", params.get("__od")):
+            if not (isinstance(k, str) and isinstance(v, dict) and "__nd" in v):
+                continue
+            dt, shape, fortran, _off, _len, _ss = v["__nd"]
+            if np.dtype(dt) != _F32 or (fortran and len(shape) > 1):
+                continue
+            numel = _numel(shape)
+            self.row_plan[id(v)] = stride
+            layout.append((k, tuple(shape), stride))
+            stride += -(-max(numel, 1) // ALIGN) * ALIGN
+        if not layout:
+            return None
+        return params, tuple(layout) + (stride,)
+
+    def aux(self, nbytes, align=16):
+        o = -(-self.aux_size // align) * align
+        self.aux_size = o + nbytes
+        return o
+
+    # pass 2: assign destinations
+    def assign(self, node):
+        if isinstance(node, list):
+            for x in node:
+                self.assign(x)
+        elif isinstance(node, dict):
+            if "__nd" in node:
+                if id(node) not in self.row_plan:
+                    node["_aux"] = self.aux(node["__nd"][4])
+            elif "__sc" in node:
+                node["_aux"] = self.aux(node["__sc"][2])
+            elif "__b" in node:
+                node["_aux"] = self.aux(node["__b"][1])
+            else:
+                for key in ("__t", "__d", "__od"):
+                    if key in node:
+                        self.assign(node[key])
+
+    def build(self, node, row_np, aux_np):
+        if isinstance(node, list):
+            return [self.build(x, row_np, aux_np) for x in node]
+        if not isinstance(node, dict):
+            return node
+        if "__nd" in node:
+            dt, shape, fortran, _off, nbytes, setstate = node["__nd"]
+            dtype = np.dtype(dt)
+            if "_aux" not in node:
+                o = self.row_plan[id(node)]
+                return row_np[o : o + _numel(shape)].view(np.ndarray).reshape(shape)
+            count = nbytes // dtype.itemsize if dtype.itemsize else 0
+            flat = np.frombuffer(aux_np, dtype=dtype, count=count, offset=node["_aux"]) if count else np.empty(0, dtype)
+            arr = flat.reshape(shape, order="F" if fortran else "C")
+            if setstate and not dtype.isnative:  # ndarray.__setstate__ hands back native byte order
+                arr = arr.astype(dtype.newbyteorder("="), order="K")
+            return arr
+        if "__sc" in node:
+            dt, _off, nbytes = node["__sc"]
+            return np.frombuffer(aux_np, dtype=np.dtype(dt), count=1, offset=node["_aux"])[0]
+        if "__b" in node:
+            o = node["_aux"]
+            return bytes(aux_np[o : o + node["__b"][1]])
+        if "__f" in node:
+            return float.fromhex(node["__f"])
+        if "__t" in node:
+            return tuple(self.build(x, row_np, aux_np) for x in node["__t"])
+        if "__dt" in node:
+            return np.dtype(node["__dt"])
+        if "__d" in node or "__od" in node:
+            out = {} if "__d" in node else collections.OrderedDict()
+            for k, v in node.get("__d", node.get("__od")):
+                out[_hashable(self.build(k, row_np, aux_np))] = self.build(v, row_np, aux_np)
+            return out
+        raise _WireError(na.FA_ERR_UNSUPPORTED, f"unknown manifest node {list(node)}")
+
+
+def _hashable(k):
+    return tuple(_hashable(x) for x in k) if isinstance(k, list) else k
+
+
+def _payload_nodes(node, out):
+    if isinstance(node, list):
+        for x in node:
+            _payload_nodes(x, out)
+    elif isinstance(node, dict):
+        if "__nd" in node or "__sc" in node or "__b" in node:
+            out.append(node)
+        else:
+            for key in ("__t", "__d", "__od"):
+                if key in node:
+                    _payload_nodes(node[key], out)
+
+
+def _pinned_row(stride: int) -> torch.Tensor:
+    if torch.cuda.is_available():
+        return torch.empty(stride, dtype=torch.float32, pin_memory=True)
+    return torch.empty(stride, dtype=torch.float32)
+
+
+def decode_fast(s: str):
+    """Decode base64(pickle) text through the scanner; raises _WireError(FA_ERR_UNSUPPORTED /
+    FA_ERR_DATA) when the content or the encoding is outside the fast path."""
+    L = na.load()
+    p, n = _ascii_ptr(s)
+    cap = 1 << 16
+    for _ in range(2):
+        buf = ctypes.create_string_buffer(cap)
+        need = ctypes.c_int64(0)
+        rc = L.fa_pickle_scan_b64(p, n, buf, cap, ctypes.byref(need))
+        if rc == na.FA_ERR_SIZE:
+            cap = need.value + 1
+            continue
+        _check(L, rc, "pickle scan")
+        break
+    tree = json.loads(buf.raw[: need.value].decode("utf-8"))
+    dec = _Decoder(L, p, n)
+    planned = dec.plan_row(tree)
+    dec.assign(tree)
+    aux_np = np.empty(max(dec.aux_size, 1), dtype=np.uint8)
+    row, row_np = None, None
+    if planned is not None:
+        stride = planned[1][-1]
+        row = _pinned_row(stride)
+        row_np = row.numpy().view(_RowArray)
+        row_np._fa_tensor = row
+        # zero the alignment gaps (reduced but never returned: keep them finite and deterministic)
+        end = 0
+        for _k, shape, off in planned[1][:-1]:
+            if off > end:
+                row_np[end:off] = 0
+            end = off + _numel(shape)
+        row_np[end:stride] = 0
+    offs, lens, dsts = [], [], []
+    for node in _payload_nodes_list(tree):
+        if "__nd" in node:
+            o, ln = node["__nd"][3], node["__nd"][4]
+            dst = row_np.ctypes.data + 4 * dec.row_plan[id(node)] if "_aux" not in node else aux_np.ctypes.data + node["_aux"]
+        elif "__sc" in node:
+            o, ln = node["__sc"][1], node["__sc"][2]
+            dst = aux_np.ctypes.data + node["_aux"]
+        else:
+            o, ln = node["__b"]
+            dst = aux_np.ctypes.data + node["_aux"]
+        if ln:
+            offs.append(o)
+            lens.append(ln)
+            dsts.append(dst)
+    if offs:
+        k = len(offs)
+        rc = L.fa_b64_decode_ranges(p, n, k, (ctypes.c_int64 * k)(*offs), (ctypes.c_int64 * k)(*lens),
+                                    (ctypes.c_void_p * k)(*dsts), _threads())
+        _check(L, rc, "payload decode")
+    obj = dec.build(tree, row_np, aux_np)
+    if planned is not None:
+        params = obj.get("params") if isinstance(obj, dict) else None
+        if isinstance(params, dict):
+            _register(params, row_np, planned[1])
+    return obj
+
+
+def _payload_nodes_list(tree):
+    out = []
+    _payload_nodes(tree, out)
+    return out
+
+
+# ---------------------------------------------------------------------------------------------
+# the codec objects
+# ---------------------------------------------------------------------------------------------
+
+
+class BaseEncrypt:
+    """Identity codec (Encrypt.py:6-13)."""
+
+    def encode(self, params):
+        return params
+
+    def decode(self, glob_params):
+        return glob_params
+
+
+class Encrypt(BaseEncrypt):
+    """base64(pickle) codec, byte-compatible with flearn's Encrypt (Encrypt.py:16-44)."""
+
+    def encode(self, params):
+        """Encrypt.py:17-30: base64.b64encode(pickle.dumps(params)).decode()."""
+        return b64encode(pickle.dumps(params))
+
+    def decode(self, glob_params):
+        """Encrypt.py:32-44: pickle.loads(base64.b64decode(glob_params.encode())) — through the
+        scanner and the pinned-row decoder when possible, else the restricted unpickler."""
+        if isinstance(glob_params, str) and glob_params.isascii():
+            try:
+                return decode_fast(glob_params)
+            except _WireError as e:
+                if e.code not in (na.FA_ERR_UNSUPPORTED, na.FA_ERR_DATA):
+                    raise
+            except (TypeError, ValueError):  # e.g. a dtype numpy rejects: let the unpickler report it
+                pass
+            try:
+                raw = b64decode(glob_params)
+            except _WireError:
+                raw = base64.b64decode(glob_params.encode())  # lenient input: the reference's decoder
+            return restricted_loads(raw)
+        return restricted_loads(base64.b64decode(glob_params.encode()))

@@ -29,13 +29,16 @@
 extern "C" {
 #endif
 
-#define FA_ABI_VERSION 2
+#define FA_ABI_VERSION 3
 
 /* return codes */
 #define FA_OK 0
 #define FA_ERR_ARG (-1)    /* bad size / null pointer / unknown enum */
 #define FA_ERR_ALIGN (-2)  /* row window not 16-byte aligned */
 #define FA_ERR_LAUNCH (-3) /* HIP launch error */
+#define FA_ERR_SIZE (-4)        /* output buffer too small (the needed size is reported)      */
+#define FA_ERR_UNSUPPORTED (-5) /* wire codec: pickle content outside the supported subset   */
+#define FA_ERR_DATA (-6)        /* wire codec: malformed / non-canonical base64 or pickle     */
 
 /* Reduce modes: how numpy (NEP 50, numpy >= 2) evaluates
  *   w = a0*x0; w += a_n*x_n; w = np.divide(w, np.sum(a))          strategy.py:123-129
@@ -123,6 +126,44 @@ int fa_opt_apply(int32_t prec, const fa_epilogue* epi, const float* local, const
  * regenerates any element.  Not a reference interface.                                        */
 int fa_fill_uniform_f32(float* dst, int64_t row_stride, int32_t n_rows, int64_t n_cols,
                         uint64_t seed, int64_t row_begin, int64_t col_global_begin, void* stream);
+
+/* ---- wire codec (HOST functions: every pointer below is host memory) -------------------------
+ * flearn's HTTP mode ships uploads and global models as base64(pickle.dumps(obj))
+ * (flearn/common/Encrypt.py:17-44, Encrypt.encode / Encrypt.decode; decoded per upload in
+ * Server.ensemble, flearn/server/Server.py:126-131).  These replace base64.b64encode /
+ * base64.b64decode / pickle.loads on that path.  `threads` <= 0 picks a default (<= 16). */
+
+/* Decoded length of canonical base64 text (length % 4 == 0, '=' only as final padding), or
+ * FA_ERR_DATA.  Non-canonical text is left to the caller (Python's lenient b64decode).       */
+int64_t fa_b64_decoded_size(const char* src, int64_t n);
+
+/* base64.b64decode(src) -> dst (cap bytes).  FA_ERR_DATA on a non-alphabet character.      */
+int fa_b64_decode(const char* src, int64_t n, uint8_t* dst, int64_t cap, int32_t threads);
+
+/* Decode only the decoded-byte ranges [offsets[r], offsets[r] + lengths[r]) of the base64
+ * text, each straight into dsts[r] — how array payloads land in pinned staging without an
+ * intermediate bytes object.  Ranges need no alignment.                                      */
+int fa_b64_decode_ranges(const char* src, int64_t n, int32_t count, const int64_t* offsets,
+                         const int64_t* lengths, void* const* dsts, int32_t threads);
+
+/* base64.b64encode(src) -> dst (4*ceil(n/3) characters, no terminator).                     */
+int fa_b64_encode(const uint8_t* src, int64_t n, char* dst, int64_t cap, int32_t threads);
+
+/* Restricted pickle scan (pickle.loads replacement for the structure check): walk the pickle
+ * inside base64 text WITHOUT decoding array payloads and write a JSON manifest of the object:
+ *   null/true/false/ints/"str"; {"__f":"<C99 hex float>"}; {"__b":[off,len]} bytes;
+ *   {"__t":[...]} tuple; [...] list; {"__d":[[k,v],...]} dict; {"__od":[...]} OrderedDict;
+ *   {"__nd":[dtype,[shape],fortran,off,len,setstate]} numpy array (setstate=1: rebuilt by
+ *   ndarray.__setstate__, which returns native byte order; 0: numpy's protocol-5 _frombuffer); {"__sc":[dtype,off,len]} numpy
+ *   scalar; {"__dt":dtype} numpy dtype — off/len are decoded-byte ranges of the payload.
+ * Accepts protocol 2-5 opcodes for dicts/lists/tuples/str/bytes/ints/floats/bools/None and the
+ * numpy reconstructors only; anything else (other globals, torch tensors) -> FA_ERR_UNSUPPORTED.
+ * FA_ERR_SIZE when cap is too small (*out_len = needed).                                     */
+int fa_pickle_scan_b64(const char* src, int64_t n, char* out, int64_t cap, int64_t* out_len);
+/* Same over already-decoded pickle bytes. */
+int fa_pickle_scan(const uint8_t* buf, int64_t n, char* out, int64_t cap, int64_t* out_len);
+/* Thread-local message of the last failing wire-codec call. */
+const char* fa_wire_last_error(void);
 
 #ifdef __cplusplus
 }

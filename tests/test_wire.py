@@ -1,0 +1,226 @@
+"""Wire codec (flearn/common/Encrypt.py:16-44) — host code, runs without a GPU.
+
+Bar: Encrypt().encode(obj) is the reference's exact string, Encrypt().decode(s) equals
+pickle.loads(base64.b64decode(s)) value for value (dtype, shape, memory order, container types),
+for the reference's own strings (tests/golden/wire_*.npz) and for a sweep of pickle protocols and
+value kinds; the native scanner never crashes on corrupted input."""
+import base64
+import collections
+import ctypes
+import pickle
+
+import numpy as np
+import pytest
+import torch
+
+from flearn_amd import _native as na
+from flearn_amd import layouts, wire
+from flearn_amd.bucket import make_plan
+from golden_io import Golden
+
+
+def same(a, b, where=""):
+    if isinstance(b, np.ndarray):
+        assert isinstance(a, np.ndarray), where
+        assert a.dtype == b.dtype and a.shape == b.shape, where
+        assert a.tobytes(order="A") == b.tobytes(order="A"), where
+        assert a.flags.f_contiguous == b.flags.f_contiguous and a.flags.c_contiguous == b.flags.c_contiguous, where
+    elif isinstance(b, torch.Tensor):
+        assert isinstance(a, torch.Tensor) and a.dtype == b.dtype and a.shape == b.shape, where
+        assert a.numpy().tobytes() == b.numpy().tobytes(), where
+    elif isinstance(b, dict):
+        assert type(a) is type(b) and list(a) == list(b), where
+        for k in b:
+            same(a[k], b[k], f"{where}/{k}")
+    elif isinstance(b, (list, tuple)):
+        assert type(a) is type(b) and len(a) == len(b), where
+        for i, (x, y) in enumerate(zip(a, b)):
+            same(x, y, f"{where}[{i}]")
+    elif isinstance(b, float) and b != b:
+        assert type(a) is type(b) and a != a, where
+    else:
+        assert type(a) is type(b) and a == b, (where, a, b)
+
+
+def sample_objects():
+    rng = np.random.default_rng(1)
+    params = collections.OrderedDict()
+    params["conv.weight"] = rng.standard_normal((4, 3, 3, 3)).astype(np.float32)
+    params["conv.bias"] = np.array([-0.0, np.nan, np.inf, 1.0], np.float32)
+    params["bn.num_batches_tracked"] = np.array(7, np.int64)
+    params["fortran"] = np.asfortranarray(rng.standard_normal((3, 5)).astype(np.float32))
+    params["bigendian"] = np.arange(5, dtype=">f8")
+    params["half"] = np.ones(7, np.float16)
+    params["mask"] = np.array([True, False, True])
+    params["empty"] = np.zeros((0, 4), np.float32)
+    params["scalar32"] = np.float32(1.5)
+    params["uint8"] = np.arange(300, dtype=np.int64).astype(np.uint8)
+    big = {"fc.weight": rng.standard_normal((300, 700)).astype(np.float32)}  # > one pickle frame
+    return [
+        {"agg_weight": 1.0, "params": dict(params)},
+        {"agg_weight": 3, "params": params},
+        {"agg_weight": np.float64(0.25), "params": big},
+        {"w_glob": {"a": np.float64(2.5), "b": np.arange(4.0)}, "meta": [1, (2, 3.5), b"\x00\xff", None, "q\"\\\né", 10**15, -7, True]},
+        [],
+        {},
+        "plain string",
+        12345678901234,
+    ]
+
+
+# ---------------------------------------------------------------------------------------------
+# base64
+# ---------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("n", list(range(0, 50)) + [255, 256, 257, 786431, 786432, 786433, 3 * 2**20 + 2])
+def test_b64_matches_python(n):
+    raw = np.random.default_rng(n).integers(0, 256, n, dtype=np.uint8).tobytes()
+    s = base64.b64encode(raw).decode()
+    assert wire.b64encode(raw) == s
+    assert bytes(wire.b64decode(s)) == raw
+
+
+def test_b64_rejects_bad_text():
+    L = na.load()
+    for bad in ("abc", "ab=c", "a===", "ab\ncd==", "ab-_"):
+        p, n = wire._ascii_ptr(bad)
+        total = L.fa_b64_decoded_size(p, n)
+        if total >= 0:
+            out = (ctypes.c_char * max(total, 1))()
+            assert L.fa_b64_decode(p, n, out, total, 1) == na.FA_ERR_DATA, bad
+        else:
+            assert total == na.FA_ERR_DATA, bad
+
+
+def test_b64_decode_ranges():
+    L = na.load()
+    rng = np.random.default_rng(3)
+    raw = rng.integers(0, 256, 1_000_003, dtype=np.uint8)
+    s = base64.b64encode(raw.tobytes()).decode()
+    p, n = wire._ascii_ptr(s)
+    offs = [0, 1, 2, 3, 5, 999_999, 1_000_000, 1_000_002, 123_457, 17]
+    lens = [1, 2, 3, 4, 4, 4, 3, 1, 600_000, 0]
+    dsts = [np.zeros(max(ln, 1), np.uint8) for ln in lens]
+    k = len(offs)
+    rc = L.fa_b64_decode_ranges(p, n, k, (ctypes.c_int64 * k)(*offs), (ctypes.c_int64 * k)(*lens),
+                                (ctypes.c_void_p * k)(*[d.ctypes.data for d in dsts]), 4)
+    assert rc == na.FA_OK
+    for o, ln, d in zip(offs, lens, dsts):
+        assert np.array_equal(d[:ln], raw[o : o + ln]), (o, ln)
+    bad = (ctypes.c_int64 * 1)(1_000_000)
+    rc = L.fa_b64_decode_ranges(p, n, 1, bad, (ctypes.c_int64 * 1)(4), (ctypes.c_void_p * 1)(dsts[0].ctypes.data), 1)
+    assert rc == na.FA_ERR_ARG
+
+
+# ---------------------------------------------------------------------------------------------
+# Encrypt
+# ---------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("i", range(len(sample_objects())))
+def test_encode_is_the_reference_string(i):
+    obj = sample_objects()[i]
+    assert wire.Encrypt().encode(obj) == base64.b64encode(pickle.dumps(obj)).decode()
+
+
+@pytest.mark.parametrize("proto", [2, 3, 4, 5])
+@pytest.mark.parametrize("i", range(len(sample_objects())))
+def test_decode_equals_pickle_loads(proto, i):
+    obj = sample_objects()[i]
+    raw = pickle.dumps(obj, protocol=proto)
+    s = base64.b64encode(raw).decode()
+    same(wire.Encrypt().decode(s), pickle.loads(raw), f"proto{proto}")
+
+
+def test_decode_fast_path_taken_for_uploads():
+    """Protocol-4 numpy uploads (what flearn clients send) never need the Python unpickler."""
+    for obj in sample_objects()[:3]:
+        s = base64.b64encode(pickle.dumps(obj)).decode()
+        same(wire.decode_fast(s), pickle.loads(pickle.dumps(obj)))
+
+
+def test_lenient_base64_like_reference():
+    """Text base64.b64decode accepts (here: embedded newlines) is decoded like the reference."""
+    obj = {"agg_weight": 1.0, "params": {"w": np.arange(10, dtype=np.float32)}}
+    s = base64.b64encode(pickle.dumps(obj)).decode()
+    s = s[:10] + "\n" + s[10:]
+    same(wire.Encrypt().decode(s), pickle.loads(base64.b64decode(s.encode())))
+
+
+def test_forbidden_globals_are_refused():
+    class Boom:
+        def __reduce__(self):
+            return (print, ("executed!",))
+
+    s = base64.b64encode(pickle.dumps({"agg_weight": 1.0, "params": {"x": Boom()}})).decode()
+    with pytest.raises(pickle.UnpicklingError):
+        wire.Encrypt().decode(s)
+
+
+def test_scanner_survives_corruption():
+    """Mutated / truncated pickles: an error code, never a crash or a hang."""
+    L = na.load()
+    obj = sample_objects()[0]
+    raw = bytearray(pickle.dumps(obj))
+    rng = np.random.default_rng(7)
+    out = ctypes.create_string_buffer(1 << 20)
+    need = ctypes.c_int64()
+    codes = set()
+    for t in range(3000):
+        b = bytearray(raw)
+        if t % 3 == 0:
+            b = b[: rng.integers(0, len(b))]
+        else:
+            for _ in range(rng.integers(1, 6)):
+                b[rng.integers(0, len(b))] = rng.integers(0, 256)
+        buf = (ctypes.c_uint8 * max(len(b), 1)).from_buffer(b if b else bytearray(1))
+        rc = L.fa_pickle_scan(buf, len(b), out, len(out), ctypes.byref(need))
+        codes.add(rc)
+        s = base64.b64encode(bytes(b)).decode()
+        p, n = wire._ascii_ptr(s)
+        L.fa_pickle_scan_b64(p, n, out, len(out), ctypes.byref(need))
+    assert na.FA_ERR_DATA in codes and codes <= {na.FA_OK, na.FA_ERR_DATA, na.FA_ERR_UNSUPPORTED}
+
+
+# ---------------------------------------------------------------------------------------------
+# the reference's own strings
+# ---------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("name", ["wire_upload", "wire_glob", "wire_torch"])
+def test_reference_strings(name):
+    g = Golden(name)
+    s = g.arrays["b64"].tobytes().decode("ascii")
+    got = wire.Encrypt().decode(s)
+    inner = got.get("params", got.get("w_glob"))
+    want = g.output()
+    kinds = g.output_kinds()
+    assert list(inner) == list(want)
+    for k, v in inner.items():
+        if kinds[k].startswith("torch:"):
+            assert isinstance(v, torch.Tensor) and str(v.dtype) == kinds[k][6:]
+            v = v.numpy()
+        elif kinds[k].startswith("scalar:"):
+            assert type(v).__name__ == kinds[k].split(":")[1]
+        else:
+            assert isinstance(v, np.ndarray)
+        w = want[k]
+        assert np.asarray(v).dtype == np.asarray(w).dtype and np.asarray(v).tobytes() == np.asarray(w).tobytes(), k
+    if "logits" in got:
+        assert torch.equal(got["logits"], torch.from_numpy(g.output("logits")["logits"]))
+    if name != "wire_torch":  # torch pickles embed a storage key derived from a memory address
+        assert wire.Encrypt().encode(got) == s  # encode(decode(s)) is the reference's string again
+
+
+def test_decoded_upload_rows_match_the_bucket_plan():
+    """An upload decoded by the codec sits in one pinned row laid out as make_plan's f32 bucket,
+    so the Packer can DMA it as is; replacing an array invalidates the row."""
+    lay = layouts.get("lenet5")
+    flat = np.random.default_rng(0).standard_normal(layouts.fp32_elems(lay)).astype(np.float32)
+    up = {"agg_weight": 1.0, "params": layouts.synthetic_state_dict(lay, flat)}
+    up["params"]["bn.num_batches_tracked"] = np.array(3, np.int64)
+    got = wire.Encrypt().decode(wire.Encrypt().encode(up))
+    plan = make_plan([1.0, 1.0], [got["params"], got["params"]])
+    g = plan.f32
+    sig = tuple((s.key, s.shape, s.offset) for s in g.segments) + (g.stride,)
+    row = wire.wire_row(got["params"], sig)
+    assert row is not None and row.numel() == g.stride
+    for s_ in g.segments:
+        assert np.array_equal(row.numpy()[s_.offset : s_.offset + s_.numel], up["params"][s_.key].reshape(-1))
+    got["params"]["fc1.weight"] = got["params"]["fc1.weight"].copy()
+    assert wire.wire_row(got["params"], sig) is None
