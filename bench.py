@@ -13,7 +13,13 @@ Configs (BASELINE.json):  c2  FedAVG    100 x ResNet-18 (11,699,112 fp32)      [
                           c3  FedAVGM   100 x ResNet-50 (25,610,152 fp32)
                           c4  FedAVG   1000 x ResNet-18
                           c5  FedOPT-Adagrad 100 x ViT-B/16 (86,567,656 fp32)
-Multi-GPU is strong scaling of the chosen config (element-range shards + all-gather).
+Multi-GPU (element-range column shards + RCCL all-gather, flearn_amd/dist.py):
+  --scaling weak   (default) the job aggregates clients x G uploads on G GPUs, so every GPU
+                   streams the same bytes as the 1-GPU run (G=8 from c2: 800 clients x
+                   ResNet-18, the shape of BASELINE config 4)
+  --scaling strong the config's clients on G GPUs (each GPU reduces P/G columns)
+  --emulate-world G  one GPU runs rank 0's share of a G-GPU job (no collective): the per-rank
+                   reduce of the multi-GPU runs, measurable on a single-GPU box
 Prints ONE JSON line on rank 0 (stdout); progress goes to stderr.
 """
 from __future__ import annotations
@@ -41,6 +47,7 @@ from flearn_amd.dist import ShardedReducer, ShardPlan, hip_reduce_fn  # noqa: E4
 METRIC = "device-resident GiB/s, FedAVG N-client weighted tensor reduce; %HBM peak"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
 GIB = 1024.0**3
+DEFAULT_STRIPES = 2  # N>1: stripe 0's all-gather overlaps stripe 1's reduce
 
 CONFIGS = {
     "c2": dict(layout="resnet18", clients=100, op="mean",
@@ -122,6 +129,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--stripes", type=int, default=None, help="reduce/gather pipeline depth (N>1)")
+    ap.add_argument("--scaling", choices=("weak", "strong"), default="weak")
+    ap.add_argument("--emulate-world", type=int, default=None,
+                    help="single process: time rank 0's reduce of a G-GPU job (no gather)")
     ap.add_argument("--cpu-sample", type=int, default=None, help="clients in the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
@@ -139,10 +149,14 @@ def main():
 
     cfg = CONFIGS[args.config]
     layout = layouts.get(cfg["layout"])
-    n = cfg["clients"]
+    emu = args.emulate_world
+    if emu is not None and world != 1:
+        raise SystemExit("--emulate-world is a single-process mode")
+    g_eff = emu or world  # GPUs of the (possibly emulated) job
+    n = cfg["clients"] * (g_eff if args.scaling == "weak" else 1)
     p_real = layouts.fp32_elems(layout)
-    stripes = args.stripes or (1 if world == 1 else 4)
-    plan = ShardPlan.make(p_real, world, rank, stripes)
+    stripes = args.stripes or (1 if g_eff == 1 else DEFAULT_STRIPES)
+    plan = ShardPlan.make(p_real, g_eff, rank, stripes)
     cols = plan.local_cols
 
     # ---- device-resident synthetic uploads: this rank's columns of all N clients ----
@@ -165,7 +179,7 @@ def main():
         epi = dict(op=na.OP_BY_NAME[cfg["op"]], prev=prev, v=v)
         local_out = prev  # the fused step advances the global model in place
     fn = hip_reduce_fn(stack, weights, na.MODE_W32_DIV64, denom, **epi)
-    red = ShardedReducer(plan, fn, dev, local_out=local_out)
+    red = ShardedReducer(plan, fn, dev, local_out=local_out, gather=world > 1)
 
     # ---- warmup + timed steps ----
     for _ in range(args.warmup):
@@ -193,10 +207,12 @@ def main():
         elapsed, wall = t.tolist()
     step_s = elapsed / args.steps
     job_bytes = algorithmic_bytes(n, p_real, cfg["op"])
+    if emu:  # rank 0's columns only
+        job_bytes = algorithmic_bytes(n, plan.local_cols, cfg["op"])
     value = job_bytes / GIB / step_s
 
     # ---- roofline of the dominant kernel: per-launch algorithmic bytes / launch time ----
-    if world == 1 and stripes == 1:
+    if g_eff == 1 and stripes == 1:
         launch_s = step_s  # the step IS one kernel launch
         launch_cols = p_real
     else:  # time the reduce launches alone (no gather) on this rank
@@ -210,7 +226,7 @@ def main():
         launch_cols = cols
     launch_bytes = algorithmic_bytes(n, launch_cols, cfg["op"])
     achieved = launch_bytes / 1e9 / launch_s
-    traffic, traffic_src = load_traffic(args.config) if world == 1 else (None, None)
+    traffic, traffic_src = load_traffic(args.config) if g_eff == 1 else (None, None)
     roofline = {
         "bound": "hbm",
         "achieved": round(achieved, 1),
@@ -225,7 +241,7 @@ def main():
         roofline["traffic_source"] = traffic_src
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and g_eff == 1 and not args.no_cpu_baseline:
         sample = args.cpu_sample or min(n, 100)
         log(f"[rank 0] CPU baseline over {sample} clients ...")
         cpu = cpu_baseline(stack, layout, sample)
@@ -240,18 +256,22 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(step_s * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "strong",
+            "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": "fp32",
             "data": "synthetic: device-generated splitmix64 U(-1,1) client uploads, agg_weight 1.0 (flearn default)",
             "config": {
-                "workload": cfg["workload"],
+                "workload": (cfg["workload"] if g_eff == 1 or args.scaling == "strong" else
+                             f"{cfg['workload']}, weak-scaled: {n} clients on {g_eff} GPUs"),
                 "config": args.config,
                 "clients": n,
                 "params": p_real,
                 "layout": cfg["layout"],
                 "epilogue": cfg["op"],
-                "parallelism": "single GPU" if world == 1 else f"element-range shards x{world} + RCCL all-gather ({stripes} stripes)",
+                "parallelism": ("single GPU" if g_eff == 1 else
+                                f"element-range shards x{g_eff} + RCCL all-gather ({stripes} stripes)"
+                                + (f"; EMULATED: rank 0's reduce of a {emu}-GPU job on one GPU, no gather"
+                                   if emu else "")),
                 "hbm_peak_frac_of_value": round(value * GIB / 1e9 / HBM_PEAK_GBS, 4),
                 "wall_s_timed_region": round(wall, 4),
             },

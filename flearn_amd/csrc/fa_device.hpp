@@ -442,6 +442,153 @@ __global__ __launch_bounds__(kThreads) void reduce_kernel(
                                            ncols, e);
 }
 
+// acc + w*x on whole quads, written as <4 x T> IR operations: per-element scalar code gets packed
+// by the SLP vectorizer, which re-places the packed products after the pipeline's scheduling
+// barriers.  Elementwise identical to P::mul / add (no contraction under -ffp-contract=off).
+template <class P>
+__device__ __forceinline__ typename vec4<typename P::acc_t>::type quad_axpy(
+    typename vec4<typename P::acc_t>::type acc, typename P::w_t w, typename vec4<float>::type x) {
+  typedef typename vec4<typename P::acc_t>::type AV;
+  if constexpr (sizeof(typename P::acc_t) == 4)
+    return acc + w * x;
+  else
+    return acc + (AV)(typename P::acc_t)w * __builtin_convertvector(x, AV);
+}
+template <class P>
+__device__ __forceinline__ typename vec4<typename P::acc_t>::type quad_mul(
+    typename P::w_t w, typename vec4<float>::type x) {
+  typedef typename vec4<typename P::acc_t>::type AV;
+  if constexpr (sizeof(typename P::acc_t) == 4)
+    return w * x;
+  else
+    return (AV)(typename P::acc_t)w * __builtin_convertvector(x, AV);
+}
+
+// Row-pipelined grid.  Built for deep, narrow windows (many clients, few columns: the per-rank
+// column shards of a multi-GPU aggregation, e.g. 800 clients x 365 K columns), where the
+// sub-tile kernels run out of column parallelism and a batch of rows that is issued, drained
+// and re-issued keeps only half its bytes in flight on average.  Here:
+//   * a block is W waves; lane l owns quads l, l+64W, ..., l+(V-1)*64W of the block's piece of
+//     every row (V*W KiB contiguous per row), so each wave instruction reads 1 KiB of one row;
+//   * rows are a rolling register pipeline D rows deep: row i+D is loaded right after row i is
+//     consumed, so D*V loads stay in flight per lane for the whole sweep (s_waitcnt
+//     vmcnt((D-1)*V) in the steady state, no drain per batch);
+//   * loads go through per-row buffer descriptors whose range check covers the window's end, so
+//     a partial last piece needs no per-lane branches; the one ragged quad (ncols % 4) goes to
+//     reduce_ragged.
+// The summation order (client list order, first product initialises the sum) is unchanged.
+template <class P, typename T, int OP, int V, int D, int W, bool NT>
+__device__ __forceinline__ void rows_piece(const float* __restrict__ stack, int64_t stride, int n,
+                                           const typename P::w_t* __restrict__ w, int64_t col0,
+                                           int64_t ncols, const Epi<T>& e, int64_t qb,
+                                           int64_t qend) {
+  // the piece is quads [qb, qend), qend - qb <= 64*W*V
+  typedef typename P::acc_t A;
+  typedef typename vec4<float>::type XV;
+  typedef typename vec4<A>::type AV;
+  const int64_t qfull = ncols / 4;
+  const int64_t left = (qend < qfull ? qend : qfull) - qb;
+  const int nq = left <= 0 ? 0 : (int)left;  // full quads of the piece
+  if (nq > 0) {
+    const char* tile0 = reinterpret_cast<const char*>(stack + col0 + qb * 4);
+    const uint32_t bytes = (uint32_t)nq * 16u;
+    const int64_t row_bytes = stride * 4;
+    const int voff = (int)threadIdx.x * 16;
+    XV x[D][V];
+#pragma unroll
+    for (int d = 0; d < D; ++d)
+      if (1 + d < n) {
+        const __amdgpu_buffer_rsrc_t r = row_rsrc(tile0 + (int64_t)(1 + d) * row_bytes, bytes);
+#pragma unroll
+        for (int v = 0; v < V; ++v) x[d][v] = buf_load_quad<NT>(r, voff, v * 64 * W * 16);
+      }
+    AV acc[V];
+    {
+      const __amdgpu_buffer_rsrc_t r = row_rsrc(tile0, bytes);
+      const typename P::w_t w0 = w[0];
+#pragma unroll
+      for (int v = 0; v < V; ++v) acc[v] = quad_mul<P>(w0, buf_load_quad<NT>(r, voff, v * 64 * W * 16));
+    }
+    // rows 1..n-1: slot d holds row i+d; consume it, refill it with row i+d+D (steady state:
+    // every refill is a real row, so no branch)
+    int i = 1;
+    for (; i + 2 * D <= n; i += D) {
+#pragma unroll
+      for (int d = 0; d < D; ++d) {
+        const typename P::w_t wi = w[i + d];
+#pragma unroll
+        for (int v = 0; v < V; ++v) acc[v] = quad_axpy<P>(acc[v], wi, x[d][v]);
+        // pin the order "consume slot d, then refill it": if the scheduler hoists the refill
+        // (or the products of later slots) the old values need copies, and the copies wait for
+        // every in-flight row — the pipeline collapses into batches
+        __builtin_amdgcn_sched_barrier(0);
+        const __amdgpu_buffer_rsrc_t r = row_rsrc(tile0 + (int64_t)(i + d + D) * row_bytes, bytes);
+#pragma unroll
+        for (int v = 0; v < V; ++v) x[d][v] = buf_load_quad<NT>(r, voff, v * 64 * W * 16);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    // drain: fewer than 2*D rows left (wave-uniform branches)
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      if (i + d < n) {
+        const typename P::w_t wi = w[i + d];
+#pragma unroll
+        for (int v = 0; v < V; ++v) acc[v] = quad_axpy<P>(acc[v], wi, x[d][v]);
+        if (i + d + D < n) {
+          const __amdgpu_buffer_rsrc_t r = row_rsrc(tile0 + (int64_t)(i + d + D) * row_bytes, bytes);
+#pragma unroll
+          for (int v = 0; v < V; ++v) x[d][v] = buf_load_quad<NT>(r, voff, v * 64 * W * 16);
+        }
+      }
+    }
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      if (i + D + d < n) {
+        const typename P::w_t wi = w[i + D + d];
+#pragma unroll
+        for (int v = 0; v < V; ++v) acc[v] = quad_axpy<P>(acc[v], wi, x[d][v]);
+      }
+    }
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      const int q = v * 64 * W + (int)threadIdx.x;
+      if (q < nq) finish_quad<T, OP, A>(e, (qb + q) * 4, 4, acc[v]);
+    }
+  }
+  // the window's ragged last quad (ncols % 4 != 0), in the piece that holds it
+  if (threadIdx.x == 0 && qfull * 4 < ncols && qfull >= qb && qfull < qend)
+    reduce_ragged<P, T, OP>(stack + col0, stride, n, w, qfull, qfull + 1, ncols, e);
+}
+
+// Work split: the window's 1-KiB chunks are cut into equal pieces of pc <= W*V chunks, as many
+// as make k whole rounds of the grid (pc = ceil(chunks / (k * grid))), so every block sweeps k
+// pieces (the last one or two blocks one fewer) and the launch has no tail round.
+//   INTERLEAVE: block b takes pieces b, b+grid, b+2*grid, ...: at any moment the grid's pieces
+//               form one contiguous stretch of each row (a linear-read access pattern);
+//   otherwise:  block b takes k consecutive pieces (one contiguous share of the window).
+template <class P, typename T, int OP, int V, int D, int W, bool NT, bool INTERLEAVE = true>
+__global__ __launch_bounds__(64 * W) void reduce_kernel_rows(const float* __restrict__ stack,
+                                                             int64_t stride, int n,
+                                                             const typename P::w_t* __restrict__ w,
+                                                             int64_t col0, int64_t ncols, Epi<T> e) {
+  static_assert(sizeof(typename P::x_t) == 4, "row pipeline is for 4-byte elements");
+  const int64_t nquads = (ncols + 3) / 4;
+  const int64_t chunks = (nquads + 63) / 64;
+  const int64_t g = gridDim.x;
+  const int64_t k = (chunks + g * W * V - 1) / (g * W * V);  // rounds
+  const int64_t pc = (chunks + g * k - 1) / (g * k);         // chunks per piece (<= W*V)
+  const int64_t pieces = (chunks + pc - 1) / pc;
+  const int64_t step = INTERLEAVE ? g : 1;
+  const int64_t first = INTERLEAVE ? blockIdx.x : blockIdx.x * k;
+  const int64_t last = INTERLEAVE ? pieces : (first + k < pieces ? first + k : pieces);
+  for (int64_t p = first; p < last; p += step) {
+    const int64_t qs = p * pc * 64;
+    rows_piece<P, T, OP, V, D, W, NT>(stack, stride, n, w, col0, ncols, e, qs,
+                                      qs + pc * 64 < nquads ? qs + pc * 64 : nquads);
+  }
+}
+
 // Column-blocked client stack: element (n, c) lives at ((c / B) * N + n) * B + c % B with
 // B = kThreads*V*4 columns (one tile).  Tile b's N rows are one contiguous N*B*4-byte region, so
 // a block streams its whole tile linearly (rows B*4 bytes apart) — the access pattern of a plain

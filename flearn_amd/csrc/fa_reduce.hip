@@ -2,15 +2,11 @@
 //
 // Host side only: argument validation, dtype/mode dispatch and launches of the gfx950 kernels in
 // fa_device.hpp on the caller's stream.  No allocation, no synchronisation, no host copies.
-// Geometry (measured with tools/tune_reduce.hip on MI355X, see DESIGN.md "Kernel geometry"):
-//   * large buckets: one 64-KiB-per-row tile per block (16 quads per thread, one client row at a
-//     time): neighbouring blocks sweep each client row almost sequentially, like a linear read;
-//     rows are read through per-row buffer descriptors (lane offset in a VGPR, slot step in
-//     soffset, range-checked partial tiles);
-//     if that grid's last round of resident blocks would be < 85% full, the same tiles are
-//     spread evenly over whole rounds (balanced grid) instead;
-//   * buckets too small to give every CU two such tiles: the round-balanced grid (4 quads per
-//     thread, 4 rows in flight) with one resident wave of blocks, each owning an equal share.
+// Geometry (measured with tools/tune_reduce.hip on MI355X):
+//   * fp32 client stacks (every configuration of the hot path): the row-pipelined kernel on
+//     192 blocks (0.75 per CU) with equal shares of the window; each block sweeps its share in
+//     pieces of V KiB x 4 waves, rows pipelined D = 16/V deep through per-row buffer descriptors
+//     (~64 KiB of client rows in flight per block, whatever the window's width or depth);
 //   * 8-byte kinds (f64 / i64 buckets, small): 4 quads per thread, one row at a time.
 #include <hip/hip_runtime.h>
 
@@ -38,19 +34,14 @@ int fail(int code, const char* what) {
 constexpr bool kNT = true;  // client bytes are read once: non-temporal
 
 template <class P>
-struct Geometry {  // fp32 buckets: big tiles read through per-row buffer descriptors
-  static constexpr int kBigV = 16, kBigU = 1, kSmallV = 4, kSmallU = 4;
-  static constexpr bool kBuf = true;
-};
+struct Geometry;  // 8-byte kinds only; fp32 stacks use the row pipeline
 template <>
 struct Geometry<AccF64> {
-  static constexpr int kBigV = 4, kBigU = 1, kSmallV = 4, kSmallU = 1;
-  static constexpr bool kBuf = false;
+  static constexpr int kSmallV = 4, kSmallU = 1;
 };
 template <>
 struct Geometry<AccI64> {
-  static constexpr int kBigV = 4, kBigU = 1, kSmallV = 4, kSmallU = 1;
-  static constexpr bool kBuf = false;
+  static constexpr int kSmallV = 4, kSmallU = 1;
 };
 
 int device_cus() {
@@ -88,39 +79,51 @@ int launch_check() {
   return FA_OK;
 }
 
+// fp32 client stacks: the row-pipelined kernel (reduce_kernel_rows) on a grid of kRowsBlocksPerCU
+// x CUs blocks, equal interleaved pieces.  The piece width and pipeline depth follow the share s
+// (KiB of every row per block): the narrowest piece that covers s (or 16 KiB per wave), D = 16/V
+// rows deep, so a block keeps ~64 KiB of client rows in flight whatever the window's shape.
+constexpr int kRowsWaves = 4;  // W: 256-thread blocks
+// Fewer blocks than CUs stream best: 192 on 256 CUs for the plain mean; the fused
+// optimizer epilogues (state reads/writes at the end of every piece) like a few more in flight.
+constexpr double kRowsBlocksPerCU = 0.75;
+constexpr double kRowsBlocksPerCUEpilogue = 0.875;
+
+template <class P, typename T, int OP, int V>
+int launch_rows(const float* stack, int64_t stride, int n, const typename P::w_t* w, int64_t col0,
+                int64_t ncols, const Epi<T>& e, int64_t grid, hipStream_t s) {
+  hipLaunchKernelGGL((reduce_kernel_rows<P, T, OP, V, 16 / V, kRowsWaves, kNT>), dim3((unsigned)grid),
+                     dim3(64 * kRowsWaves), 0, s, stack, stride, n, w, col0, ncols, e);
+  return launch_check();
+}
+
 template <class P, typename T, int OP>
 int launch_reduce(const typename P::x_t* stack, int64_t stride, int n, const void* w, int64_t col0,
                   int64_t ncols, const Epi<T>& e, hipStream_t s) {
-  typedef Geometry<P> G;
   const typename P::w_t* wt = static_cast<const typename P::w_t*>(w);
   const int cus = device_cus();
   const int64_t chunks = ((ncols + 3) / 4 + 63) / 64;  // 1-KiB row pieces
-  const int64_t per_big = (int64_t)kThreads * G::kBigV * 4;
-  const int64_t big_tiles = (ncols + per_big - 1) / per_big;
-  if (big_tiles > 0x7fffffff) return fail(FA_ERR_ARG, "n_cols too large");
-  if (big_tiles >= 2 * (int64_t)cus) {
-    auto one = reduce_kernel<P, T, OP, G::kBigV, G::kBigU, kNT, G::kBuf>;
-    const int64_t slots = (int64_t)cus * resident_blocks_per_cu(one);
-    const int64_t rounds = (big_tiles + slots - 1) / slots;
-    if (big_tiles * 100 >= rounds * slots * 85) {  // one-shot rounds >= 85% full: no real tail
-      hipLaunchKernelGGL(one, dim3((unsigned)big_tiles), dim3(kThreads), 0, s, stack, stride, n, wt, col0,
-                         ncols, e);
-      return launch_check();
-    }
-    // a badly filled last round: same tile shape, `rounds` equal waves of resident blocks
-    auto bal = reduce_kernel_balanced<P, T, OP, G::kBigV, G::kBigU, kNT, G::kBuf>;
-    const int64_t bslots = (int64_t)cus * resident_blocks_per_cu(bal);
-    const int64_t grid = ((big_tiles + bslots - 1) / bslots) * bslots;
-    hipLaunchKernelGGL(bal, dim3((unsigned)(grid < chunks ? grid : chunks)), dim3(kThreads), 0, s, stack,
-                       stride, n, wt, col0, ncols, e);
+  if constexpr (sizeof(typename P::x_t) == 4) {
+    int64_t grid = (int64_t)(cus * (OP == FA_OP_MEAN ? kRowsBlocksPerCU : kRowsBlocksPerCUEpilogue) + 0.5);
+    if (grid < 1) grid = 1;
+    if (grid > chunks) grid = chunks;
+    const int64_t share = (chunks + grid - 1) / grid;  // chunks per block
+    if (share <= 1 * kRowsWaves) return launch_rows<P, T, OP, 1>(stack, stride, n, wt, col0, ncols, e, grid, s);
+    if (share <= 2 * kRowsWaves) return launch_rows<P, T, OP, 2>(stack, stride, n, wt, col0, ncols, e, grid, s);
+    if (share <= 4 * kRowsWaves) return launch_rows<P, T, OP, 4>(stack, stride, n, wt, col0, ncols, e, grid, s);
+    if (share <= 8 * kRowsWaves) return launch_rows<P, T, OP, 8>(stack, stride, n, wt, col0, ncols, e, grid, s);
+    return launch_rows<P, T, OP, 16>(stack, stride, n, wt, col0, ncols, e, grid, s);
+  } else {
+    // 8-byte kinds (f64 / i64 buckets: BN counters, float64 state; small): 4 quads per thread,
+    // one row at a time, round-balanced grid
+    typedef Geometry<P> G;
+    auto kern = reduce_kernel_balanced<P, T, OP, G::kSmallV, G::kSmallU, kNT>;
+    const int64_t slots = (int64_t)cus * resident_blocks_per_cu(kern);
+    const int64_t grid = chunks < slots ? chunks : slots;
+    hipLaunchKernelGGL(kern, dim3((unsigned)(grid > 0 ? grid : 1)), dim3(kThreads), 0, s, stack, stride, n, wt,
+                       col0, ncols, e);
     return launch_check();
   }
-  auto kern = reduce_kernel_balanced<P, T, OP, G::kSmallV, G::kSmallU, kNT>;
-  const int64_t slots = (int64_t)cus * resident_blocks_per_cu(kern);
-  const int64_t grid = chunks < slots ? chunks : slots;
-  hipLaunchKernelGGL(kern, dim3((unsigned)(grid > 0 ? grid : 1)), dim3(kThreads), 0, s, stack, stride, n, wt,
-                     col0, ncols, e);
-  return launch_check();
 }
 
 template <class P, typename T>

@@ -177,6 +177,56 @@ def test_reduce_kernel_big_tiles_ragged(n, ncols, cuda):
     assert bitwise_equal(out64.cpu().numpy(), want)
 
 
+# row-pipeline geometry: each (n, ncols) lands on a different piece width V (1, 2, 4, 8, 16 KiB
+# per wave) and pipeline depth D = 16/V on the 192/224-block grid, with ragged piece and window
+# ends; deep stacks are the per-rank shapes of the multi-GPU runs
+ROW_SHAPES = [(800, 150001), (300, 390001), (200, 700003), (64, 1500007), (40, 3300001), (17, 33), (2, 5000003)]
+
+
+@pytest.mark.parametrize("n,ncols", ROW_SHAPES)
+def test_row_pipeline_geometries(n, ncols, cuda):
+    stride = -(-ncols // 64) * 64
+    x = _device_stack(n, stride, seed=n + ncols)
+    w32 = np.linspace(0.25, 3.0, n).astype(np.float32)
+    denom = float(np.sum([float(v) for v in w32]))
+    out64 = torch.empty(ncols, dtype=torch.float64, device=cuda)
+    agg.reduce_stack(x, torch.from_numpy(w32).to(cuda), na.MODE_W32_DIV64, denom, n_cols=ncols, out64=out64)
+    want = oracle.c_reduce(oracle.MODE_W32_DIV64, x[:, :ncols].cpu().numpy(), w32, denom)
+    assert bitwise_equal(out64.cpu().numpy(), want)
+
+
+@pytest.mark.parametrize("n,ncols,op", [(300, 390001, "avgm"), (64, 1500007, "adagrad"), (800, 150001, "adam")])
+def test_row_pipeline_fused_epilogues(n, ncols, op, cuda):
+    stride = -(-ncols // 64) * 64
+    x = _device_stack(n, stride, seed=ncols)
+    w = np.ones(n, np.float32)
+    prev = torch.empty((1, stride), dtype=torch.float32, device=cuda)
+    agg.fill_uniform(prev, seed=9)
+    prev_h = prev[0, :ncols].cpu().numpy().copy()
+    v = torch.full((ncols,), 0.5, dtype=torch.float64, device=cuda)
+    v_h = v.cpu().numpy().copy()
+    out32 = torch.empty(ncols, dtype=torch.float32, device=cuda)
+    agg.reduce_stack(x, torch.from_numpy(w).to(cuda), na.MODE_W32_DIV64, float(n), n_cols=ncols, out32=out32,
+                     op=na.OP_BY_NAME[op], prev=prev[0], v=v)
+    g = oracle.c_reduce(oracle.MODE_W32_DIV64, x[:, :ncols].cpu().numpy(), w, float(n))
+    want = oracle.c_update(op, g, prev_h, v_h)
+    assert bitwise_equal(out32.cpu().numpy(), want.astype(np.float32))
+    assert bitwise_equal(v.cpu().numpy(), v_h)
+
+
+def test_row_pipeline_deep_window_offsets(cuda):
+    """Windows of a deep stack (multi-GPU shard slices) equal the same columns of the full reduce."""
+    n, stride = 400, 1 << 20
+    x = _device_stack(n, stride, seed=3)
+    w = torch.ones(n, dtype=torch.float32, device=cuda)
+    full = torch.empty(stride, dtype=torch.float64, device=cuda)
+    agg.reduce_stack(x, w, na.MODE_W32_DIV64, float(n), out64=full)
+    for c0, width in [(0, 262144), (262144, 262144), (4096, 500003), (stride - 70004, 70001)]:
+        part = torch.empty(width, dtype=torch.float64, device=cuda)
+        agg.reduce_stack(x, w, na.MODE_W32_DIV64, float(n), col_begin=c0, n_cols=width, out64=part)
+        assert torch.equal(part, full[c0 : c0 + width]), c0
+
+
 @pytest.mark.parametrize("op", ["avgm", "adagrad"])
 def test_fused_epilogue_big_tiles(op, cuda):
     n, p = 4, 8388608 + 5

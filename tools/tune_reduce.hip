@@ -117,6 +117,22 @@ Variant make_balanced(const float* stack, int64_t stride, int n, const float* w,
           true, {}};
 }
 
+template <int V, int D, int W, int OP, typename T, bool IL = true>
+Variant make_rows(const float* stack, int64_t stride, int n, const float* w, int64_t ncols, Epi<T> e,
+                  double bytes, int64_t max_grid = 0) {
+  int64_t grid = ((ncols + 3) / 4 + 64 * W * V - 1) / (64 * W * V);
+  const int64_t chunks = ((ncols + 3) / 4 + 63) / 64;
+  if (max_grid > 0) grid = max_grid < chunks ? max_grid : chunks;
+  char name[96];
+  snprintf(name, sizeof name, "rows%s V%d D%d W%d g%lld", IL ? "-il" : "-ct", V, D, W, (long long)grid);
+  return {name, bytes,
+          [=] {
+            hipLaunchKernelGGL((reduce_kernel_rows<AccF32, T, OP, V, D, W, true, IL>), dim3((unsigned)grid),
+                               dim3(64 * W), 0, 0, stack, stride, n, w, (int64_t)0, ncols, e);
+          },
+          true, {}};
+}
+
 template <int V, int U, int OP, typename T>
 Variant make_blocked(const float* stack, int n, const float* w, int64_t ncols, Epi<T> e, double bytes) {
   const int64_t B = 256 * V * 4;
@@ -257,6 +273,84 @@ int main(int argc, char** argv) {
     ONESHOT(10, 1, true);
     BAL(16, 1, 0);
     BAL(12, 1, 0);
+  }
+#define ROWSG(V, D, W, G)                                                                                      \
+  vs.push_back(op == FA_OP_AVGM      ? make_rows<V, D, W, FA_OP_AVGM, double>(stack, stride, n, w, ncols, e, bytes, G)   \
+               : op == FA_OP_ADAGRAD ? make_rows<V, D, W, FA_OP_ADAGRAD, double>(stack, stride, n, w, ncols, e, bytes, G) \
+                                     : make_rows<V, D, W, FA_OP_MEAN, double>(stack, stride, n, w, ncols, e, bytes, G))
+#define ROWS(V, D, W) ROWSG(V, D, W, 0)
+#define ROWSC(V, D, W, G)                                                                                      \
+  vs.push_back(op == FA_OP_AVGM      ? make_rows<V, D, W, FA_OP_AVGM, double, false>(stack, stride, n, w, ncols, e, bytes, G)   \
+               : op == FA_OP_ADAGRAD ? make_rows<V, D, W, FA_OP_ADAGRAD, double, false>(stack, stride, n, w, ncols, e, bytes, G) \
+                                     : make_rows<V, D, W, FA_OP_MEAN, double, false>(stack, stride, n, w, ncols, e, bytes, G))
+  if (!strcmp(set, "il")) {  // interleaved vs contiguous piece assignment
+    ONESHOTB(16, 1);
+    for (int g : {160, 192, 224, 256}) {
+      ROWSG(16, 1, 4, g);
+      ROWSC(16, 1, 4, g);
+      ROWSG(8, 2, 4, g);
+      ROWSC(8, 2, 4, g);
+    }
+    ROWSG(4, 4, 4, 192);
+    ROWSC(4, 4, 4, 192);
+    ROWSG(16, 2, 4, 192);
+  }
+  if (!strcmp(set, "inflight")) {  // blocks vs bytes in flight per block
+    ONESHOTB(16, 1);
+    ROWSG(16, 1, 4, 192);
+    ROWSG(16, 1, 4, 160);
+    ROWSG(16, 1, 4, 176);
+    ROWSG(16, 1, 4, 208);
+    ROWSG(12, 1, 4, 256);
+    ROWSG(12, 1, 4, 192);
+    ROWSG(8, 1, 4, 384);
+    ROWSG(8, 1, 4, 256);
+    ROWSG(16, 1, 3, 256);
+    ROWSG(16, 1, 2, 384);
+    ROWSG(16, 1, 2, 512);
+    ROWSG(8, 2, 4, 192);
+    ROWSG(4, 4, 4, 192);
+    ROWSG(4, 3, 4, 256);
+  }
+  if (!strcmp(set, "grid")) {  // balanced row pipeline: how many resident blocks stream best
+    ONESHOTB(16, 1);
+    for (int g : {128, 192, 224, 256, 384, 512}) {
+      ROWSG(16, 1, 4, g);
+      ROWSG(8, 2, 4, g);
+      ROWSG(4, 4, 4, g);
+    }
+    ROWSG(16, 2, 4, 256);
+    ROWSG(2, 8, 4, 256);
+    ROWSG(1, 16, 4, 256);
+  }
+  if (!strcmp(set, "rows")) {  // row-pipelined grid vs the product geometries
+    ONESHOTB(16, 1);
+    BALB(16, 1, 0);
+    BALB(4, 8, 0);
+    ROWS(1, 16, 1);
+    ROWS(2, 8, 1);
+    ROWS(4, 4, 1);
+    ROWS(4, 8, 1);
+    ROWS(2, 8, 4);
+    ROWS(4, 4, 4);
+    ROWS(4, 8, 4);
+    ROWS(8, 2, 4);
+    ROWS(8, 4, 4);
+    ROWS(16, 1, 4);
+    ROWS(16, 2, 4);
+  }
+  if (!strcmp(set, "narrow")) {  // many rows x few columns: per-rank shards of the multi-GPU runs
+    BAL(4, 4, 0);
+    BAL(4, 8, 0);
+    BAL(2, 8, 0);
+    BAL(2, 16, 0);
+    BAL(1, 16, 0);
+    BAL(4, 4, 1);
+    BALB(4, 4, 0);
+    BALB(4, 8, 0);
+    BALB(8, 4, 0);
+    BALB(16, 1, 0);
+    ONESHOTB(16, 1);
   }
   if (!strcmp(set, "main")) {
     ONESHOT(4, 1, true);
