@@ -1,0 +1,18 @@
+# Round-1 measurement pass for the row-pipelined kernel: parity suite, smoke, rocprofv3 kernel
+# traces and HBM counters (separate --pmc passes) for every config, plain bench runs.
+set -e
+R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out/r01v2
+mkdir -p $O
+timeout -k 10 400 python -u -m pytest $R/tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > $O/pytest_gpu.log 2>&1
+timeout -k 10 200 python -c "import sys; sys.path.insert(0, '$R'); import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
+cd /tmp && export TMPDIR=/tmp
+for c in c2 c3 c4 c5; do
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace_$c -o $c -- python3 $R/bench.py --config $c --no-cpu-baseline > $O/trace_${c}_bench.json 2> $O/trace_$c.err
+  timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/fetch_$c -o $c -- python3 $R/bench.py --config $c --no-cpu-baseline --steps 5 --warmup 1 > /dev/null 2> $O/fetch_$c.err
+  timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/write_$c -o $c -- python3 $R/bench.py --config $c --no-cpu-baseline --steps 5 --warmup 1 > /dev/null 2> $O/write_$c.err
+done
+for c in c2 c3 c4 c5; do
+  timeout -k 10 300 python3 $R/bench.py --config $c > $O/bench_$c.json 2> $O/bench_$c.err
+done
+echo done

@@ -283,6 +283,13 @@ int main(int argc, char** argv) {
   vs.push_back(op == FA_OP_AVGM      ? make_rows<V, D, W, FA_OP_AVGM, double, false>(stack, stride, n, w, ncols, e, bytes, G)   \
                : op == FA_OP_ADAGRAD ? make_rows<V, D, W, FA_OP_ADAGRAD, double, false>(stack, stride, n, w, ncols, e, bytes, G) \
                                      : make_rows<V, D, W, FA_OP_MEAN, double, false>(stack, stride, n, w, ncols, e, bytes, G))
+  if (!strcmp(set, "one")) {  // the product geometry against the roofs
+    ONESHOTB(16, 1);
+    ROWSG(16, 1, 4, 192);
+    ROWSG(16, 1, 4, 224);
+    ROWSG(16, 1, 4, 256);
+    ROWSG(32, 1, 4, 192);
+  }
   if (!strcmp(set, "il")) {  // interleaved vs contiguous piece assignment
     ONESHOTB(16, 1);
     for (int g : {160, 192, 224, 256}) {
