@@ -474,8 +474,8 @@ __device__ __forceinline__ typename vec4<typename P::acc_t>::type quad_mul(
 //     consumed, so D*V loads stay in flight per lane for the whole sweep (s_waitcnt
 //     vmcnt((D-1)*V) in the steady state, no drain per batch);
 //   * loads go through per-row buffer descriptors whose range check covers the window's end, so
-//     a partial last piece needs no per-lane branches; the one ragged quad (ncols % 4) goes to
-//     reduce_ragged.
+//     a partial last piece needs no per-lane branches (the slot offset rides in voffset, which
+//     the range check always covers); the one ragged quad (ncols % 4) goes to reduce_ragged.
 // The summation order (client list order, first product initialises the sum) is unchanged.
 template <class P, typename T, int OP, int V, int D, int W, bool NT>
 __device__ __forceinline__ void rows_piece(const float* __restrict__ stack, int64_t stride, int n,
@@ -500,14 +500,14 @@ __device__ __forceinline__ void rows_piece(const float* __restrict__ stack, int6
       if (1 + d < n) {
         const __amdgpu_buffer_rsrc_t r = row_rsrc(tile0 + (int64_t)(1 + d) * row_bytes, bytes);
 #pragma unroll
-        for (int v = 0; v < V; ++v) x[d][v] = buf_load_quad<NT>(r, voff, v * 64 * W * 16);
+        for (int v = 0; v < V; ++v) x[d][v] = buf_load_quad<NT>(r, voff + v * 64 * W * 16, 0);
       }
     AV acc[V];
     {
       const __amdgpu_buffer_rsrc_t r = row_rsrc(tile0, bytes);
       const typename P::w_t w0 = w[0];
 #pragma unroll
-      for (int v = 0; v < V; ++v) acc[v] = quad_mul<P>(w0, buf_load_quad<NT>(r, voff, v * 64 * W * 16));
+      for (int v = 0; v < V; ++v) acc[v] = quad_mul<P>(w0, buf_load_quad<NT>(r, voff + v * 64 * W * 16, 0));
     }
     // rows 1..n-1: slot d holds row i+d; consume it, refill it with row i+d+D (steady state:
     // every refill is a real row, so no branch)
@@ -524,7 +524,7 @@ __device__ __forceinline__ void rows_piece(const float* __restrict__ stack, int6
         __builtin_amdgcn_sched_barrier(0);
         const __amdgpu_buffer_rsrc_t r = row_rsrc(tile0 + (int64_t)(i + d + D) * row_bytes, bytes);
 #pragma unroll
-        for (int v = 0; v < V; ++v) x[d][v] = buf_load_quad<NT>(r, voff, v * 64 * W * 16);
+        for (int v = 0; v < V; ++v) x[d][v] = buf_load_quad<NT>(r, voff + v * 64 * W * 16, 0);
         __builtin_amdgcn_sched_barrier(0);
       }
     }
@@ -538,7 +538,7 @@ __device__ __forceinline__ void rows_piece(const float* __restrict__ stack, int6
         if (i + d + D < n) {
           const __amdgpu_buffer_rsrc_t r = row_rsrc(tile0 + (int64_t)(i + d + D) * row_bytes, bytes);
 #pragma unroll
-          for (int v = 0; v < V; ++v) x[d][v] = buf_load_quad<NT>(r, voff, v * 64 * W * 16);
+          for (int v = 0; v < V; ++v) x[d][v] = buf_load_quad<NT>(r, voff + v * 64 * W * 16, 0);
         }
       }
     }

@@ -15,4 +15,12 @@ done
 for c in c2 c3 c4 c5; do
   timeout -k 10 300 python3 $R/bench.py --config $c > $O/bench_$c.json 2> $O/bench_$c.err
 done
+for g in 2 4 8; do
+  for st in 1 2 4; do
+    timeout -k 10 200 python3 $R/bench.py --emulate-world $g --stripes $st --no-cpu-baseline > $O/emu_c2_weak_g${g}_s${st}.json 2>> $O/emu.err
+  done
+  timeout -k 10 200 python3 $R/bench.py --emulate-world $g --scaling strong --stripes 2 --no-cpu-baseline > $O/emu_c2_strong_g${g}_s2.json 2>> $O/emu.err
+  timeout -k 10 200 python3 $R/bench.py --emulate-world $g --scaling strong --config c3 --stripes 2 --no-cpu-baseline > $O/emu_c3_strong_g${g}_s2.json 2>> $O/emu.err
+done
+for c in c1 c2 c3; do timeout -k 10 300 python3 $R/tools/bench_e2e.py --config $c > $O/e2e_$c.json 2> $O/e2e_$c.err; done
 echo done
