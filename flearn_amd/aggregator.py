@@ -502,6 +502,16 @@ class Aggregator:
         self.output = output
         self.packer = Packer(self.devices, workers)
         self.last_plan: BucketPlan | None = None
+        self._wcache = {}  # (device, dtype, bytes) -> device weights: a pageable H2D per round saved
+
+    def _weights(self, nm: Numerics, device) -> torch.Tensor:
+        key = (str(device), nm.weights.dtype.str, nm.weights.tobytes())
+        t = self._wcache.get(key)
+        if t is None:
+            if len(self._wcache) >= 64:
+                self._wcache.clear()
+            t = self._wcache[key] = torch.from_numpy(np.ascontiguousarray(nm.weights)).to(device)
+        return t
 
     def ensemble(self, agg_weight_lst, w_local_lst, key_lst=None, server_opt: ServerOptimizer | None = None):
         plan = make_plan(agg_weight_lst, w_local_lst, key_lst)
@@ -518,7 +528,7 @@ class Aggregator:
             res = []
             for sh, stack in parts:
                 with torch.cuda.device(sh.device):
-                    w = torch.from_numpy(nm.weights).to(sh.device)
+                    w = self._weights(nm, sh.device)
                     if kind == KIND_F32:
                         out = self._reduce_f32(g, sh, stack, w, server_opt, fused, first_means)
                     else:

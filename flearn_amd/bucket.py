@@ -27,6 +27,7 @@ import torch
 from .semantics import KIND_F32, KIND_F64, KIND_I64, Numerics, resolve
 
 ALIGN = 64  # elements: 256 B for fp32, 512 B for 8-byte kinds
+SMALL_BYTES = 4 << 20  # below this, host packing / unpacking runs on the calling thread
 
 _STORE = {KIND_F32: np.float32, KIND_F64: np.float64, KIND_I64: np.int64}
 _TORCH = {np.float32: torch.float32, np.float64: torch.float64, np.int64: torch.int64}
@@ -176,7 +177,15 @@ class Packer:
         self._pinned = {}
         self._dev = {}
         self._shards = {}
+        self._pool = None
         self.last_wire_rows = 0
+
+    def _executor(self) -> concurrent.futures.ThreadPoolExecutor:
+        """One persistent pool per Packer: creating threads per call costs ~0.3 ms, which is the
+        whole budget of a LeNet-sized round."""
+        if self._pool is None:
+            self._pool = concurrent.futures.ThreadPoolExecutor(self.workers, thread_name_prefix="fa-pack")
+        return self._pool
 
     def _buf(self, cache, key, shape, dtype, **kw):
         t = cache.get(key)
@@ -288,17 +297,18 @@ class Packer:
 
         n = plan.n_clients
         workers = max(1, min(self.workers, n))
-        if workers == 1 or all(r is not None for r in rows):
+        nbytes = sum(int(d.numel()) * d.element_size() for d in devs)
+        if workers == 1 or nbytes < SMALL_BYTES or all(r is not None for r in rows):
             for r in range(n):
                 fill(r)
             ship(0, n)
             return
         chunk = max(workers, -(-n // 8))  # ~8 chunks, at least one row per worker
-        with concurrent.futures.ThreadPoolExecutor(workers) as ex:
-            for lo in range(0, n, chunk):
-                hi = min(n, lo + chunk)
-                list(ex.map(fill, range(lo, hi)))
-                ship(lo, hi)
+        ex = self._executor()
+        for lo in range(0, n, chunk):
+            hi = min(n, lo + chunk)
+            list(ex.map(fill, range(lo, hi)))
+            ship(lo, hi)
 
     def unpack(self, plan: BucketPlan, results: dict, as_torch: bool, out_dtype_override=None) -> dict:
         """results: kind -> [(shard, device tensor [shard.width])].  Returns {key: fresh value} in
@@ -330,9 +340,9 @@ class Packer:
             dst, d0, src, lo, hi = t
             np.copyto(dst[d0 : d0 + (hi - lo)], src[lo:hi])
 
-        if len(tasks) > 1 and self.workers > 1:
-            with concurrent.futures.ThreadPoolExecutor(self.workers) as ex:
-                list(ex.map(copy, tasks))
+        nbytes = sum(int(h.numel()) * h.element_size() for _, _, h in staged)
+        if len(tasks) > 1 and self.workers > 1 and nbytes >= SMALL_BYTES:
+            list(self._executor().map(copy, tasks))
         else:
             for t in tasks:
                 copy(t)

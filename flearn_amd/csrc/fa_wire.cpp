@@ -12,6 +12,7 @@
 // Pure host C++: no HIP calls.  The scanner accepts only the opcodes and globals that pickled
 // dicts / lists / tuples of numpy arrays and scalars use; anything else is reported as
 // FA_ERR_UNSUPPORTED and the caller falls back to a restricted Python unpickler.
+#include <immintrin.h>
 #include <pthread.h>
 
 #include <atomic>
@@ -165,11 +166,55 @@ const Tables& T() {
   return t;
 }
 
+// AVX2 decode of 8 groups (32 characters -> 24 bytes) per step: validation and translation by
+// nibble lookups (vpshufb), bit packing by vpmaddubsw / vpmaddwd, then a byte shuffle and a lane
+// permute (the published Mula-Lemire scheme).  Runs while >= 11 groups remain, so the 32-byte
+// store (24 decoded bytes + 8 that later groups overwrite) stays inside this call's output.
+// Returns the groups decoded; stops early at a block holding a non-alphabet character, which the
+// scalar loop then reports.
+__attribute__((target("avx2"))) int64_t dec_groups_avx2(const uint8_t* s, int64_t ng, uint8_t* d) {
+  const __m256i lut_lo = _mm256_setr_epi8(0x15, 0x11, 0x11, 0x11, 0x11, 0x11, 0x11, 0x11, 0x11, 0x11, 0x13, 0x1A,
+                                          0x1B, 0x1B, 0x1B, 0x1A, 0x15, 0x11, 0x11, 0x11, 0x11, 0x11, 0x11, 0x11,
+                                          0x11, 0x11, 0x13, 0x1A, 0x1B, 0x1B, 0x1B, 0x1A);
+  const __m256i lut_hi = _mm256_setr_epi8(0x10, 0x10, 0x01, 0x02, 0x04, 0x08, 0x04, 0x08, 0x10, 0x10, 0x10, 0x10,
+                                          0x10, 0x10, 0x10, 0x10, 0x10, 0x10, 0x01, 0x02, 0x04, 0x08, 0x04, 0x08,
+                                          0x10, 0x10, 0x10, 0x10, 0x10, 0x10, 0x10, 0x10);
+  const __m256i lut_roll = _mm256_setr_epi8(0, 16, 19, 4, -65, -65, -71, -71, 0, 0, 0, 0, 0, 0, 0, 0, 0, 16, 19, 4,
+                                            -65, -65, -71, -71, 0, 0, 0, 0, 0, 0, 0, 0);
+  const __m256i mask_2f = _mm256_set1_epi8(0x2F);
+  const __m256i pack_ab = _mm256_set1_epi32(0x01400140);
+  const __m256i pack_abc = _mm256_set1_epi32(0x00011000);
+  const __m256i shuf = _mm256_setr_epi8(2, 1, 0, 6, 5, 4, 10, 9, 8, 14, 13, 12, -1, -1, -1, -1, 2, 1, 0, 6, 5, 4, 10,
+                                        9, 8, 14, 13, 12, -1, -1, -1, -1);
+  const __m256i perm = _mm256_setr_epi32(0, 1, 2, 4, 5, 6, 7, 7);
+  int64_t g = 0;
+  for (; g + 11 <= ng; g += 8) {
+    __m256i str = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(s + 4 * g));
+    const __m256i hi_nib = _mm256_and_si256(_mm256_srli_epi32(str, 4), mask_2f);
+    const __m256i lo_nib = _mm256_and_si256(str, mask_2f);
+    const __m256i hi = _mm256_shuffle_epi8(lut_hi, hi_nib);
+    const __m256i lo = _mm256_shuffle_epi8(lut_lo, lo_nib);
+    if (!_mm256_testz_si256(lo, hi)) break;
+    const __m256i eq_2f = _mm256_cmpeq_epi8(str, mask_2f);
+    str = _mm256_add_epi8(str, _mm256_shuffle_epi8(lut_roll, _mm256_add_epi8(eq_2f, hi_nib)));
+    __m256i out = _mm256_madd_epi16(_mm256_maddubs_epi16(str, pack_ab), pack_abc);
+    out = _mm256_permutevar8x32_epi32(_mm256_shuffle_epi8(out, shuf), perm);
+    _mm256_storeu_si256(reinterpret_cast<__m256i*>(d + 3 * g), out);
+  }
+  return g;
+}
+
+const bool kAvx2 = __builtin_cpu_supports("avx2");
+
 // Decode `ng` full (unpadded) groups; returns false on a non-alphabet character.
 inline bool dec_groups(const uint8_t* s, int64_t ng, uint8_t* d) {
   const Tables& t = T();
   uint32_t bad = 0;
   int64_t g = 0;
+  if (kAvx2 && ng >= 11) {
+    const int64_t done = dec_groups_avx2(s, ng, d);
+    s += 4 * done, d += 3 * done, ng -= done;
+  }
   for (; g + 4 <= ng; g += 4, s += 16, d += 12) {
 #pragma GCC unroll 4
     for (int k = 0; k < 4; ++k) {
@@ -296,7 +341,9 @@ struct B64Reader {  // decodes the base64 text on demand, through a small window
   int64_t pos = 0;
   std::vector<uint8_t> win;
   int64_t w0 = 0, w1 = 0;  // window covers decoded [w0, w1)
-  explicit B64Reader(const B64& bb) : b(bb) { win.resize(1 << 16); }
+  // 4 KiB: the scanner reads headers (a few hundred bytes between payloads it skips); a wider
+  // window would decode payload bytes that fa_b64_decode_ranges decodes again
+  explicit B64Reader(const B64& bb) : b(bb) { win.resize(1 << 12); }
   bool read(int64_t len, uint8_t* out) {
     if (len < 0 || pos + len > b.total) return false;
     if (pos >= w0 && pos + len <= w1) {

@@ -53,10 +53,21 @@ _AsUTF8AndSize.argtypes = [ctypes.py_object, ctypes.POINTER(ctypes.c_ssize_t)]
 _PyUnicode_New = ctypes.pythonapi.PyUnicode_New
 _PyUnicode_New.restype = ctypes.py_object
 _PyUnicode_New.argtypes = [ctypes.c_ssize_t, ctypes.c_uint32]
+# a fresh, not yet shared bytes object whose buffer we fill (PyBytes_FromStringAndSize(NULL, n))
+_PyBytes_New = ctypes.pythonapi.PyBytes_FromStringAndSize
+_PyBytes_New.restype = ctypes.py_object
+_PyBytes_New.argtypes = [ctypes.c_void_p, ctypes.c_ssize_t]
+_PyBytes_AsString = ctypes.pythonapi.PyBytes_AsString
+_PyBytes_AsString.restype = ctypes.c_void_p
+_PyBytes_AsString.argtypes = [ctypes.py_object]
 
 
-def _threads() -> int:
-    return max(1, min(16, os.cpu_count() or 1))
+_THREADS = max(1, min(16, os.cpu_count() or 1))
+_SERIAL_BYTES = 1 << 20  # below ~1 MB of payload, waking the pool costs more than it saves
+
+
+def _threads(nbytes: int | None = None) -> int:
+    return 1 if nbytes is not None and nbytes < _SERIAL_BYTES else _THREADS
 
 
 def _ascii_ptr(s: str) -> tuple[int, int]:
@@ -96,21 +107,21 @@ def b64encode(raw) -> str:
         return out
     dst, _ = _ascii_ptr(out)
     src = np.frombuffer(mv, dtype=np.uint8)
-    _check(L, L.fa_b64_encode(src.ctypes.data, n, dst, m, _threads()), "base64 encode")
+    _check(L, L.fa_b64_encode(src.ctypes.data, n, dst, m, _threads(n)), "base64 encode")
     return out
 
 
-def b64decode(s: str) -> bytearray:
-    """base64.b64decode(s) for canonical input (what b64encode produces), natively."""
+def b64decode(s: str) -> bytes:
+    """base64.b64decode(s) for canonical input (what b64encode produces), natively, into a new
+    bytes object (no zero fill; io.BytesIO and pickle then read it without another copy)."""
     L = na.load()
     p, n = _ascii_ptr(s)
     total = L.fa_b64_decoded_size(p, n)
     if total < 0:
         raise _WireError(total, "not canonical base64")
-    out = bytearray(total)
+    out = _PyBytes_New(None, total)
     if total:
-        dst = (ctypes.c_char * total).from_buffer(out)
-        _check(L, L.fa_b64_decode(p, n, ctypes.addressof(dst), total, _threads()), "base64 decode")
+        _check(L, L.fa_b64_decode(p, n, _PyBytes_AsString(out), total, _threads(total)), "base64 decode")
     return out
 
 
@@ -383,7 +394,7 @@ def decode_fast(s: str):
     if offs:
         k = len(offs)
         rc = L.fa_b64_decode_ranges(p, n, k, (ctypes.c_int64 * k)(*offs), (ctypes.c_int64 * k)(*lens),
-                                    (ctypes.c_void_p * k)(*dsts), _threads())
+                                    (ctypes.c_void_p * k)(*dsts), _threads(sum(lens)))
         _check(L, rc, "payload decode")
     obj = dec.build(tree, row_np, aux_np)
     if planned is not None:
@@ -404,6 +415,9 @@ def _payload_nodes_list(tree):
 # ---------------------------------------------------------------------------------------------
 
 
+FAST_MIN_CHARS = 2 << 20  # base64 characters from which uploads are decoded into pinned rows
+
+
 class BaseEncrypt:
     """Identity codec (Encrypt.py:6-13)."""
 
@@ -415,7 +429,12 @@ class BaseEncrypt:
 
 
 class Encrypt(BaseEncrypt):
-    """base64(pickle) codec, byte-compatible with flearn's Encrypt (Encrypt.py:16-44)."""
+    """base64(pickle) codec, byte-compatible with flearn's Encrypt (Encrypt.py:16-44).
+    fast_min_chars: strings from this length on are decoded into pinned bucket rows (default
+    FAST_MIN_CHARS); shorter ones take native base64 + the restricted unpickler."""
+
+    def __init__(self, fast_min_chars: int | None = None):
+        self.fast_min_chars = FAST_MIN_CHARS if fast_min_chars is None else fast_min_chars
 
     def encode(self, params):
         """Encrypt.py:17-30: base64.b64encode(pickle.dumps(params)).decode()."""
@@ -423,8 +442,11 @@ class Encrypt(BaseEncrypt):
 
     def decode(self, glob_params):
         """Encrypt.py:32-44: pickle.loads(base64.b64decode(glob_params.encode())) — through the
-        scanner and the pinned-row decoder when possible, else the restricted unpickler."""
-        if isinstance(glob_params, str) and glob_params.isascii():
+        scanner and the pinned-row decoder when possible, else the restricted unpickler.
+        Small strings (< fast_min_chars, e.g. a LeNet upload) take the native base64 + restricted
+        unpickler route: the scanner's per-upload Python work (~0.3 ms) would exceed the pack
+        copy it saves."""
+        if isinstance(glob_params, str) and glob_params.isascii() and len(glob_params) >= self.fast_min_chars:
             try:
                 return decode_fast(glob_params)
             except _WireError as e:

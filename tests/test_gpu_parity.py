@@ -664,22 +664,24 @@ def test_distill_server_matches_reference(cuda):
 # ---------------------------------------------------------------------------------------------
 # HTTP mode: uploads arrive as base64(pickle) strings (Encrypt.py:16-44, Server.py:126-142)
 # ---------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("fast", [True, False])
 @pytest.mark.parametrize("shards", [1, 2])
 @pytest.mark.parametrize("name,strategy", [("avg_lenet5_n10", "avg"), ("avg_bnmodel_pyint_n4", "avg"),
                                            ("bn_strategy_n4", "bn")])
-def test_wire_uploads_through_the_engine(name, strategy, shards, cuda):
+def test_wire_uploads_through_the_engine(name, strategy, shards, fast, cuda):
     """Server.ensemble's loop: receive_processing(str) per upload, then server(); decoded fp32
-    params are DMA'd straight from the codec's pinned rows when their layout is the bucket's."""
+    params are DMA'd straight from the codec's pinned rows when their layout is the bucket's
+    (scanner route, fast=True) — small uploads by default take native base64 + unpickler."""
     from flearn_amd.wire import Encrypt
 
     g = Golden(name)
-    enc = Encrypt()
+    enc = Encrypt(fast_min_chars=0 if fast else None)
     strs = [enc.encode({"agg_weight": w, "params": c}) for w, c in zip(g.weights(), g.clients())]
     s = (BN if strategy == "bn" else AVG)(encrypt=enc, devices=[cuda] * shards)
     ups = [s.receive_processing(x) for x in strs]
     got = s.server(ups, 0)["w_glob"]
     assert_dict_bitwise(got, g.output(), name)
-    want_rows = 0 if strategy == "bn" else len(strs)  # BN drops keys: layouts differ -> plain pack
+    want_rows = 0 if strategy == "bn" or not fast else len(strs)  # BN drops keys: layouts differ -> plain pack
     assert s.engine.packer.last_wire_rows == want_rows
     back = enc.decode(s.upload_processing({"w_glob": got}))["w_glob"]
     assert_dict_bitwise(back, got, "round trip")
@@ -689,6 +691,6 @@ def test_wire_rows_are_pinned(cuda):
     from flearn_amd import wire
 
     up = {"agg_weight": 1.0, "params": {"w": np.arange(1000, dtype=np.float32)}}
-    d = wire.Encrypt().decode(wire.Encrypt().encode(up))
+    d = wire.Encrypt(fast_min_chars=0).decode(wire.Encrypt().encode(up))
     row = wire.wire_row(d["params"], (("w", (1000,), 0), 1024))
     assert row is not None and row.is_pinned()

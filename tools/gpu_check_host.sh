@@ -1,0 +1,9 @@
+# Parity suite + e2e (loopback) + HTTP-mode rounds after host-path changes.
+set -e
+R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out/host
+mkdir -p $O
+timeout -k 10 400 python -u -m pytest $R/tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > $O/pytest_gpu.log 2>&1
+for c in c1 c2 c3; do timeout -k 10 300 python3 $R/tools/bench_e2e.py --config $c > $O/e2e_$c.json 2> $O/e2e_$c.err; done
+for c in c1 c2; do timeout -k 10 300 python3 $R/tools/bench_wire.py --config $c > $O/wire_$c.json 2> $O/wire_$c.err; done
+echo done
