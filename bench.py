@@ -47,7 +47,8 @@ from flearn_amd.dist import ShardedReducer, ShardPlan, hip_reduce_fn  # noqa: E4
 METRIC = "device-resident GiB/s, FedAVG N-client weighted tensor reduce; %HBM peak"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
 GIB = 1024.0**3
-DEFAULT_STRIPES = 2  # N>1: stripe 0's all-gather overlaps stripe 1's reduce
+DEFAULT_STRIPES = 2  # N>1: stripe 0's all-gather overlaps stripe 1's reduce ...
+DEFAULT_STRIPE_WEIGHTS = (3, 1)  # ... and the small last stripe leaves little of the gather exposed
 
 CONFIGS = {
     "c2": dict(layout="resnet18", clients=100, op="mean",
@@ -129,6 +130,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--stripes", type=int, default=None, help="reduce/gather pipeline depth (N>1)")
+    ap.add_argument("--stripe-weights", default=None,
+                    help="relative stripe widths, e.g. 3,1 (default for 2 stripes); 'equal' for equal")
     ap.add_argument("--scaling", choices=("weak", "strong"), default="weak")
     ap.add_argument("--emulate-world", type=int, default=None,
                     help="single process: time rank 0's reduce of a G-GPU job (no gather)")
@@ -156,7 +159,13 @@ def main():
     n = cfg["clients"] * (g_eff if args.scaling == "weak" else 1)
     p_real = layouts.fp32_elems(layout)
     stripes = args.stripes or (1 if g_eff == 1 else DEFAULT_STRIPES)
-    plan = ShardPlan.make(p_real, g_eff, rank, stripes)
+    if args.stripe_weights == "equal" or stripes == 1:
+        sw = None
+    elif args.stripe_weights:
+        sw = tuple(float(x) for x in args.stripe_weights.split(","))
+    else:
+        sw = DEFAULT_STRIPE_WEIGHTS if stripes == len(DEFAULT_STRIPE_WEIGHTS) else None
+    plan = ShardPlan.make(p_real, g_eff, rank, stripes, weights=sw)
     cols = plan.local_cols
 
     # ---- device-resident synthetic uploads: this rank's columns of all N clients ----
@@ -164,7 +173,8 @@ def main():
     stack = torch.empty((n, cols), dtype=torch.float32, device=dev)
     for c in range(stripes):
         lo = plan.local_begin(c)
-        agg.fill_uniform(stack[:, lo:], seed=2024, row_begin=0, col_begin=plan.global_begin(c), n_cols=plan.shard)
+        agg.fill_uniform(stack[:, lo:], seed=2024, row_begin=0, col_begin=plan.global_begin(c),
+                         n_cols=plan.shard_of(c))
     weights = torch.ones(n, dtype=torch.float32, device=dev)  # Python 1.0 -> fl32(1.0)
     denom = float(np.sum([1.0] * n))  # np.sum(agg_weight_lst), strategy.py:127
     epi = {}
@@ -173,7 +183,7 @@ def main():
         prev = torch.empty((1, cols), dtype=torch.float32, device=dev)
         for c in range(stripes):
             lo = plan.local_begin(c)
-            agg.fill_uniform(prev[:, lo:], seed=1, col_begin=plan.global_begin(c), n_cols=plan.shard)
+            agg.fill_uniform(prev[:, lo:], seed=1, col_begin=plan.global_begin(c), n_cols=plan.shard_of(c))
         prev = prev[0]
         v = torch.zeros(cols, dtype=torch.float64, device=dev)
         epi = dict(op=na.OP_BY_NAME[cfg["op"]], prev=prev, v=v)
@@ -269,7 +279,8 @@ def main():
                 "layout": cfg["layout"],
                 "epilogue": cfg["op"],
                 "parallelism": ("single GPU" if g_eff == 1 else
-                                f"element-range shards x{g_eff} + RCCL all-gather ({stripes} stripes)"
+                                f"element-range shards x{g_eff} + RCCL all-gather ({stripes} stripes"
+                                + (f", widths {'/'.join(str(x) for x in plan.widths)}" if stripes > 1 else "") + ")"
                                 + (f"; EMULATED: rank 0's reduce of a {emu}-GPU job on one GPU, no gather"
                                    if emu else "")),
                 "hbm_peak_frac_of_value": round(value * GIB / 1e9 / HBM_PEAK_GBS, 4),

@@ -7,10 +7,10 @@ global model.  Layer-granular sharding (what the north star's wording suggests) 
 ResNet-18 at ~5x on 8 GPUs because fc/layer4 tensors are up to 20% of the model; columns
 balance exactly.
 
-Column layout (block-cyclic, `stripes` stripes):
-    P_pad = stripes * world * S,  S a multiple of 64 (256-B aligned shard slices)
-    stripe c covers global columns [c*W*S, (c+1)*W*S); rank r owns [c*W*S + r*S, +S)
-    rank r's local stack is [N, stripes*S]: local column c*S + j <-> global c*W*S + r*S + j
+Column layout (block-cyclic, `stripes` stripes of per-rank widths S_c, multiples of 64):
+    O_c = S_0 + ... + S_{c-1};  P_pad = W * (S_0 + ... + S_{last})
+    stripe c covers global columns [W*O_c, W*(O_c + S_c)); rank r owns [W*O_c + r*S_c, +S_c)
+    rank r's local stack is [N, sum S_c]: local column O_c + j <-> global W*O_c + r*S_c + j
 so the all-gather of stripe c writes one contiguous range of the global bucket, and stripe c's
 gather (on RCCL's stream) overlaps the reduce of stripe c+1 (on the compute stream).
 Optimizer state (prev, v_t) is sharded the same way and never communicated.
@@ -30,40 +30,72 @@ class ShardPlan:
     n_cols: int  # real global columns (parameters)
     world: int
     rank: int
-    stripes: int
-    shard: int  # S: columns per (stripe, rank) slice
+    widths: tuple  # S_c: columns per (stripe c, rank) slice, each a multiple of ALIGN
 
     @staticmethod
-    def make(n_cols: int, world: int, rank: int, stripes: int = 4) -> "ShardPlan":
+    def make(n_cols: int, world: int, rank: int, stripes: int = 4, weights=None) -> "ShardPlan":
+        """Equal stripes by default; `weights` (one per stripe) sizes them unevenly, e.g. (3, 1):
+        the gather of the big first stripe hides behind the small last stripe's reduce and only
+        the last stripe's gather stays exposed."""
         if world < 1 or not 0 <= rank < world or stripes < 1:
             raise ValueError("bad world / rank / stripes")
-        per = -(-max(n_cols, 1) // (world * stripes))
-        shard = -(-per // ALIGN) * ALIGN
-        return ShardPlan(n_cols, world, rank, stripes, shard)
+        if weights is None:
+            per = -(-max(n_cols, 1) // (world * stripes))
+            return ShardPlan(n_cols, world, rank, (-(-per // ALIGN) * ALIGN,) * stripes)
+        weights = tuple(float(x) for x in weights)
+        if len(weights) != stripes or min(weights) <= 0:
+            raise ValueError("need one positive weight per stripe")
+        total = -(-max(n_cols, 1) // world)  # columns per rank
+        total = -(-total // ALIGN) * ALIGN
+        widths, acc = [], 0
+        for c in range(stripes - 1):
+            w = -(-int(total * weights[c] / sum(weights)) // ALIGN) * ALIGN
+            w = max(ALIGN, min(w, total - acc - ALIGN * (stripes - 1 - c)))
+            widths.append(w)
+            acc += w
+        widths.append(max(ALIGN, total - acc))
+        return ShardPlan(n_cols, world, rank, tuple(widths))
+
+    @property
+    def stripes(self) -> int:
+        return len(self.widths)
+
+    @property
+    def shard(self) -> int:
+        """The slice width when all stripes are equal."""
+        if len(set(self.widths)) != 1:
+            raise ValueError("stripes differ in width: use shard_of(stripe)")
+        return self.widths[0]
+
+    def shard_of(self, stripe: int) -> int:
+        return self.widths[stripe]
 
     @property
     def padded(self) -> int:
-        return self.stripes * self.world * self.shard
+        return self.world * sum(self.widths)
 
     @property
     def local_cols(self) -> int:
-        return self.stripes * self.shard
+        return sum(self.widths)
+
+    def local_begin(self, stripe: int) -> int:
+        return sum(self.widths[:stripe])
 
     def global_begin(self, stripe: int, rank: int | None = None) -> int:
         r = self.rank if rank is None else rank
-        return stripe * self.world * self.shard + r * self.shard
-
-    def local_begin(self, stripe: int) -> int:
-        return stripe * self.shard
+        return self.world * self.local_begin(stripe) + r * self.widths[stripe]
 
     def local_to_global(self, local_col: int) -> int:
-        c, j = divmod(local_col, self.shard)
-        return self.global_begin(c) + j
+        for c in range(self.stripes):
+            lo = self.local_begin(c)
+            if local_col < lo + self.widths[c]:
+                return self.global_begin(c) + (local_col - lo)
+        raise IndexError(local_col)
 
     def real_cols_in_slice(self, stripe: int, rank: int | None = None) -> int:
         """Columns of this slice that are real parameters (the tail slices may be padding)."""
         g0 = self.global_begin(stripe, rank)
-        return max(0, min(self.shard, self.n_cols - g0))
+        return max(0, min(self.widths[stripe], self.n_cols - g0))
 
 
 class ShardedReducer:
@@ -93,11 +125,12 @@ class ShardedReducer:
         p = self.plan
         works = []
         for c in range(p.stripes):
-            lo = p.local_begin(c)
-            self.reduce_fn(lo, p.shard, self.local_out[lo : lo + p.shard])
+            lo, sc = p.local_begin(c), p.shard_of(c)
+            self.reduce_fn(lo, sc, self.local_out[lo : lo + sc])
             if self.gather:
-                dst = self.full[c * p.world * p.shard : (c + 1) * p.world * p.shard]
-                works.append(dist.all_gather_into_tensor(dst, self.local_out[lo : lo + p.shard],
+                g0 = p.world * lo  # stripe c's contiguous range of the global bucket
+                dst = self.full[g0 : g0 + p.world * sc]
+                works.append(dist.all_gather_into_tensor(dst, self.local_out[lo : lo + sc],
                                                          group=self.group, async_op=True))
         for w in works:
             w.wait()

@@ -21,13 +21,13 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, n, p, stripes, op):
+def _worker(rank, world, port, n, p, stripes, op, weights=None):
     import oracle
     from flearn_amd.dist import ShardedReducer, ShardPlan
 
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     try:
-        plan = ShardPlan.make(p, world, rank, stripes)
+        plan = ShardPlan.make(p, world, rank, stripes, weights=weights)
         local = np.zeros((n, plan.local_cols), np.float32)
         prev = np.zeros(plan.local_cols, np.float32)
         for c in range(stripes):
@@ -61,8 +61,15 @@ def _worker(rank, world, port, n, p, stripes, op):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("p,stripes,op", [(44_426, 4, "mean"), (100_003, 3, "avgm"), (5_000, 1, "adagrad"),
-                                          (63, 2, "mean")])
-def test_sharded_reduce_two_ranks(p, stripes, op):
+@pytest.mark.parametrize("p,stripes,op,weights", [(44_426, 4, "mean", None), (100_003, 3, "avgm", None),
+                                                  (5_000, 1, "adagrad", None), (63, 2, "mean", None),
+                                                  (100_003, 2, "avgm", (3, 1)), (44_426, 3, "mean", (1, 2, 1))])
+def test_sharded_reduce_two_ranks(p, stripes, op, weights):
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-    mp.spawn(_worker, args=(2, _free_port(), 7, p, stripes, op), nprocs=2, join=True)
+    mp.spawn(_worker, args=(2, _free_port(), 7, p, stripes, op, weights), nprocs=2, join=True)
+
+
+def test_sharded_reduce_four_ranks():
+    """More ranks than the GPU box's CI can rehearse on one card: world 4, uneven stripes."""
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    mp.spawn(_worker, args=(4, _free_port(), 5, 70_001, 2, "mean", (3, 1)), nprocs=4, join=True)

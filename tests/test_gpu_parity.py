@@ -410,8 +410,9 @@ def test_baseline_config_spot_parity(layout, n, op, cuda):
 # ---------------------------------------------------------------------------------------------
 
 
+@pytest.mark.parametrize("stripes,weights", [(4, None), (2, (3, 1))])
 @pytest.mark.parametrize("op", ["mean", "avgm"])
-def test_sharded_reducer_rccl_one_rank(op, cuda, tmp_path):
+def test_sharded_reducer_rccl_one_rank(op, stripes, weights, cuda, tmp_path):
     import torch.distributed as dist
 
     from flearn_amd.dist import ShardedReducer, ShardPlan, hip_reduce_fn
@@ -423,11 +424,11 @@ def test_sharded_reducer_rccl_one_rank(op, cuda, tmp_path):
         created = True
     try:
         n, p = 9, 1_000_003
-        plan = ShardPlan.make(p, 1, 0, stripes=4)
+        plan = ShardPlan.make(p, 1, 0, stripes=stripes, weights=weights)
         stack = torch.empty((n, plan.local_cols), dtype=torch.float32, device=cuda)
         for c in range(plan.stripes):
             agg.fill_uniform(stack[:, plan.local_begin(c):], seed=3, col_begin=plan.global_begin(c),
-                             n_cols=plan.shard)
+                             n_cols=plan.shard_of(c))
         w = torch.ones(n, dtype=torch.float32, device=cuda)
         epi, local_out = {}, None
         if op != "mean":

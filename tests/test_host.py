@@ -194,14 +194,23 @@ def test_product_never_imports_the_oracle():
         assert "import oracle" not in f.read_text(), f
 
 
-@pytest.mark.parametrize("n_cols,world,stripes", [(1, 1, 1), (11_699_112, 8, 4), (44_426, 2, 3), (1000, 4, 4)])
-def test_shard_plan_covers_columns_once(n_cols, world, stripes):
-    seen = np.zeros(ShardPlan.make(n_cols, world, 0, stripes).padded, dtype=np.int32)
+@pytest.mark.parametrize("n_cols,world,stripes,weights", [
+    (1, 1, 1, None), (11_699_112, 8, 4, None), (44_426, 2, 3, None), (1000, 4, 4, None),
+    (11_699_112, 8, 2, (3, 1)), (44_426, 2, 3, (1, 2, 1)), (63, 2, 2, (3, 1)), (25_610_152, 4, 2, (4, 1))])
+def test_shard_plan_covers_columns_once(n_cols, world, stripes, weights):
+    p0 = ShardPlan.make(n_cols, world, 0, stripes, weights=weights)
+    seen = np.zeros(p0.padded, dtype=np.int32)
+    assert p0.padded >= n_cols and p0.stripes == stripes
     for r in range(world):
-        p = ShardPlan.make(n_cols, world, r, stripes)
-        assert p.shard % 64 == 0
+        p = ShardPlan.make(n_cols, world, r, stripes, weights=weights)
+        assert p.widths == p0.widths and all(w % 64 == 0 and w > 0 for w in p.widths)
         for c in range(stripes):
             g0 = p.global_begin(c)
-            seen[g0 : g0 + p.shard] += 1
+            seen[g0 : g0 + p.shard_of(c)] += 1
             assert p.local_to_global(p.local_begin(c)) == g0
+            assert p.local_to_global(p.local_begin(c) + p.shard_of(c) - 1) == g0 + p.shard_of(c) - 1
     assert (seen == 1).all()
+    if weights:  # widths follow the weights (to 64-column granularity)
+        tot = sum(p0.widths)
+        for wd, wt in zip(p0.widths, weights):
+            assert abs(wd / tot - wt / sum(weights)) <= 64 * stripes / tot + 1e-9 or tot <= 64 * stripes
