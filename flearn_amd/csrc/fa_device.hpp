@@ -567,7 +567,8 @@ __device__ __forceinline__ void rows_piece(const float* __restrict__ stack, int6
 //   INTERLEAVE: block b takes pieces b, b+grid, b+2*grid, ...: at any moment the grid's pieces
 //               form one contiguous stretch of each row (a linear-read access pattern);
 //   otherwise:  block b takes k consecutive pieces (one contiguous share of the window).
-template <class P, typename T, int OP, int V, int D, int W, bool NT, bool INTERLEAVE = true>
+template <class P, typename T, int OP, int V, int D, int W, bool NT, bool INTERLEAVE = true,
+          bool XCDMAP = false>
 __global__ __launch_bounds__(64 * W) void reduce_kernel_rows(const float* __restrict__ stack,
                                                              int64_t stride, int n,
                                                              const typename P::w_t* __restrict__ w,
@@ -580,7 +581,10 @@ __global__ __launch_bounds__(64 * W) void reduce_kernel_rows(const float* __rest
   const int64_t pc = (chunks + g * k - 1) / (g * k);         // chunks per piece (<= W*V)
   const int64_t pieces = (chunks + pc - 1) / pc;
   const int64_t step = INTERLEAVE ? g : 1;
-  const int64_t first = INTERLEAVE ? blockIdx.x : blockIdx.x * k;
+  // XCDMAP (tuning): blocks b, b+8, b+16, ... share an XCD under round-robin placement; give
+  // them consecutive piece slots so each XCD streams one contiguous stretch per round
+  const int64_t slot = (XCDMAP && g % 8 == 0) ? (blockIdx.x % 8) * (g / 8) + blockIdx.x / 8 : blockIdx.x;
+  const int64_t first = INTERLEAVE ? slot : slot * k;
   const int64_t last = INTERLEAVE ? pieces : (first + k < pieces ? first + k : pieces);
   for (int64_t p = first; p < last; p += step) {
     const int64_t qs = p * pc * 64;

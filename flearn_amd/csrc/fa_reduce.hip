@@ -4,9 +4,10 @@
 // fa_device.hpp on the caller's stream.  No allocation, no synchronisation, no host copies.
 // Geometry (measured with tools/tune_reduce.hip on MI355X):
 //   * fp32 client stacks (every configuration of the hot path): the row-pipelined kernel on
-//     192 blocks (0.75 per CU) with equal shares of the window; each block sweeps its share in
-//     pieces of V KiB x 4 waves, rows pipelined D = 16/V deep through per-row buffer descriptors
-//     (~64 KiB of client rows in flight per block, whatever the window's width or depth);
+//     192 blocks (0.75 per CU) with equal interleaved pieces of the window; each block sweeps its
+//     pieces (V KiB x W waves wide; W = 4 for the mean, 8 with a fused optimizer epilogue), rows
+//     pipelined D = 64/(V*W) deep through per-row buffer descriptors (~64 KiB of client rows in
+//     flight per block, whatever the window's width or depth);
 //   * 8-byte kinds (f64 / i64 buckets, small): 4 quads per thread, one row at a time.
 #include <hip/hip_runtime.h>
 
@@ -83,17 +84,19 @@ int launch_check() {
 // x CUs blocks, equal interleaved pieces.  The piece width and pipeline depth follow the share s
 // (KiB of every row per block): the narrowest piece that covers s (or 16 KiB per wave), D = 16/V
 // rows deep, so a block keeps ~64 KiB of client rows in flight whatever the window's shape.
-constexpr int kRowsWaves = 4;  // W: 256-thread blocks
-// Fewer blocks than CUs stream best: 192 on 256 CUs for the plain mean; the fused
-// optimizer epilogues (state reads/writes at the end of every piece) like a few more in flight.
+// Fewer blocks than CUs stream best: 192 blocks on 256 CUs, each keeping ~64 KiB
+// of client rows in flight.  Plain mean: 4 waves x up to 16 KiB per row; fused optimizer
+// epilogues: 8 waves x up to 8 KiB (half the per-lane state work at every piece end, twice the
+// waves to overlap it: +2-4% on C3/C5).
 constexpr double kRowsBlocksPerCU = 0.75;
-constexpr double kRowsBlocksPerCUEpilogue = 0.875;
+constexpr int kPieceChunks = 64;  // max KiB of a row per block and piece (= W * Vmax)
 
-template <class P, typename T, int OP, int V>
+template <class P, typename T, int OP, int V, int W>
 int launch_rows(const float* stack, int64_t stride, int n, const typename P::w_t* w, int64_t col0,
                 int64_t ncols, const Epi<T>& e, int64_t grid, hipStream_t s) {
-  hipLaunchKernelGGL((reduce_kernel_rows<P, T, OP, V, 16 / V, kRowsWaves, kNT>), dim3((unsigned)grid),
-                     dim3(64 * kRowsWaves), 0, s, stack, stride, n, w, col0, ncols, e);
+  static_assert(V * W <= kPieceChunks, "piece wider than the in-flight budget");
+  hipLaunchKernelGGL((reduce_kernel_rows<P, T, OP, V, kPieceChunks / (V * W), W, kNT>), dim3((unsigned)grid),
+                     dim3(64 * W), 0, s, stack, stride, n, w, col0, ncols, e);
   return launch_check();
 }
 
@@ -104,15 +107,28 @@ int launch_reduce(const typename P::x_t* stack, int64_t stride, int n, const voi
   const int cus = device_cus();
   const int64_t chunks = ((ncols + 3) / 4 + 63) / 64;  // 1-KiB row pieces
   if constexpr (sizeof(typename P::x_t) == 4) {
-    int64_t grid = (int64_t)(cus * (OP == FA_OP_MEAN ? kRowsBlocksPerCU : kRowsBlocksPerCUEpilogue) + 0.5);
+    int64_t grid = (int64_t)(cus * kRowsBlocksPerCU + 0.5);
+    // a window just wider than one round of full pieces: a few more blocks (up to one per CU)
+    // instead of a second, nearly empty round
+    if (chunks > grid * kPieceChunks && chunks <= (int64_t)cus * kPieceChunks)
+      grid = (chunks + kPieceChunks - 1) / kPieceChunks;
     if (grid < 1) grid = 1;
     if (grid > chunks) grid = chunks;
     const int64_t share = (chunks + grid - 1) / grid;  // chunks per block
-    if (share <= 1 * kRowsWaves) return launch_rows<P, T, OP, 1>(stack, stride, n, wt, col0, ncols, e, grid, s);
-    if (share <= 2 * kRowsWaves) return launch_rows<P, T, OP, 2>(stack, stride, n, wt, col0, ncols, e, grid, s);
-    if (share <= 4 * kRowsWaves) return launch_rows<P, T, OP, 4>(stack, stride, n, wt, col0, ncols, e, grid, s);
-    if (share <= 8 * kRowsWaves) return launch_rows<P, T, OP, 8>(stack, stride, n, wt, col0, ncols, e, grid, s);
-    return launch_rows<P, T, OP, 16>(stack, stride, n, wt, col0, ncols, e, grid, s);
+    if constexpr (OP == FA_OP_MEAN) {
+      constexpr int W = 4;
+      if (share <= 1 * W) return launch_rows<P, T, OP, 1, W>(stack, stride, n, wt, col0, ncols, e, grid, s);
+      if (share <= 2 * W) return launch_rows<P, T, OP, 2, W>(stack, stride, n, wt, col0, ncols, e, grid, s);
+      if (share <= 4 * W) return launch_rows<P, T, OP, 4, W>(stack, stride, n, wt, col0, ncols, e, grid, s);
+      if (share <= 8 * W) return launch_rows<P, T, OP, 8, W>(stack, stride, n, wt, col0, ncols, e, grid, s);
+      return launch_rows<P, T, OP, 16, W>(stack, stride, n, wt, col0, ncols, e, grid, s);
+    } else {
+      constexpr int W = 8;
+      if (share <= 1 * W) return launch_rows<P, T, OP, 1, W>(stack, stride, n, wt, col0, ncols, e, grid, s);
+      if (share <= 2 * W) return launch_rows<P, T, OP, 2, W>(stack, stride, n, wt, col0, ncols, e, grid, s);
+      if (share <= 4 * W) return launch_rows<P, T, OP, 4, W>(stack, stride, n, wt, col0, ncols, e, grid, s);
+      return launch_rows<P, T, OP, 8, W>(stack, stride, n, wt, col0, ncols, e, grid, s);
+    }
   } else {
     // 8-byte kinds (f64 / i64 buckets: BN counters, float64 state; small): 4 quads per thread,
     // one row at a time, round-balanced grid

@@ -180,7 +180,8 @@ def test_reduce_kernel_big_tiles_ragged(n, ncols, cuda):
 # row-pipeline geometry: each (n, ncols) lands on a different piece width V (1, 2, 4, 8, 16 KiB
 # per wave) and pipeline depth D = 16/V on the 192/224-block grid, with ragged piece and window
 # ends; deep stacks are the per-rank shapes of the multi-GPU runs
-ROW_SHAPES = [(800, 150001), (300, 390001), (200, 700003), (64, 1500007), (40, 3300001), (17, 33), (2, 5000003)]
+ROW_SHAPES = [(800, 150001), (300, 390001), (200, 700003), (64, 1500007), (40, 3300001), (17, 33), (2, 5000003),
+              (12, 3500001)]  # the last one widens the grid to one full piece per block
 
 
 @pytest.mark.parametrize("n,ncols", ROW_SHAPES)
@@ -195,7 +196,9 @@ def test_row_pipeline_geometries(n, ncols, cuda):
     assert bitwise_equal(out64.cpu().numpy(), want)
 
 
-@pytest.mark.parametrize("n,ncols,op", [(300, 390001, "avgm"), (64, 1500007, "adagrad"), (800, 150001, "adam")])
+@pytest.mark.parametrize("n,ncols,op", [(300, 390001, "avgm"), (64, 1500007, "adagrad"), (800, 150001, "adam"),
+                                         (50, 700003, "yogi"), (20, 3000001, "avgm"), (10, 3500001, "adagrad"),
+                                         (6, 9000003, "avgm")])
 def test_row_pipeline_fused_epilogues(n, ncols, op, cuda):
     stride = -(-ncols // 64) * 64
     x = _device_stack(n, stride, seed=ncols)

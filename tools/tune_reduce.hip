@@ -117,17 +117,18 @@ Variant make_balanced(const float* stack, int64_t stride, int n, const float* w,
           true, {}};
 }
 
-template <int V, int D, int W, int OP, typename T, bool IL = true>
+template <int V, int D, int W, int OP, typename T, bool IL = true, bool XM = false, bool NTL = true>
 Variant make_rows(const float* stack, int64_t stride, int n, const float* w, int64_t ncols, Epi<T> e,
                   double bytes, int64_t max_grid = 0) {
   int64_t grid = ((ncols + 3) / 4 + 64 * W * V - 1) / (64 * W * V);
   const int64_t chunks = ((ncols + 3) / 4 + 63) / 64;
   if (max_grid > 0) grid = max_grid < chunks ? max_grid : chunks;
   char name[96];
-  snprintf(name, sizeof name, "rows%s V%d D%d W%d g%lld", IL ? "-il" : "-ct", V, D, W, (long long)grid);
+  snprintf(name, sizeof name, "rows%s%s%s V%d D%d W%d g%lld", IL ? "-il" : "-ct", XM ? "-xcd" : "",
+           NTL ? "" : "-temporal", V, D, W, (long long)grid);
   return {name, bytes,
           [=] {
-            hipLaunchKernelGGL((reduce_kernel_rows<AccF32, T, OP, V, D, W, true, IL>), dim3((unsigned)grid),
+            hipLaunchKernelGGL((reduce_kernel_rows<AccF32, T, OP, V, D, W, NTL, IL, XM>), dim3((unsigned)grid),
                                dim3(64 * W), 0, 0, stack, stride, n, w, (int64_t)0, ncols, e);
           },
           true, {}};
@@ -283,6 +284,30 @@ int main(int argc, char** argv) {
   vs.push_back(op == FA_OP_AVGM      ? make_rows<V, D, W, FA_OP_AVGM, double, false>(stack, stride, n, w, ncols, e, bytes, G)   \
                : op == FA_OP_ADAGRAD ? make_rows<V, D, W, FA_OP_ADAGRAD, double, false>(stack, stride, n, w, ncols, e, bytes, G) \
                                      : make_rows<V, D, W, FA_OP_MEAN, double, false>(stack, stride, n, w, ncols, e, bytes, G))
+#define ROWSX(V, D, W, G, XM, NTL)                                                                                      \
+  vs.push_back(op == FA_OP_AVGM      ? make_rows<V, D, W, FA_OP_AVGM, double, true, XM, NTL>(stack, stride, n, w, ncols, e, bytes, G)   \
+               : op == FA_OP_ADAGRAD ? make_rows<V, D, W, FA_OP_ADAGRAD, double, true, XM, NTL>(stack, stride, n, w, ncols, e, bytes, G) \
+                                     : make_rows<V, D, W, FA_OP_MEAN, double, true, XM, NTL>(stack, stride, n, w, ncols, e, bytes, G))
+  if (!strcmp(set, "epi")) {  // fused-epilogue geometry: 4 vs 8 waves per block
+    ROWSG(16, 1, 4, 224);
+    ROWSG(16, 1, 4, 192);
+    ROWSG(8, 1, 8, 160);
+    ROWSG(8, 1, 8, 192);
+    ROWSG(8, 1, 8, 224);
+    ROWSG(8, 1, 8, 256);
+    ROWSG(4, 2, 8, 192);
+    ROWSG(2, 4, 8, 192);
+    ROWSG(1, 8, 8, 192);
+  }
+  if (!strcmp(set, "misc")) {
+    ROWSX(16, 1, 4, 192, false, true);
+    ROWSX(16, 1, 4, 192, true, true);
+    ROWSX(16, 1, 4, 192, false, false);
+    ROWSX(8, 1, 8, 192, false, true);
+    ROWSX(8, 2, 8, 192, false, true);
+    ROWSX(4, 4, 8, 192, false, true);
+    ROWSX(16, 1, 4, 256, true, true);
+  }
   if (!strcmp(set, "one")) {  // the product geometry against the roofs
     ONESHOTB(16, 1);
     ROWSG(16, 1, 4, 192);
