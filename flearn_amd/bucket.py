@@ -179,6 +179,7 @@ class Packer:
         self._shards = {}
         self._pool = None
         self.last_wire_rows = 0
+        self.last_wire_staged = 0
 
     def _executor(self) -> concurrent.futures.ThreadPoolExecutor:
         """One persistent pool per Packer: creating threads per call costs ~0.3 ms, which is the
@@ -225,6 +226,7 @@ class Packer:
         """Copy every client's selected tensors into the device buckets.
         Returns kind -> [(shard, device stack [N, shard.width])]."""
         out = {}
+        self.last_wire_staged = 0
         for kind, g in plan.groups.items():
             tdt = _TORCH[g.store_dtype]
             shards = self.shards(plan, kind)
@@ -237,6 +239,12 @@ class Packer:
                         devs[sh.index][n, d : d + (b - a)].copy_(w[s.key].reshape(-1)[a:b])
             else:
                 rows = self._wire_rows(g, w_local_lst) if kind == KIND_F32 else [None] * plan.n_clients
+                if len(shards) == 1 and all(r is not None for r in rows):
+                    staged = self._wire_stack(g, w_local_lst, shards[0].device)
+                    if staged is not None:  # uploads already copied to the device at decode time
+                        out[kind] = [(shards[0], staged)]
+                        self.last_wire_staged = plan.n_clients
+                        continue
                 if all(r is not None for r in rows):
                     hosts = [None] * len(shards)  # every row already sits in pinned memory
                 else:
@@ -245,6 +253,12 @@ class Packer:
                 self._pack_pipelined(plan, pieces, w_local_lst, shards, hosts, devs, rows)
             out[kind] = list(zip(shards, devs))
         return out
+
+    def _wire_stack(self, g: Group, w_local_lst, device):
+        from .wire import wire_device_stack
+
+        sig = tuple((s.key, s.shape, s.offset) for s in g.segments) + (g.stride,)
+        return wire_device_stack(w_local_lst, sig, device)
 
     def _wire_rows(self, g: Group, w_local_lst) -> list:
         """Per client: the pinned row the wire codec decoded its fp32 params into, when that row

@@ -42,7 +42,8 @@ import torch
 from . import _native as na
 from .bucket import ALIGN
 
-__all__ = ["BaseEncrypt", "Encrypt", "b64encode", "b64decode", "wire_row"]
+__all__ = ["BaseEncrypt", "Encrypt", "b64encode", "b64decode", "wire_row", "wire_device_stack",
+           "release_device_staging"]
 
 _F32 = np.dtype("<f4")
 
@@ -188,12 +189,102 @@ class _RowArray(np.ndarray):
     long as any of them (the registry below only holds a weak reference)."""
 
 
-def _register(params: dict, row_np: _RowArray, layout: tuple):
+def _register(params: dict, row_np: _RowArray, layout: tuple, staged=None):
     with _ROWS_LOCK:
         if len(_ROWS) > 4096:
-            for k in [k for k, (ref, _) in _ROWS.items() if ref() is None]:
+            for k in [k for k, ent in _ROWS.items() if ent[0]() is None]:
                 del _ROWS[k]
-        _ROWS[id(params)] = (weakref.ref(row_np), layout)
+        _ROWS[id(params)] = (weakref.ref(row_np), layout, staged)
+
+
+class _DeviceStage:
+    """Device staging of decoded uploads (HTTP mode, `Encrypt(stage_to_device=True)`).
+
+    flearn's server decodes every upload (Server.py:126-131) before it aggregates them
+    (Server.py:140); the decode of upload i+1 is CPU work and the PCIe copy of upload i is DMA
+    work, so they can overlap.  Each decoded row is copied, on a side stream, into slot i of a
+    [cap, stride] device stack (one per device and layout) as soon as it is decoded; when the
+    engine then aggregates exactly those uploads in that order, the stack IS the bucket and no
+    H2D is left to do.  The copy is a snapshot taken at decode time."""
+
+    def __init__(self, device: torch.device, layout: tuple):
+        self.device, self.layout, self.stride = device, layout, layout[-1]
+        self.buf = None
+        self.cap = 0
+        self.n = 0  # rows staged in the current round
+        self.gen = 0
+        self.stream = torch.cuda.Stream(device)
+        self.done = None  # event after the last staged copy
+
+    def stage(self, row: torch.Tensor):
+        with torch.cuda.device(self.device):
+            if self.n == 0:  # new round: slots may still be read by the previous round's reduce
+                self.stream.wait_stream(torch.cuda.current_stream(self.device))
+            if self.n == self.cap:
+                cap = max(8, 2 * self.cap)
+                with torch.cuda.stream(self.stream):
+                    buf = torch.empty((cap, self.stride), dtype=torch.float32, device=self.device)
+                    if self.n:
+                        buf[: self.n].copy_(self.buf[: self.n], non_blocking=True)
+                        self.buf.record_stream(self.stream)
+                self.buf, self.cap = buf, cap
+            with torch.cuda.stream(self.stream):
+                # (torch's pinned-host allocator records this copy's event itself: the pinned row
+                # is not reused before the DMA has read it)
+                self.buf[self.n].copy_(row, non_blocking=True)
+                self.done = torch.cuda.Event()
+                self.done.record(self.stream)
+        slot = self.n
+        self.n += 1
+        return (self, self.gen, slot)
+
+    def take(self, n: int) -> torch.Tensor:
+        """Hand the first n slots to the engine (its stream waits for the copies) and start a new
+        round of slots."""
+        cur = torch.cuda.current_stream(self.device)
+        cur.wait_event(self.done)
+        self.buf.record_stream(cur)  # read there by the reduce: not reused before it finishes
+        view = self.buf[:n]
+        self.gen += 1
+        self.n = 0
+        return view
+
+
+_STAGES: dict = {}
+
+
+def _stage_for(layout: tuple) -> _DeviceStage:
+    dev = torch.device("cuda", torch.cuda.current_device())
+    key = (dev.index, layout)
+    st = _STAGES.get(key)
+    if st is None:
+        st = _STAGES[key] = _DeviceStage(dev, layout)
+    return st
+
+
+def release_device_staging():
+    """Free the device stacks of `stage_to_device` decoding."""
+    _STAGES.clear()
+
+
+def wire_device_stack(params_list, layout: tuple, device):
+    """The staged device stack [N, stride] of these decoded uploads when every one was staged,
+    in list order, into slots 0..N-1 of the same round on `device` and still holds the decoder's
+    arrays — else None (the caller then DMAs the pinned rows or packs)."""
+    ents = [_ROWS.get(id(p)) for p in params_list]
+    stages = {e[2][0] for e in ents if e is not None and e[2] is not None}
+    ok = bool(ents) and len(stages) == 1 and all(e is not None and e[2] is not None for e in ents)
+    if ok:
+        st, gen = ents[0][2][0], ents[0][2][1]
+        ok = st.device == torch.device(device) and st.n == len(ents) and gen == st.gen
+        ok = ok and all(e[2] == (st, gen, i) and wire_row(p, layout) is not None
+                        for i, (e, p) in enumerate(zip(ents, params_list)))
+    if ok:
+        return st.take(len(ents))
+    for st in stages:  # these uploads go the pinned-row way: the next decode starts a new round
+        st.gen += 1
+        st.n = 0
+    return None
 
 
 def wire_row(params: dict, layout: tuple):
@@ -343,9 +434,10 @@ def _pinned_row(stride: int) -> torch.Tensor:
     return torch.empty(stride, dtype=torch.float32)
 
 
-def decode_fast(s: str):
+def decode_fast(s: str, stage_to_device: bool = False):
     """Decode base64(pickle) text through the scanner; raises _WireError(FA_ERR_UNSUPPORTED /
-    FA_ERR_DATA) when the content or the encoding is outside the fast path."""
+    FA_ERR_DATA) when the content or the encoding is outside the fast path.  stage_to_device:
+    also start the upload's H2D into a device staging stack (_DeviceStage)."""
     L = na.load()
     p, n = _ascii_ptr(s)
     cap = 1 << 16
@@ -400,7 +492,10 @@ def decode_fast(s: str):
     if planned is not None:
         params = obj.get("params") if isinstance(obj, dict) else None
         if isinstance(params, dict):
-            _register(params, row_np, planned[1])
+            staged = None
+            if stage_to_device and torch.cuda.is_available() and row.is_pinned():
+                staged = _stage_for(planned[1]).stage(row)
+            _register(params, row_np, planned[1], staged)
     return obj
 
 
@@ -433,8 +528,11 @@ class Encrypt(BaseEncrypt):
     fast_min_chars: strings from this length on are decoded into pinned bucket rows (default
     FAST_MIN_CHARS); shorter ones take native base64 + the restricted unpickler."""
 
-    def __init__(self, fast_min_chars: int | None = None):
+    def __init__(self, fast_min_chars: int | None = None, stage_to_device: bool = False):
         self.fast_min_chars = FAST_MIN_CHARS if fast_min_chars is None else fast_min_chars
+        # opt-in: copy each decoded upload to the GPU right away (overlaps PCIe with the next
+        # decode); the engine then aggregates the device copy — a snapshot taken at decode time
+        self.stage_to_device = stage_to_device
 
     def encode(self, params):
         """Encrypt.py:17-30: base64.b64encode(pickle.dumps(params)).decode()."""
@@ -448,7 +546,7 @@ class Encrypt(BaseEncrypt):
         copy it saves."""
         if isinstance(glob_params, str) and glob_params.isascii() and len(glob_params) >= self.fast_min_chars:
             try:
-                return decode_fast(glob_params)
+                return decode_fast(glob_params, self.stage_to_device)
             except _WireError as e:
                 if e.code not in (na.FA_ERR_UNSUPPORTED, na.FA_ERR_DATA):
                     raise

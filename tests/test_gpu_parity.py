@@ -691,6 +691,29 @@ def test_wire_uploads_through_the_engine(name, strategy, shards, fast, cuda):
     assert_dict_bitwise(back, got, "round trip")
 
 
+@pytest.mark.parametrize("name", ["avg_lenet5_n10", "avg_bnmodel_pyint_n4"])
+def test_wire_device_staging_rounds(name, cuda):
+    """stage_to_device: each decoded upload is copied to the GPU at decode time and the engine
+    aggregates the staged stack — same bits as the reference, over 3 rounds (slot reuse, stack
+    growth past 8 slots); a reordered upload list falls back to the pinned-row path."""
+    from flearn_amd.wire import Encrypt
+
+    g = Golden(name)
+    enc = Encrypt(fast_min_chars=0, stage_to_device=True)
+    strs = [enc.encode({"agg_weight": w, "params": c}) for w, c in zip(g.weights(), g.clients())]
+    s = AVG(encrypt=enc)
+    for r in range(3):
+        ups = [s.receive_processing(x) for x in strs]
+        if r == 2:
+            ups = ups[::-1] + []  # order differs from the decode order: no staged stack
+            want = oracle.server_ensemble(g.weights()[::-1], g.clients()[::-1])
+        else:
+            want = g.output()
+        got = s.server(ups, r)["w_glob"]
+        assert_dict_bitwise(got, want, f"{name} round {r}")
+        assert s.engine.packer.last_wire_staged == (0 if r == 2 else len(strs))
+
+
 def test_wire_rows_are_pinned(cuda):
     from flearn_amd import wire
 

@@ -36,6 +36,7 @@ def main():
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--ref-sample", type=int, default=8, help="uploads the reference codec is timed on")
+    ap.add_argument("--stage", action="store_true", help="Encrypt(stage_to_device=True): H2D during decode")
     a = ap.parse_args()
     name, n = CONFIGS[a.config]
     lay = layouts.get(name)
@@ -54,7 +55,7 @@ def main():
     b64_bytes = sum(len(s) for s in strs)
 
     # ---- flearn_amd: Server.ensemble's loop with the wire codec and the engine -------------
-    s = flearn_amd.AVG(encrypt=wire.Encrypt())
+    s = flearn_amd.AVG(encrypt=wire.Encrypt(stage_to_device=a.stage))
     ph = {"decode": [], "server": [], "encode": [], "total": []}
     out_len = 0
     for _ in range(a.rounds + 1):
@@ -69,6 +70,7 @@ def main():
         for k, v in (("decode", t1 - t0), ("server", t2 - t1), ("encode", t3 - t2), ("total", t3 - t0)):
             ph[k].append(v)
         rows = s.engine.packer.last_wire_rows
+        staged = s.engine.packer.last_wire_staged
         del ups, glob, payload
     med = {k: float(np.median(v[1:])) for k, v in ph.items()}
 
@@ -90,6 +92,7 @@ def main():
         "config": a.config, "layout": name, "clients": n, "params": p,
         "b64_MB_in": round(b64_bytes / 1e6, 1), "b64_MB_out": round(out_len / 1e6, 1),
         "wire_rows_dma": rows,
+        "wire_rows_staged_at_decode": staged,
         "flearn_amd_s": {k2: round(v, 4) for k2, v in med.items()},
         "flearn_amd_decode_GB_s_b64": round(b64_bytes / 1e9 / med["decode"], 2),
         "reference_s_scaled": {k2: round(v, 3) for k2, v in ref.items()},
