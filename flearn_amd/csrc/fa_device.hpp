@@ -593,6 +593,114 @@ __global__ __launch_bounds__(64 * W) void reduce_kernel_rows(const float* __rest
   }
 }
 
+// Row-major variant for blocks that own several pieces (k > 1: C2-C5-sized buckets).  The
+// column-major walk (reduce_kernel_rows: piece after piece, all rows each) starts every round of
+// pieces with the blocks out of step, and rounds after the first measured ~8% slower per row on
+// 100-client buckets (tune/trace_*).  Here a block sweeps the rows ONCE for a group of up to KG
+// pieces: step s = (row i, piece j) with j fastest, KG accumulators per lane, and the same
+// rolling register pipeline D steps deep (D divides KG, so every slot index is static).  The
+// whole grid then moves through the client rows together.  Per element the sum is still rows
+// 0..N-1 in order.
+template <class P, typename T, int OP, int V, int D, int W, int KG, bool NT>
+__global__ __launch_bounds__(64 * W) void reduce_kernel_rowmajor(const float* __restrict__ stack,
+                                                                 int64_t stride, int n,
+                                                                 const typename P::w_t* __restrict__ w,
+                                                                 int64_t col0, int64_t ncols, Epi<T> e) {
+  static_assert(sizeof(typename P::x_t) == 4, "row pipeline is for 4-byte elements");
+  static_assert(KG % D == 0, "pipeline depth must divide the group size");
+  typedef typename P::acc_t A;
+  typedef typename vec4<float>::type XV;
+  typedef typename vec4<A>::type AV;
+  const int64_t nquads = (ncols + 3) / 4;
+  const int64_t qfull = ncols / 4;
+  const int64_t chunks = (nquads + 63) / 64;
+  const int64_t g = gridDim.x;
+  const int64_t k = (chunks + g * W * V - 1) / (g * W * V);  // pieces per block
+  const int64_t pc = (chunks + g * k - 1) / (g * k);         // chunks per piece (<= W*V)
+  const int64_t pieces = (chunks + pc - 1) / pc;
+  const int64_t row_bytes = stride * 4;
+  const int voff = (int)threadIdx.x * 16;
+  const char* base = reinterpret_cast<const char*>(stack + col0);
+  for (int64_t g0 = 0; g0 < k; g0 += KG) {  // groups of KG of this block's pieces
+    int64_t qb[KG];
+    uint32_t bytes[KG];
+    int nq[KG];
+#pragma unroll
+    for (int j = 0; j < KG; ++j) {
+      const int64_t pj = blockIdx.x + (g0 + j) * g;  // interleaved pieces, as reduce_kernel_rows
+      qb[j] = pj * pc * 64;
+      const int64_t qe = qb[j] + pc * 64 < nquads ? qb[j] + pc * 64 : nquads;
+      const int64_t left = (qe < qfull ? qe : qfull) - qb[j];
+      nq[j] = (pj < pieces && g0 + j < k && left > 0) ? (int)left : 0;
+      bytes[j] = (uint32_t)nq[j] * 16u;  // 0: every load of this slot is dropped by the range check
+      if (nq[j] == 0) qb[j] = 0;
+    }
+    XV x[D][V];
+    AV acc[KG][V];
+    // step s = (i, j), i = s / KG, j = s % KG; slot = j % D
+#define FA_RM_LOAD(slot, row, j)                                                                      \
+  {                                                                                                   \
+    const __amdgpu_buffer_rsrc_t r_ = row_rsrc(base + qb[j] * 16 + (int64_t)(row) * row_bytes, bytes[j]); \
+    _Pragma("unroll") for (int v = 0; v < V; ++v) x[slot][v] = buf_load_quad<NT>(r_, voff + v * 64 * W * 16, 0); \
+  }
+#pragma unroll
+    for (int d = 0; d < D; ++d) FA_RM_LOAD(d, 0, d);
+    // row 0: products initialise the sums
+#pragma unroll
+    for (int j = 0; j < KG; ++j) {
+      const typename P::w_t w0 = w[0];
+#pragma unroll
+      for (int v = 0; v < V; ++v) acc[j][v] = quad_mul<P>(w0, x[j % D][v]);
+      __builtin_amdgcn_sched_barrier(0);
+      if (j + D < KG) {
+        FA_RM_LOAD(j % D, 0, j + D);
+      } else if (n > 1) {
+        FA_RM_LOAD(j % D, 1, j + D - KG);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    int i = 1;
+    for (; i + 1 < n; ++i) {  // rows with a successor: every refill is a real step
+      const typename P::w_t wi = w[i];
+#pragma unroll
+      for (int j = 0; j < KG; ++j) {
+#pragma unroll
+        for (int v = 0; v < V; ++v) acc[j][v] = quad_axpy<P>(acc[j][v], wi, x[j % D][v]);
+        __builtin_amdgcn_sched_barrier(0);
+        if (j + D < KG) {
+          FA_RM_LOAD(j % D, i, j + D);
+        } else {
+          FA_RM_LOAD(j % D, i + 1, j + D - KG);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    if (i < n) {  // last row: refills only inside the row
+      const typename P::w_t wi = w[i];
+#pragma unroll
+      for (int j = 0; j < KG; ++j) {
+#pragma unroll
+        for (int v = 0; v < V; ++v) acc[j][v] = quad_axpy<P>(acc[j][v], wi, x[j % D][v]);
+        if (j + D < KG) FA_RM_LOAD(j % D, i, j + D);
+      }
+    }
+#undef FA_RM_LOAD
+#pragma unroll
+    for (int j = 0; j < KG; ++j) {
+#pragma unroll
+      for (int v = 0; v < V; ++v) {
+        const int q = v * 64 * W + (int)threadIdx.x;
+        if (q < nq[j]) finish_quad<T, OP, A>(e, (qb[j] + q) * 4, 4, acc[j][v]);
+      }
+    }
+  }
+  // the window's ragged last quad (ncols % 4 != 0): the block that owns its piece
+  if (threadIdx.x == 0 && qfull * 4 < ncols) {
+    const int64_t pr = qfull / (pc * 64);
+    if (pr % g == blockIdx.x) reduce_ragged<P, T, OP>(stack + col0, stride, n, w, qfull, qfull + 1, ncols, e);
+  }
+}
+
 // Column-blocked client stack: element (n, c) lives at ((c / B) * N + n) * B + c % B with
 // B = kThreads*V*4 columns (one tile).  Tile b's N rows are one contiguous N*B*4-byte region, so
 // a block streams its whole tile linearly (rows B*4 bytes apart) — the access pattern of a plain

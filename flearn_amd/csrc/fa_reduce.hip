@@ -100,6 +100,37 @@ int launch_rows(const float* stack, int64_t stride, int n, const typename P::w_t
   return launch_check();
 }
 
+template <class P, typename T, int OP, int KG>
+int launch_rowmajor(const float* stack, int64_t stride, int n, const typename P::w_t* w, int64_t col0,
+                    int64_t ncols, const Epi<T>& e, int64_t grid, hipStream_t s) {
+  hipLaunchKernelGGL((reduce_kernel_rowmajor<P, T, OP, 8, 1, 8, KG, kNT>), dim3((unsigned)grid), dim3(512), 0, s,
+                     stack, stride, n, w, col0, ncols, e);
+  return launch_check();
+}
+
+// Row-major geometry for windows of several 64-KiB pieces per block (k >= 2): a grid near 192
+// blocks whose k splits into equal groups of KG in {4, 3, 2, 5} pieces (every step of a group is
+// a real piece).  Returns false when no grid in [160, cus] gives such a k.
+bool rowmajor_geometry(int64_t chunks, int cus, int64_t target, int64_t* grid, int* kg) {
+  const int64_t lo = 160 < cus ? 160 : cus, hi = cus;
+  for (int64_t d = 0; d <= hi - lo; ++d) {
+    for (int sgn = 0; sgn < 2; ++sgn) {
+      const int64_t g = sgn ? target - d : target + d;
+      if (g < lo || g > hi || (d == 0 && sgn)) continue;
+      const int64_t k = (chunks + g * kPieceChunks - 1) / (g * kPieceChunks);
+      if (k < 2) return false;  // one piece per block: the column-major kernel
+      for (int c : {4, 3, 2, 5}) {
+        if (k % c == 0 && (c != 5 || k == 5)) {
+          *grid = g;
+          *kg = c;
+          return true;
+        }
+      }
+    }
+  }
+  return false;
+}
+
 template <class P, typename T, int OP>
 int launch_reduce(const typename P::x_t* stack, int64_t stride, int n, const void* w, int64_t col0,
                   int64_t ncols, const Epi<T>& e, hipStream_t s) {
@@ -107,6 +138,19 @@ int launch_reduce(const typename P::x_t* stack, int64_t stride, int n, const voi
   const int cus = device_cus();
   const int64_t chunks = ((ncols + 3) / 4 + 63) / 64;  // 1-KiB row pieces
   if constexpr (sizeof(typename P::x_t) == 4) {
+    if constexpr (sizeof(typename P::acc_t) == 4) {  // fp32 sums (every flearn weight type but f64)
+      int64_t g = 0;
+      int kg = 0;
+      if (chunks > (int64_t)cus * kPieceChunks &&
+          rowmajor_geometry(chunks, cus, (int64_t)(cus * kRowsBlocksPerCU + 0.5), &g, &kg)) {
+        switch (kg) {
+          case 2: return launch_rowmajor<P, T, OP, 2>(stack, stride, n, wt, col0, ncols, e, g, s);
+          case 3: return launch_rowmajor<P, T, OP, 3>(stack, stride, n, wt, col0, ncols, e, g, s);
+          case 4: return launch_rowmajor<P, T, OP, 4>(stack, stride, n, wt, col0, ncols, e, g, s);
+          default: return launch_rowmajor<P, T, OP, 5>(stack, stride, n, wt, col0, ncols, e, g, s);
+        }
+      }
+    }
     int64_t grid = (int64_t)(cus * kRowsBlocksPerCU + 0.5);
     // a window just wider than one round of full pieces: a few more blocks (up to one per CU)
     // instead of a second, nearly empty round

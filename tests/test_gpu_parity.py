@@ -181,7 +181,31 @@ def test_reduce_kernel_big_tiles_ragged(n, ncols, cuda):
 # per wave) and pipeline depth D = 16/V on the 192/224-block grid, with ragged piece and window
 # ends; deep stacks are the per-rank shapes of the multi-GPU runs
 ROW_SHAPES = [(800, 150001), (300, 390001), (200, 700003), (64, 1500007), (40, 3300001), (17, 33), (2, 5000003),
-              (12, 3500001)]  # the last one widens the grid to one full piece per block
+              (12, 3500001),  # widens the grid to one full piece per block
+              (3, 14000003), (2, 9000001)]  # row-major groups of 5 and 3 pieces
+
+
+@pytest.mark.parametrize("mode", [na.MODE_W32_DIV32, na.MODE_W64])
+def test_big_window_modes_bit_exact(mode, cuda):
+    """Multi-piece windows (row-major geometry for fp32 sums, column-major for f64 sums) in the
+    np.float32 / np.float64 weight modes."""
+    n, ncols = 5, 9_000_001
+    stride = -(-ncols // 64) * 64
+    x = _device_stack(n, stride, seed=ncols + mode)
+    if mode == na.MODE_W64:
+        w = np.linspace(0.5, 2.5, n)
+        wd = torch.from_numpy(w).to(cuda)
+        denom = float(np.sum(w))
+    else:
+        w = np.linspace(0.5, 2.5, n).astype(np.float32)
+        wd = torch.from_numpy(w).to(cuda)
+        denom = float(np.sum(w))  # np.float32 pairwise sum, exact as double
+    out64 = torch.empty(ncols, dtype=torch.float64, device=cuda)
+    out32 = torch.empty(ncols, dtype=torch.float32, device=cuda)
+    agg.reduce_stack(x, wd, mode, denom, n_cols=ncols, out32=out32, out64=out64)
+    want = oracle.c_reduce(mode, x[:, :ncols].cpu().numpy(), w, denom)
+    got = out32.cpu().numpy() if want.dtype == np.float32 else out64.cpu().numpy()
+    assert bitwise_equal(got, want)
 
 
 @pytest.mark.parametrize("n,ncols", ROW_SHAPES)

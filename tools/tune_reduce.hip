@@ -134,6 +134,21 @@ Variant make_rows(const float* stack, int64_t stride, int n, const float* w, int
           true, {}};
 }
 
+template <int V, int D, int W, int KG, int OP, typename T>
+Variant make_rowmajor(const float* stack, int64_t stride, int n, const float* w, int64_t ncols, Epi<T> e,
+                      double bytes, int64_t grid) {
+  const int64_t chunks = ((ncols + 3) / 4 + 63) / 64;
+  if (grid > chunks) grid = chunks;
+  char name[96];
+  snprintf(name, sizeof name, "rowmajor V%d D%d W%d KG%d g%lld", V, D, W, KG, (long long)grid);
+  return {name, bytes,
+          [=] {
+            hipLaunchKernelGGL((reduce_kernel_rowmajor<AccF32, T, OP, V, D, W, KG, true>), dim3((unsigned)grid),
+                               dim3(64 * W), 0, 0, stack, stride, n, w, (int64_t)0, ncols, e);
+          },
+          true, {}};
+}
+
 template <int V, int U, int OP, typename T>
 Variant make_blocked(const float* stack, int n, const float* w, int64_t ncols, Epi<T> e, double bytes) {
   const int64_t B = 256 * V * 4;
@@ -288,6 +303,20 @@ int main(int argc, char** argv) {
   vs.push_back(op == FA_OP_AVGM      ? make_rows<V, D, W, FA_OP_AVGM, double, true, XM, NTL>(stack, stride, n, w, ncols, e, bytes, G)   \
                : op == FA_OP_ADAGRAD ? make_rows<V, D, W, FA_OP_ADAGRAD, double, true, XM, NTL>(stack, stride, n, w, ncols, e, bytes, G) \
                                      : make_rows<V, D, W, FA_OP_MEAN, double, true, XM, NTL>(stack, stride, n, w, ncols, e, bytes, G))
+#define RM(V, D, W, KG, G)                                                                                      \
+  vs.push_back(op == FA_OP_AVGM      ? make_rowmajor<V, D, W, KG, FA_OP_AVGM, double>(stack, stride, n, w, ncols, e, bytes, G)   \
+               : op == FA_OP_ADAGRAD ? make_rowmajor<V, D, W, KG, FA_OP_ADAGRAD, double>(stack, stride, n, w, ncols, e, bytes, G) \
+                                     : make_rowmajor<V, D, W, KG, FA_OP_MEAN, double>(stack, stride, n, w, ncols, e, bytes, G))
+  if (!strcmp(set, "rm")) {  // row-major multi-piece sweep vs the column-major product geometry
+    ROWSG(16, 1, 4, 192);
+    ROWSG(8, 1, 8, 192);
+    RM(8, 1, 8, 4, 192);
+    RM(4, 2, 8, 8, 192);
+    RM(4, 2, 8, 4, 192);
+    RM(8, 2, 4, 4, 192);
+    RM(4, 4, 4, 4, 192);
+    RM(8, 1, 8, 4, 224);
+  }
   if (!strcmp(set, "epi")) {  // fused-epilogue geometry: 4 vs 8 waves per block
     ROWSG(16, 1, 4, 224);
     ROWSG(16, 1, 4, 192);
