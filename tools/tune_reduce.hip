@@ -307,6 +307,16 @@ int main(int argc, char** argv) {
   vs.push_back(op == FA_OP_AVGM      ? make_rowmajor<V, D, W, KG, FA_OP_AVGM, double>(stack, stride, n, w, ncols, e, bytes, G)   \
                : op == FA_OP_ADAGRAD ? make_rowmajor<V, D, W, KG, FA_OP_ADAGRAD, double>(stack, stride, n, w, ncols, e, bytes, G) \
                                      : make_rowmajor<V, D, W, KG, FA_OP_MEAN, double>(stack, stride, n, w, ncols, e, bytes, G))
+  if (!strcmp(set, "rmgrid")) {  // row-major: grid / group size around the product's choice
+    RM(8, 1, 8, 5, 176);
+    RM(8, 1, 8, 4, 192);
+    RM(8, 1, 8, 4, 208);
+    RM(8, 1, 8, 4, 224);
+    RM(8, 1, 8, 3, 240);
+    RM(8, 1, 8, 3, 192);
+    RM(8, 1, 8, 2, 208);
+    RM(8, 1, 8, 3, 256);
+  }
   if (!strcmp(set, "rm")) {  // row-major multi-piece sweep vs the column-major product geometry
     ROWSG(16, 1, 4, 192);
     ROWSG(8, 1, 8, 192);
