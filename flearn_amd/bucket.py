@@ -71,11 +71,21 @@ class BucketPlan:
 
 def _as_array_meta(v, where):
     """(dtype, shape, kind) of one uploaded value without copying it."""
+    if isinstance(v, (np.ndarray, np.generic)):
+        return v.dtype, v.shape, "numpy"
     if isinstance(v, torch.Tensor):
         return np.dtype(str(v.dtype).replace("torch.", "")), tuple(v.shape), "torch"
-    if isinstance(v, (np.ndarray, np.generic)):
-        return v.dtype, tuple(np.shape(v)), "numpy"
     raise TypeError(f"{where}: unsupported value type {type(v).__name__} (expected ndarray or Tensor)")
+
+
+def _raw_signature(w, keys):
+    """(type, dtype, shape) of every selected value, as the objects report them (no
+    normalisation): equal signatures mean equal metadata, so only the first client needs the
+    per-key checks (10,200 of them for 100 ResNet-18 uploads)."""
+    try:
+        return tuple((type(v), v.dtype, v.shape) for v in map(w.__getitem__, keys))
+    except (AttributeError, KeyError):
+        return None
 
 
 def select_keys(w_local_lst, key_lst=None):
@@ -104,10 +114,13 @@ def make_plan(agg_weight_lst, w_local_lst, key_lst=None) -> BucketPlan:
     key_group = {}
     key_segment = {}
     input_kinds = set()
+    sig0 = _raw_signature(w_local_lst[0], keys)
+    slow = [n for n in range(1, len(w_local_lst))
+            if sig0 is None or _raw_signature(w_local_lst[n], keys) != sig0]
     for k in keys:
         dt, shape, ik = _as_array_meta(w_local_lst[0][k], f"client 0 key {k!r}")
         input_kinds.add(ik)
-        for n in range(1, len(w_local_lst)):
+        for n in slow:  # clients whose metadata differs somewhere: find and report it
             dtn, shn, ikn = _as_array_meta(w_local_lst[n][k], f"client {n} key {k!r}")
             input_kinds.add(ikn)
             if dtn != dt or shn != shape:

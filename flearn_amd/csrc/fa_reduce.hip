@@ -80,14 +80,14 @@ int launch_check() {
   return FA_OK;
 }
 
-// fp32 client stacks: the row-pipelined kernel (reduce_kernel_rows) on a grid of kRowsBlocksPerCU
-// x CUs blocks, equal interleaved pieces.  The piece width and pipeline depth follow the share s
-// (KiB of every row per block): the narrowest piece that covers s (or 16 KiB per wave), D = 16/V
-// rows deep, so a block keeps ~64 KiB of client rows in flight whatever the window's shape.
-// Fewer blocks than CUs stream best: 192 blocks on 256 CUs, each keeping ~64 KiB
-// of client rows in flight.  Plain mean: 4 waves x up to 16 KiB per row; fused optimizer
-// epilogues: 8 waves x up to 8 KiB (half the per-lane state work at every piece end, twice the
-// waves to overlap it: +2-4% on C3/C5).
+// fp32 client stacks.  Fewer blocks than CUs stream best: ~192 blocks on 256 CUs,
+// each keeping ~64 KiB of client rows in flight, equal interleaved pieces of the window.
+//   * several pieces per block (k >= 2): reduce_kernel_rowmajor, 8 waves x 8 KiB per piece,
+//     rows swept once per group of KG pieces (fp32 sums only: f64 sums need 2x the registers);
+//   * one piece per block: reduce_kernel_rows; the piece width and pipeline depth follow the
+//     share s (KiB of every row per block): the narrowest piece that covers s, D = 64/(V*W) rows
+//     deep.  Plain mean: 4 waves x up to 16 KiB per row; fused optimizer epilogues: 8 waves x up
+//     to 8 KiB (half the per-lane state work at every piece end, twice the waves to overlap it).
 constexpr double kRowsBlocksPerCU = 0.75;
 constexpr int kPieceChunks = 64;  // max KiB of a row per block and piece (= W * Vmax)
 

@@ -190,11 +190,14 @@ class _RowArray(np.ndarray):
 
 
 def _register(params: dict, row_np: _RowArray, layout: tuple, staged=None):
+    # the exact array objects handed out, weakly: wire_row then checks identity (an array that was
+    # replaced is a different object; an array cannot move, so identity pins its address too)
+    refs = tuple(weakref.ref(params[k]) for k, _, _ in layout[:-1])
     with _ROWS_LOCK:
         if len(_ROWS) > 4096:
             for k in [k for k, ent in _ROWS.items() if ent[0]() is None]:
                 del _ROWS[k]
-        _ROWS[id(params)] = (weakref.ref(row_np), layout, staged)
+        _ROWS[id(params)] = (weakref.ref(row_np), layout, staged, refs)
 
 
 class _DeviceStage:
@@ -296,15 +299,11 @@ def wire_row(params: dict, layout: tuple):
     row_np = ent[0]()
     if row_np is None or ent[1] != layout:
         return None
-    row = row_np._fa_tensor
-    base = row.data_ptr()
-    for key, shape, off in layout[:-1]:
+    for (key, _shape, _off), ref in zip(layout[:-1], ent[3]):
         a = params.get(key)
-        if not isinstance(a, np.ndarray) or a.dtype != _F32 or a.shape != shape or not a.flags.c_contiguous:
+        if a is None or a is not ref():
             return None
-        if a.__array_interface__["data"][0] != base + 4 * off:
-            return None
-    return row
+    return row_np._fa_tensor
 
 
 # ---------------------------------------------------------------------------------------------
@@ -492,6 +491,12 @@ def decode_fast(s: str, stage_to_device: bool = False):
     if planned is not None:
         params = obj.get("params") if isinstance(obj, dict) else None
         if isinstance(params, dict):
+            base = row_np.ctypes.data
+            for k, shape, off in planned[1][:-1]:  # the decoder's views, laid out as planned
+                a = params[k]
+                if not (isinstance(a, np.ndarray) and a.dtype == _F32 and a.shape == shape and
+                        (a.size == 0 or a.__array_interface__["data"][0] == base + 4 * off)):
+                    raise _WireError(na.FA_ERR_DATA, f"decoded array {k!r} is not in its planned slot")
             staged = None
             if stage_to_device and torch.cuda.is_available() and row.is_pinned():
                 staged = _stage_for(planned[1]).stage(row)
