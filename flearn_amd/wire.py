@@ -549,14 +549,15 @@ class Encrypt(BaseEncrypt):
         Small strings (< fast_min_chars, e.g. a LeNet upload) take the native base64 + restricted
         unpickler route: the scanner's per-upload Python work (~0.3 ms) would exceed the pack
         copy it saves."""
-        if isinstance(glob_params, str) and glob_params.isascii() and len(glob_params) >= self.fast_min_chars:
-            try:
-                return decode_fast(glob_params, self.stage_to_device)
-            except _WireError as e:
-                if e.code not in (na.FA_ERR_UNSUPPORTED, na.FA_ERR_DATA):
-                    raise
-            except (TypeError, ValueError):  # e.g. a dtype numpy rejects: let the unpickler report it
-                pass
+        if isinstance(glob_params, str) and glob_params.isascii():
+            if len(glob_params) >= self.fast_min_chars:
+                try:
+                    return decode_fast(glob_params, self.stage_to_device)
+                except _WireError as e:
+                    if e.code not in (na.FA_ERR_UNSUPPORTED, na.FA_ERR_DATA):
+                        raise
+                except (TypeError, ValueError):  # e.g. a dtype numpy rejects: let the unpickler report it
+                    pass
             try:
                 raw = b64decode(glob_params)
             except _WireError:
