@@ -13,6 +13,8 @@ HOST_SOURCES = [HERE / "csrc" / "fa_wire.cpp"]  # plain host C++ (g++), linked i
 DEPS = [HERE / "csrc" / "fa_device.hpp"]
 HEADERS = [REPO / "include" / "flearn_amd.h"]
 OUT = HERE / "lib" / "libflearn_amd.so"
+PYHOST_SOURCE = HERE / "csrc" / "fa_pyhost.c"  # Python-object pack helper (ctypes.PyDLL), not C ABI
+PYHOST_OUT = HERE / "lib" / "libfa_pyhost.so"
 ARCH = os.environ.get("FLEARN_AMD_ARCH", "gfx950")
 
 
@@ -23,7 +25,27 @@ def hipcc() -> str:
     raise RuntimeError("hipcc not found")
 
 
+def build_pyhost(force: bool = False, verbose: bool = False) -> Path:
+    """libfa_pyhost.so: gcc against this interpreter's headers; Python symbols stay undefined and
+    resolve against the interpreter that loads it."""
+    import sysconfig
+
+    newest = max(PYHOST_SOURCE.stat().st_mtime, Path(__file__).stat().st_mtime)
+    if PYHOST_OUT.exists() and not force and PYHOST_OUT.stat().st_mtime >= newest:
+        return PYHOST_OUT
+    PYHOST_OUT.parent.mkdir(parents=True, exist_ok=True)
+    tmp = PYHOST_OUT.with_suffix(".so.tmp")
+    cmd = [os.environ.get("CC", "gcc"), "-O2", "-fPIC", "-shared", "-Wall", "-Werror",
+           f"-I{sysconfig.get_paths()['include']}", str(PYHOST_SOURCE), "-o", str(tmp)]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.run(cmd, check=True)
+    tmp.replace(PYHOST_OUT)
+    return PYHOST_OUT
+
+
 def build_native(force: bool = False, verbose: bool = False) -> Path:
+    build_pyhost(force, verbose)
     newest = max(p.stat().st_mtime for p in SOURCES + HOST_SOURCES + DEPS + HEADERS + [Path(__file__)])
     if OUT.exists() and not force and OUT.stat().st_mtime >= newest:
         return OUT

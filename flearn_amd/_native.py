@@ -74,6 +74,27 @@ class Epilogue(ctypes.Structure):
 
 _lock = threading.Lock()
 _lib = None
+_pyhost = None
+PYHOST_PATH = LIB_PATH.parent / "libfa_pyhost.so"
+
+
+def load_pyhost():
+    """The Python-object pack helper (csrc/fa_pyhost.c), loaded with ctypes.PyDLL so it runs with
+    the GIL held (it releases it around its copies).  Raises NativeUnavailable."""
+    global _pyhost
+    with _lock:
+        if _pyhost is None:
+            if not PYHOST_PATH.exists():
+                raise NativeUnavailable(
+                    f"{PYHOST_PATH} not built; run `python -c 'import __graft_entry__ as g; g.build()'`"
+                )
+            L = ctypes.PyDLL(str(PYHOST_PATH))
+            P, I64 = ctypes.c_void_p, ctypes.c_int64
+            fn = L.fa_py_pack_rows
+            fn.argtypes = [ctypes.py_object, ctypes.py_object, I64, P, I64, I64]
+            fn.restype = ctypes.c_int
+            _pyhost = fn
+    return _pyhost
 
 
 def load(require_gpu: bool = False):

@@ -16,6 +16,7 @@ Padding elements are zero and never read back.
 """
 from __future__ import annotations
 
+import collections
 import concurrent.futures
 import math
 from dataclasses import dataclass, field
@@ -24,6 +25,7 @@ from functools import reduce
 import numpy as np
 import torch
 
+from . import _native as na
 from .semantics import KIND_F32, KIND_F64, KIND_I64, Numerics, resolve
 
 ALIGN = 64  # elements: 256 B for fp32, 512 B for 8-byte kinds
@@ -32,6 +34,41 @@ SMALL_BYTES = 4 << 20  # below this, host packing / unpacking runs on the callin
 _STORE = {KIND_F32: np.float32, KIND_F64: np.float64, KIND_I64: np.int64}
 _TORCH = {np.float32: torch.float32, np.float64: torch.float64, np.int64: torch.int64}
 _NP = {torch.float32: np.float32, torch.float64: np.float64, torch.int64: np.int64}
+_FMT = {np.dtype(np.float32): ord("f"), np.dtype(np.float64): ord("d"), np.dtype(np.int64): ord("i")}
+
+
+class _NativeRows:
+    """Packs client rows through fa_py_pack_rows (csrc/fa_pyhost.c): one native call walks the
+    clients' dicts and copies every piece into the pinned staging, the GIL released around the
+    copies.  Built per pack call from the plan's pieces; `__call__(lo, hi)` returns False when a
+    value is not a plain C-contiguous array of its planned dtype (torch tensors, views of other
+    layouts...), and the caller then packs those rows from Python."""
+
+    def __init__(self, pieces, hosts, w_local_lst, rows):
+        self.fn = na.load_pyhost()
+        # plain dicts only (dict / OrderedDict, whose item lookup the C side reproduces)
+        self.clients = [w if type(w) in (dict, collections.OrderedDict) else None for w in w_local_lst]
+        self.keys = tuple(s.key for s, *_ in pieces)
+        hp = [(h.data_ptr(), h.stride(0)) for h in hosts]
+        # per piece: itemsize, numel, src lo, src hi, format, dst base, dst row stride (elements),
+        # dst off -> the byte table fa_py_pack_rows reads (7 rows of pieces, then the skip row)
+        t = np.array([(s.src_dtype.itemsize, s.numel, a, b, _FMT[s.src_dtype]) + hp[sh.index] + (d,)
+                      for s, a, b, sh, d in pieces], dtype=np.int64).reshape(-1, 8).T
+        item = t[0]
+        self.desc = np.concatenate([t[1] * item, t[2] * item, (t[3] - t[2]) * item, t[4], t[5],
+                                    t[6] * item, t[7] * item,
+                                    np.fromiter((r is not None for r in rows), dtype=np.int64, count=len(rows))])
+        self.ptr = self.desc.ctypes.data
+
+    @staticmethod
+    def usable(pieces, hosts) -> bool:
+        """Byte copies only: every source dtype is its bucket's storage dtype."""
+        return bool(pieces) and all(
+            h is not None and s.src_dtype in _FMT and np.dtype(_NP[h.dtype]) == s.src_dtype
+            for s, _, _, sh, _ in pieces for h in (hosts[sh.index],))
+
+    def __call__(self, lo: int, hi: int) -> bool:
+        return self.fn(self.clients, self.keys, len(self.keys), self.ptr, lo, hi) == 0
 
 
 @dataclass
@@ -292,6 +329,7 @@ class Packer:
         into a pinned row of this layout (`rows[n]`) skip the pack and are DMA'd from there."""
         rows = rows if rows is not None else [None] * plan.n_clients
         host_np = [h.numpy() if h is not None else None for h in hosts]
+        native = _NativeRows(pieces, hosts, w_local_lst, rows) if _NativeRows.usable(pieces, hosts) else None
 
         def fill(n):
             if rows[n] is not None:
@@ -306,6 +344,11 @@ class Packer:
                         v = v.detach().cpu().numpy()
                     src = cache[s.key] = np.asarray(v).reshape(-1)
                 host_np[sh.index][n, d : d + (b - a)] = src[a:b]
+
+        def fill_rows(lo, hi):
+            if native is None or not native(lo, hi):
+                for r in range(lo, hi):
+                    fill(r)
 
         def ship(lo, hi):
             for sh, h, dv in zip(shards, hosts, devs):
@@ -326,15 +369,14 @@ class Packer:
         workers = max(1, min(self.workers, n))
         nbytes = sum(int(d.numel()) * d.element_size() for d in devs)
         if workers == 1 or nbytes < SMALL_BYTES or all(r is not None for r in rows):
-            for r in range(n):
-                fill(r)
+            fill_rows(0, n)
             ship(0, n)
             return
         chunk = max(workers, -(-n // 8))  # ~8 chunks, at least one row per worker
         ex = self._executor()
         for lo in range(0, n, chunk):
             hi = min(n, lo + chunk)
-            list(ex.map(fill, range(lo, hi)))
+            list(ex.map(lambda r: fill_rows(r, r + 1), range(lo, hi)))
             ship(lo, hi)
 
     def unpack(self, plan: BucketPlan, results: dict, as_torch: bool, out_dtype_override=None) -> dict:

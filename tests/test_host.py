@@ -214,3 +214,77 @@ def test_shard_plan_covers_columns_once(n_cols, world, stripes, weights):
         tot = sum(p0.widths)
         for wd, wt in zip(p0.widths, weights):
             assert abs(wd / tot - wt / sum(weights)) <= 64 * stripes / tot + 1e-9 or tot <= 64 * stripes
+
+
+def _cpu_stage(plan, kind, shards):
+    from flearn_amd.bucket import Packer, _STORE
+
+    g = plan.groups[kind]
+    hosts = [torch.zeros((plan.n_clients, sh.c1 - sh.c0), dtype=torch.from_numpy(np.zeros(0, _STORE[kind])).dtype)
+             for sh in shards]
+    return g, Packer._pieces(g, shards), hosts
+
+
+def _python_pack(plan, pieces, ups, hosts):
+    out = [np.zeros(h.shape, dtype=h.numpy().dtype) for h in hosts]
+    for n, w in enumerate(ups):
+        for s, a, b, sh, d in pieces:
+            out[sh.index][n, d: d + (b - a)] = np.asarray(w[s.key]).reshape(-1)[a:b]
+    return out
+
+
+@pytest.mark.parametrize("n_shards", [1, 3])
+def test_native_row_pack_matches_python(n_shards):
+    """fa_py_pack_rows (csrc/fa_pyhost.c) writes exactly what the Python pack writes, for whole
+    keys and for keys split at shard boundaries, with wire-staged rows skipped."""
+    from flearn_amd.bucket import Shard, _NativeRows, split_columns
+
+    lay = layouts.get("lenet5")
+    p = layouts.fp32_elems(lay)
+    rng = np.random.default_rng(3)
+    ups = [layouts.synthetic_state_dict(lay, rng.random(p, dtype=np.float32), counter=i) for i in range(5)]
+    plan = make_plan([1.0] * 5, ups)
+    stride = plan.groups[KIND_F32].stride
+    shards = ([Shard(0, torch.device("cpu"), 0, stride)] if n_shards == 1 else
+              [Shard(i, torch.device("cpu"), c0, c1) for i, (c0, c1) in
+               enumerate((sh.c0, sh.c1) for sh in split_columns(stride, ["cpu"] * n_shards))])
+    g, pieces, hosts = _cpu_stage(plan, KIND_F32, shards)
+    assert _NativeRows.usable(pieces, hosts)
+    rows = [None, None, "staged", None, None]
+    nat = _NativeRows(pieces, hosts, ups, rows)
+    assert nat(0, 5)
+    want = _python_pack(plan, pieces, ups, hosts)
+    for h, w in zip(hosts, want):
+        w[2] = 0  # the staged row is not packed
+        np.testing.assert_array_equal(h.numpy(), w)
+
+
+def test_native_row_pack_falls_back_without_copying():
+    """Values the byte copy cannot take (torch tensors, non-contiguous views, a missing key, a
+    non-dict upload) make the call return False with nothing written; int64 sources stored in an
+    f64 bucket are not offered to it at all."""
+    from flearn_amd.bucket import Shard, _NativeRows
+
+    base = {"a": np.arange(6, dtype=np.float32).reshape(2, 3), "b": np.ones(4, np.float32)}
+    plan = make_plan([1.0, 1.0], [base, base])
+    sh = [Shard(0, torch.device("cpu"), 0, plan.groups[KIND_F32].stride)]
+    g, pieces, hosts = _cpu_stage(plan, KIND_F32, sh)
+    bad = [
+        {"a": torch.zeros(2, 3), "b": np.ones(4, np.float32)},
+        {"a": np.arange(6, dtype=np.float32).reshape(3, 2).T, "b": np.ones(4, np.float32)},
+        {"b": np.ones(4, np.float32)},
+        {"a": np.zeros((2, 3), np.float64), "b": np.ones(4, np.float32)},
+    ]
+    for other in bad:
+        hosts[0].zero_()
+        assert not _NativeRows(pieces, hosts, [base, other], [None, None])(0, 2)
+        assert not hosts[0].numpy().any()
+    from collections import UserDict
+    assert not _NativeRows(pieces, hosts, [base, UserDict(base)], [None, None])(0, 2)
+    assert _NativeRows(pieces, hosts, [base, base], [None, None])(0, 2)
+    # int64 buffers under float weights live in the f64 bucket: a cast, not a byte copy
+    ints = {"n": np.array(5, dtype=np.int64)}
+    plan = make_plan([1.0, 2.0], [ints, ints])
+    kind = plan.key_group["n"]
+    _, pieces, hosts = _cpu_stage(plan, kind, [Shard(0, torch.device("cpu"), 0, plan.groups[kind].stride)])
+    assert kind == KIND_F64 and not _NativeRows.usable(pieces, hosts)

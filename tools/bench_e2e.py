@@ -25,6 +25,7 @@ sys.path.insert(0, str(REPO))
 import flearn_amd  # noqa: E402
 from flearn_amd import aggregator as agg  # noqa: E402
 from flearn_amd import layouts  # noqa: E402
+from _refavg import reference_avg  # noqa: E402
 
 CONFIGS = {"c2": ("resnet18", 100), "c3": ("resnet50", 100), "c1": ("lenet5", 10)}
 
@@ -81,6 +82,13 @@ def main():
         t["total"].append(time.perf_counter() - t0)
     assert len(w_glob) == len(layout)
     med = {k: float(np.median(v[1:])) for k, v in t.items() if not k.startswith("_")}
+    # the reference's loopback server step on the same uploads (numpy, 1 core), best of a few
+    ref_s = []
+    ws, ps = [u["agg_weight"] for u in uploads], [u["params"] for u in uploads]
+    for _ in range(3 if n * p > 1 << 24 else 30):
+        t0 = time.perf_counter()
+        reference_avg(ws, ps)
+        ref_s.append(time.perf_counter() - t0)
     in_bytes = n * p * 4
     out_bytes = p * (8 if a.output == "reference" else 4)
     res = {
@@ -89,6 +97,8 @@ def main():
         "e2e_GiB_s_algorithmic": round((in_bytes + out_bytes) / 2**30 / med["total"], 2),
         "h2d_input_GB": round(in_bytes / 1e9, 3),
         "pack_h2d_GB_s": round(in_bytes / 1e9 / med["plan_pack_h2d"], 2),
+        "reference_server_s": round(min(ref_s), 5),
+        "speedup_vs_reference": round(min(ref_s) / med["total"], 2),
         "note": "uploads are host numpy views (flearn loopback); first round (pinned-buffer allocation) excluded",
     }
     print(json.dumps(res))

@@ -27,6 +27,7 @@ sys.path.insert(0, str(REPO))
 import flearn_amd  # noqa: E402
 from flearn_amd import aggregator as agg  # noqa: E402
 from flearn_amd import layouts, wire  # noqa: E402
+from _refavg import reference_avg as _reference_avg  # noqa: E402
 
 CONFIGS = {"c1": ("lenet5", 10), "c2": ("resnet18", 100), "c3": ("resnet50", 100)}
 
@@ -75,13 +76,11 @@ def main():
     med = {k: float(np.median(v[1:])) for k, v in ph.items()}
 
     # ---- reference codec + numpy AVG on a bounded sample -----------------------------------
-    import oracle
-
     k = min(a.ref_sample, n)
     t0 = time.perf_counter()
     dec = [pickle.loads(base64.b64decode(x.encode())) for x in strs[:k]]  # Encrypt.decode
     t1 = time.perf_counter()
-    w = oracle.server_ensemble([d["agg_weight"] for d in dec], [d["params"] for d in dec])
+    w = _reference_avg([d["agg_weight"] for d in dec], [d["params"] for d in dec])
     t2 = time.perf_counter()
     enc = base64.b64encode(pickle.dumps({"w_glob": w})).decode()  # Encrypt.encode
     t3 = time.perf_counter()
