@@ -1,5 +1,7 @@
+"""cProfile of the loopback C1 server step (10 LeNet5 uploads as host numpy dicts): median round
+time, then the hottest host functions.  python tools/prof_host_c1.py (on a GPU box)."""
 import sys, time, cProfile, pstats
-sys.path.insert(0, ".")
+sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__))))
 import numpy as np, torch
 import flearn_amd
 from flearn_amd import layouts
