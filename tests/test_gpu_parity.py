@@ -745,3 +745,47 @@ def test_wire_rows_are_pinned(cuda):
     d = wire.Encrypt(fast_min_chars=0).decode(wire.Encrypt().encode(up))
     row = wire.wire_row(d["params"], (("w", (1000,), 0), 1024))
     assert row is not None and row.is_pinned()
+
+
+@pytest.mark.parametrize("shards", [1, 2])
+def test_host_pack_mixed_upload_kinds(shards, cuda):
+    """Loopback ingest above the small-bucket size (thread-pool pack) with uploads the native row
+    pack takes (dict / OrderedDict of C-contiguous arrays) mixed with rows it hands back to the
+    Python pack (a Fortran-order array, a read-only strided view, a numpy 0-d scalar, a Mapping
+    that is not a dict): bit-exact against the oracle, twice (reused staging)."""
+    import collections
+    from collections.abc import Mapping
+
+    class Upload(Mapping):
+        def __init__(self, d):
+            self.d = d
+
+        def __getitem__(self, k):
+            return self.d[k]
+
+        def __iter__(self):
+            return iter(self.d)
+
+        def __len__(self):
+            return len(self.d)
+
+    rng = np.random.default_rng(11)
+    shapes = {"a.weight": (512, 700), "a.bias": (700,), "b.weight": (300, 333), "s": ()}
+    clients = []
+    for i in range(12):
+        c = {k: rng.standard_normal(sh).astype(np.float32) if sh else np.float32(rng.standard_normal())
+             for k, sh in shapes.items()}
+        clients.append(c)
+    clients[3]["a.weight"] = np.asfortranarray(clients[3]["a.weight"])
+    big = rng.standard_normal((300, 666)).astype(np.float32)
+    clients[5]["b.weight"] = big[:, ::2]
+    clients[5]["b.weight"].flags.writeable = False
+    clients[7] = collections.OrderedDict(clients[7])
+    weights = [float(w) for w in rng.integers(1, 9, size=12)]
+    want = oracle.server_ensemble(weights, clients)
+    s = AVG()
+    s.devices = [cuda] * shards
+    for _ in range(2):
+        ups = upload([Upload(c) if i == 9 else c for i, c in enumerate(clients)], weights)
+        got = s.server(ups, 0)["w_glob"]
+        assert_dict_bitwise(got, want, f"mixed x{shards}")
