@@ -121,6 +121,7 @@ def load(require_gpu: bool = False):
                 "fa_b64_decode": ([P, I64, P, I64, I32], ctypes.c_int),
                 "fa_b64_decode_ranges": ([P, I64, I32, P, P, P, I32], ctypes.c_int),
                 "fa_b64_encode": ([P, I64, P, I64, I32], ctypes.c_int),
+                "fa_b64_encode_gather": ([I32, P, P, P, I64, I32], ctypes.c_int),
                 "fa_pickle_scan_b64": ([P, I64, P, I64, ctypes.POINTER(I64)], ctypes.c_int),
                 "fa_pickle_scan": ([P, I64, P, I64, ctypes.POINTER(I64)], ctypes.c_int),
                 "fa_wire_last_error": ([], ctypes.c_char_p),

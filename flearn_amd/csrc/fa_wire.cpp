@@ -13,6 +13,7 @@
 // dicts / lists / tuples of numpy arrays and scalars use; anything else is reported as
 // FA_ERR_UNSUPPORTED and the caller falls back to a restricted Python unpickler.
 #include <immintrin.h>
+#include <algorithm>
 #include <pthread.h>
 
 #include <atomic>
@@ -963,6 +964,17 @@ int fa_b64_decode_ranges(const char* src, int64_t n, int32_t count, const int64_
   return bad.load() ? wfail(FA_ERR_DATA, "non-alphabet character in base64 input") : FA_OK;
 }
 
+namespace {
+// the last 1-2 bytes of an encode, with '=' padding (what base64.b64encode emits)
+void enc_tail(const uint8_t* s, int64_t rem, char* d) {
+  const uint32_t v = ((uint32_t)s[0] << 16) | (rem == 2 ? (uint32_t)s[1] << 8 : 0);
+  d[0] = kAlpha[(v >> 18) & 63];
+  d[1] = kAlpha[(v >> 12) & 63];
+  d[2] = rem == 2 ? kAlpha[(v >> 6) & 63] : '=';
+  d[3] = '=';
+}
+}  // namespace
+
 int fa_b64_encode(const uint8_t* src, int64_t n, char* dst, int64_t cap, int32_t threads) {
   if (n < 0 || (n && !src)) return wfail(FA_ERR_ARG, "bad input");
   const int64_t ng = n / 3, rem = n % 3, outn = 4 * ((n + 2) / 3);
@@ -973,14 +985,62 @@ int fa_b64_encode(const uint8_t* src, int64_t n, char* dst, int64_t cap, int32_t
     const int64_t g0 = t * per, g1 = g0 + per < ng ? g0 + per : ng;
     enc_groups(src + 3 * g0, g1 - g0, dst + 4 * g0);
   });
+  if (rem) enc_tail(src + 3 * ng, rem, dst + 4 * ng);
+  return FA_OK;
+}
+
+int fa_b64_encode_gather(int32_t count, const uint8_t* const* srcs, const int64_t* lens, char* dst,
+                         int64_t cap, int32_t threads) {
+  if (count < 0 || (count && (!srcs || !lens))) return wfail(FA_ERR_ARG, "bad chunk arrays");
+  std::vector<int64_t> off(count + 1, 0);
+  for (int32_t i = 0; i < count; ++i) {
+    if (lens[i] < 0 || (lens[i] && !srcs[i])) return wfail(FA_ERR_ARG, "bad chunk");
+    off[i + 1] = off[i] + lens[i];
+  }
+  const int64_t n = off[count], ng = n / 3, rem = n % 3, outn = 4 * ((n + 2) / 3);
+  if (cap < outn || (outn && !dst)) return wfail(FA_ERR_ARG, "output buffer too small");
+  // byte position (chunk c, offset o) of decoded byte b: the last chunk starting at or before b
+  auto locate = [&](int64_t b, int32_t& c, int64_t& o) {
+    c = (int32_t)(std::upper_bound(off.begin(), off.end(), b) - off.begin()) - 1;
+    o = b - off[c];
+  };
+  auto take = [&](int32_t& c, int64_t& o, uint8_t* out, int64_t cnt) {  // across chunk ends
+    for (int64_t j = 0; j < cnt; ++j) {
+      while (o == lens[c]) { ++c; o = 0; }
+      out[j] = srcs[c][o++];
+    }
+  };
+  const int64_t per = kPiece / 3;
+  const int64_t tasks = (ng + per - 1) / per;
+  Pool::get().run(tasks, clamp_threads(threads), [&](int64_t t) {
+    int64_t g = t * per;
+    const int64_t g1 = g + per < ng ? g + per : ng;
+    int32_t c;
+    int64_t o;
+    locate(3 * g, c, o);
+    char* d = dst + 4 * g;
+    while (g < g1) {
+      while (o == lens[c]) { ++c; o = 0; }
+      int64_t whole = (lens[c] - o) / 3;
+      if (whole > g1 - g) whole = g1 - g;
+      if (whole > 0) {  // groups inside one chunk
+        enc_groups(srcs[c] + o, whole, d);
+        g += whole, o += 3 * whole, d += 4 * whole;
+        continue;
+      }
+      uint8_t tmp[3];  // a group straddling chunk ends
+      take(c, o, tmp, 3);
+      enc_groups(tmp, 1, d);
+      ++g, d += 4;
+    }
+  });
   if (rem) {
-    const uint8_t* s = src + 3 * ng;
-    char* d = dst + 4 * ng;
-    const uint32_t v = ((uint32_t)s[0] << 16) | (rem == 2 ? (uint32_t)s[1] << 8 : 0);
-    d[0] = kAlpha[(v >> 18) & 63];
-    d[1] = kAlpha[(v >> 12) & 63];
-    d[2] = rem == 2 ? kAlpha[(v >> 6) & 63] : '=';
-    d[3] = '=';
+    uint8_t tmp[2];
+    int32_t c;
+    int64_t o;
+    locate(3 * ng, c, o);
+    take(c, o, tmp, rem);
+    enc_tail(tmp, rem, dst + 4 * ng);
   }
   return FA_OK;
 }

@@ -16,8 +16,9 @@ are copied once more into the aggregation input.
   numpy views of it — a plain dict of plain ndarrays, equal to what ``pickle.loads`` returns.
   When the engine later aggregates those uploads, the Packer recognises the rows and DMAs them
   to the GPU as they are (no pack copy).
-* ``encode`` — ``pickle.dumps`` (the reference's bytes) + a multi-threaded base64 encoder
-  writing directly into the result ``str``.
+* ``encode`` — the reference's pickle bytes, streamed by ``pickle.Pickler`` into a chunk list
+  (large payloads by reference, pickle.dumps's own framing) and base64-encoded from those chunks
+  by a multi-threaded native encoder writing directly into the result ``str``.
 
 Safety: pickle content outside the scanner's subset (e.g. torch tensors) goes through a
 *restricted* unpickler that only resolves numpy / torch / collections reconstructors; any other
@@ -109,6 +110,41 @@ def b64encode(raw) -> str:
     dst, _ = _ascii_ptr(out)
     src = np.frombuffer(mv, dtype=np.uint8)
     _check(L, L.fa_b64_encode(src.ctypes.data, n, dst, m, _threads(n)), "base64 encode")
+    return out
+
+
+class _Chunks:
+    """File object a pickle.Pickler streams into: keeps every chunk by reference (the pickler
+    hands large payloads, e.g. array bytes, straight to write() and flushes its frames as
+    separate bytes objects, with exactly pickle.dumps's framing)."""
+
+    __slots__ = ("parts",)
+
+    def __init__(self):
+        self.parts = []
+
+    def write(self, b):
+        self.parts.append(b if type(b) is bytes else bytes(b))
+        return len(self.parts[-1])
+
+
+def pickle_b64(obj) -> str:
+    """base64.b64encode(pickle.dumps(obj)).decode(), byte for byte, without joining the pickle
+    into one bytes object: the chunks are base64-encoded in place, in order, natively."""
+    sink = _Chunks()
+    pickle.Pickler(sink, protocol=pickle.DEFAULT_PROTOCOL).dump(obj)
+    parts = sink.parts
+    k = len(parts)
+    n = sum(map(len, parts))
+    m = 4 * ((n + 2) // 3)
+    out = _PyUnicode_New(m, 127)
+    if m == 0:
+        return out
+    L = na.load()
+    dst, _ = _ascii_ptr(out)
+    srcs = (ctypes.c_char_p * k)(*parts)  # the bytes objects' own buffers (kept alive by parts)
+    lens = (ctypes.c_int64 * k)(*map(len, parts))
+    _check(L, L.fa_b64_encode_gather(k, srcs, lens, dst, m, _threads(n)), "base64 encode")
     return out
 
 
@@ -540,8 +576,9 @@ class Encrypt(BaseEncrypt):
         self.stage_to_device = stage_to_device
 
     def encode(self, params):
-        """Encrypt.py:17-30: base64.b64encode(pickle.dumps(params)).decode()."""
-        return b64encode(pickle.dumps(params))
+        """Encrypt.py:17-30: base64.b64encode(pickle.dumps(params)).decode() — the same text,
+        encoded from the pickler's chunks (pickle_b64)."""
+        return pickle_b64(params)
 
     def decode(self, glob_params):
         """Encrypt.py:32-44: pickle.loads(base64.b64decode(glob_params.encode())) — through the

@@ -149,6 +149,12 @@ int fa_b64_decode_ranges(const char* src, int64_t n, int32_t count, const int64_
 /* base64.b64encode(src) -> dst (4*ceil(n/3) characters, no terminator).                     */
 int fa_b64_encode(const uint8_t* src, int64_t n, char* dst, int64_t cap, int32_t threads);
 
+/* base64.b64encode(srcs[0] + srcs[1] + ... + srcs[count-1]) -> dst: the encode of a byte
+ * stream held in pieces (the chunks a pickler streamed out, large payloads by reference), so
+ * Encrypt.encode (Encrypt.py:17-30) never joins them into one pickle bytes object.           */
+int fa_b64_encode_gather(int32_t count, const uint8_t* const* srcs, const int64_t* lens, char* dst,
+                         int64_t cap, int32_t threads);
+
 /* Restricted pickle scan (pickle.loads replacement for the structure check): walk the pickle
  * inside base64 text WITHOUT decoding array payloads and write a JSON manifest of the object:
  *   null/true/false/ints/"str"; {"__f":"<C99 hex float>"}; {"__b":[off,len]} bytes;

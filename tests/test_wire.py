@@ -254,3 +254,45 @@ def test_decoded_upload_rows_match_the_bucket_plan():
         assert np.array_equal(row.numpy()[s_.offset : s_.offset + s_.numel], up["params"][s_.key].reshape(-1))
     got["params"]["fc1.weight"] = got["params"]["fc1.weight"].copy()
     assert wire.wire_row(got["params"], sig) is None
+
+
+def test_gather_encode_any_chunking():
+    """fa_b64_encode_gather == base64.b64encode of the concatenation, for random chunkings
+    (empty chunks, 1-2 byte chunks, groups straddling several chunks) and thread counts."""
+    L = na.load()
+    rng = np.random.default_rng(5)
+    for trial in range(60):
+        n = int(rng.choice([0, 1, 2, 3, 4, 5, 100, 4099, 300_001, 2_000_003]))
+        data = rng.bytes(n)
+        cuts = np.sort(rng.integers(0, n + 1, size=int(rng.integers(0, 12))))
+        if trial % 3 == 0 and n > 10:
+            cuts = np.sort(np.concatenate([cuts, [1, 1, 2, 3, n - 1]]))  # tiny and empty chunks
+        bounds = [0, *cuts.tolist(), n]
+        parts = [data[a:b] for a, b in zip(bounds[:-1], bounds[1:])]
+        k = len(parts)
+        m = 4 * ((n + 2) // 3)
+        dst = ctypes.create_string_buffer(max(m, 1))
+        srcs = (ctypes.c_char_p * k)(*parts)
+        lens = (ctypes.c_int64 * k)(*map(len, parts))
+        rc = L.fa_b64_encode_gather(k, srcs, lens, dst, m, int(rng.choice([1, 4, 16])))
+        assert rc == na.FA_OK
+        assert dst.raw[:m] == base64.b64encode(data), (n, bounds)
+    assert L.fa_b64_encode_gather(1, (ctypes.c_char_p * 1)(b"abcd"), (ctypes.c_int64 * 1)(4),
+                                  ctypes.create_string_buffer(8), 7, 1) == na.FA_ERR_ARG  # cap too small
+
+
+@pytest.mark.parametrize("i", range(len(sample_objects())))
+def test_encode_is_reference_text(i):
+    """Encrypt.encode (pickler chunks -> gather encode) == base64.b64encode(pickle.dumps(obj))."""
+    obj = sample_objects()[i]
+    assert wire.Encrypt().encode(obj) == base64.b64encode(pickle.dumps(obj)).decode()
+
+
+def test_encode_frame_boundaries():
+    """Payloads around pickle's 64 KiB frame target (below it they are framed, from it on the
+    pickler passes them by reference) encode to the reference text."""
+    rng = np.random.default_rng(9)
+    for n in [0, 1, 65535 - 40, 65535, 65536, 65537, 200_000]:
+        for obj in ({"b": rng.bytes(n)}, {"params": {"w": rng.standard_normal(n // 8 + 1), "c": np.int64(n)}},
+                    [rng.bytes(n), rng.bytes(3), rng.bytes(n // 2)]):
+            assert wire.pickle_b64(obj) == base64.b64encode(pickle.dumps(obj)).decode(), n
