@@ -40,6 +40,7 @@ EXPORTS = (
     "fa_b64_decode",
     "fa_b64_decode_ranges",
     "fa_b64_encode",
+    "fa_b64_encode_gather",
     "fa_pickle_scan_b64",
     "fa_pickle_scan",
     "fa_wire_last_error",
