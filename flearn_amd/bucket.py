@@ -19,6 +19,7 @@ from __future__ import annotations
 import collections
 import concurrent.futures
 import math
+import threading
 from dataclasses import dataclass, field
 from functools import reduce
 
@@ -140,20 +141,50 @@ def select_keys(w_local_lst, key_lst=None):
     return [k for k in w_local_lst[0].keys() if k in common]
 
 
+_PLANS: collections.OrderedDict = collections.OrderedDict()  # recent plans (read-only once built)
+_PLANS_MAX = 8
+_PLANS_LOCK = threading.Lock()
+
+
 def make_plan(agg_weight_lst, w_local_lst, key_lst=None) -> BucketPlan:
+    """The bucket plan of one aggregation.  A federated run aggregates the same model with the
+    same weights round after round, so a plan is reused when the selected keys, every client's
+    (type, dtype, shape) per key, the client count and the weights (types and exact values, by
+    repr: -0.0 and NaN included) all equal a recent call's."""
     if len(w_local_lst) == 0 or len(agg_weight_lst) == 0:
         raise IndexError("list index out of range")  # reference: agg_weight_lst[0] (strategy.py:123)
     if len(agg_weight_lst) != len(w_local_lst):
         raise ValueError("agg_weight_lst and w_local_lst differ in length")
     keys = select_keys(w_local_lst, key_lst)
+    sig0 = _raw_signature(w_local_lst[0], keys)
+    slow = [n for n in range(1, len(w_local_lst))
+            if sig0 is None or _raw_signature(w_local_lst[n], keys) != sig0]
+    ck = None
+    if sig0 is not None and not slow:
+        ck = (tuple(keys), sig0, len(w_local_lst), tuple(map(type, agg_weight_lst)), repr(list(agg_weight_lst)))
+        try:
+            with _PLANS_LOCK:
+                plan = _PLANS.get(ck)
+                if plan is not None:
+                    _PLANS.move_to_end(ck)
+                    return plan
+        except TypeError:  # something unhashable in the metadata: plan afresh, uncached
+            ck = None
+    plan = _build_plan(agg_weight_lst, w_local_lst, keys, slow)
+    if ck is not None:
+        with _PLANS_LOCK:
+            _PLANS[ck] = plan
+            while len(_PLANS) > _PLANS_MAX:
+                _PLANS.popitem(last=False)
+    return plan
+
+
+def _build_plan(agg_weight_lst, w_local_lst, keys, slow) -> BucketPlan:
     numerics_by_dtype = {}
     groups: dict = {}
     key_group = {}
     key_segment = {}
     input_kinds = set()
-    sig0 = _raw_signature(w_local_lst[0], keys)
-    slow = [n for n in range(1, len(w_local_lst))
-            if sig0 is None or _raw_signature(w_local_lst[n], keys) != sig0]
     for k in keys:
         dt, shape, ik = _as_array_meta(w_local_lst[0][k], f"client 0 key {k!r}")
         input_kinds.add(ik)

@@ -291,3 +291,25 @@ def test_native_row_pack_falls_back_without_copying():
     kind = plan.key_group["n"]
     _, pieces, hosts = _cpu_stage(plan, kind, [Shard(0, torch.device("cpu"), 0, plan.groups[kind].stride)])
     assert kind == KIND_F64 and not _NativeRows.usable(pieces, hosts)
+
+
+def test_plan_cache_reuses_only_identical_metadata_and_weights():
+    """Repeated rounds of one model reuse the plan; any change of weights (incl. 0.0 vs -0.0,
+    float vs int), shapes, dtypes, key selection or client count plans afresh; a mismatching
+    client still raises after the plan was cached."""
+    a = {"w": np.ones((2, 3), np.float32), "b": np.ones(3, np.float32)}
+    p1 = make_plan([1.0, 2.0], [a, dict(a)])
+    assert make_plan([1.0, 2.0], [dict(a), a]) is p1
+    for ws in ([1.0, 2.5], [1, 2], [np.float32(1.0), np.float32(2.0)], [-0.0, 2.0]):
+        assert make_plan(ws, [a, a]) is not p1
+    z1, z2 = make_plan([0.0, 1.0], [a, a]), make_plan([-0.0, 1.0], [a, a])
+    assert z1 is not z2 and np.signbit(z2.f32.numerics.weights[0]) and not np.signbit(z1.f32.numerics.weights[0])
+    assert make_plan([1.0, 2.0], [a, a], key_lst=["w"]) is not p1
+    assert make_plan([1.0, 2.0, 1.0], [a, a, a]) is not p1
+    b = dict(a, w=np.ones((3, 2), np.float32))
+    assert make_plan([1.0, 2.0], [b, b]) is not p1
+    with pytest.raises(ValueError):
+        make_plan([1.0, 2.0], [a, b])
+    c = dict(a, w=torch.ones(2, 3))
+    with pytest.raises(TypeError):
+        make_plan([1.0, 2.0], [a, c])
