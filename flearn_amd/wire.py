@@ -360,6 +360,8 @@ class _Decoder:
         self.ranges = []  # (off, len, dst address)
         self.aux_size = 0
         self.row_plan = {}  # id(node) -> row offset (elements)
+        self.row_nodes = []  # the planned manifest nodes, in layout order
+        self.row_built = {}  # id(node) -> the ndarray view build() made for it
 
     # pass 1: find the upload's params dict and lay out its fp32 C-order arrays
     def plan_row(self, tree):
@@ -380,6 +382,7 @@ class _Decoder:
                 continue
             numel = _numel(shape)
             self.row_plan[id(v)] = stride
+            self.row_nodes.append(v)
             layout.append((k, tuple(shape), stride))
             stride += -(-max(numel, 1) // ALIGN) * ALIGN
         if not layout:
@@ -419,7 +422,8 @@ class _Decoder:
             dtype = np.dtype(dt)
             if "_aux" not in node:
                 o = self.row_plan[id(node)]
-                return row_np[o : o + _numel(shape)].view(np.ndarray).reshape(shape)
+                arr = self.row_built[id(node)] = row_np[o : o + _numel(shape)].view(np.ndarray).reshape(shape)
+                return arr
             count = nbytes // dtype.itemsize if dtype.itemsize else 0
             flat = np.frombuffer(aux_np, dtype=dtype, count=count, offset=node["_aux"]) if count else np.empty(0, dtype)
             arr = flat.reshape(shape, order="F" if fortran else "C")
@@ -463,6 +467,25 @@ def _payload_nodes(node, out):
                     _payload_nodes(node[key], out)
 
 
+_GAPS: dict = {}  # row layout -> int64 indices of its alignment gaps
+
+
+def _gap_index(layout: tuple) -> np.ndarray:
+    idx = _GAPS.get(layout)
+    if idx is None:
+        parts, end = [], 0
+        for _k, shape, off in layout[:-1]:
+            if off > end:
+                parts.append(np.arange(end, off, dtype=np.int64))
+            end = off + _numel(shape)
+        parts.append(np.arange(end, layout[-1], dtype=np.int64))
+        idx = np.concatenate(parts)
+        if len(_GAPS) >= 64:
+            _GAPS.clear()
+        _GAPS[layout] = idx
+    return idx
+
+
 def _pinned_row(stride: int) -> torch.Tensor:
     if torch.cuda.is_available():
         return torch.empty(stride, dtype=torch.float32, pin_memory=True)
@@ -497,23 +520,20 @@ def decode_fast(s: str, stage_to_device: bool = False):
         row_np = row.numpy().view(_RowArray)
         row_np._fa_tensor = row
         # zero the alignment gaps (reduced but never returned: keep them finite and deterministic)
-        end = 0
-        for _k, shape, off in planned[1][:-1]:
-            if off > end:
-                row_np[end:off] = 0
-            end = off + _numel(shape)
-        row_np[end:stride] = 0
+        row_np[_gap_index(planned[1])] = 0
+    row_base = row_np.ctypes.data if row_np is not None else 0
+    aux_base = aux_np.ctypes.data
     offs, lens, dsts = [], [], []
     for node in _payload_nodes_list(tree):
         if "__nd" in node:
             o, ln = node["__nd"][3], node["__nd"][4]
-            dst = row_np.ctypes.data + 4 * dec.row_plan[id(node)] if "_aux" not in node else aux_np.ctypes.data + node["_aux"]
+            dst = row_base + 4 * dec.row_plan[id(node)] if "_aux" not in node else aux_base + node["_aux"]
         elif "__sc" in node:
             o, ln = node["__sc"][1], node["__sc"][2]
-            dst = aux_np.ctypes.data + node["_aux"]
+            dst = aux_base + node["_aux"]
         else:
             o, ln = node["__b"]
-            dst = aux_np.ctypes.data + node["_aux"]
+            dst = aux_base + node["_aux"]
         if ln:
             offs.append(o)
             lens.append(ln)
@@ -527,11 +547,10 @@ def decode_fast(s: str, stage_to_device: bool = False):
     if planned is not None:
         params = obj.get("params") if isinstance(obj, dict) else None
         if isinstance(params, dict):
-            base = row_np.ctypes.data
-            for k, shape, off in planned[1][:-1]:  # the decoder's views, laid out as planned
-                a = params[k]
-                if not (isinstance(a, np.ndarray) and a.dtype == _F32 and a.shape == shape and
-                        (a.size == 0 or a.__array_interface__["data"][0] == base + 4 * off)):
+            # the decoder's own views, laid out as planned (a key repeated in the pickled dict
+            # would leave an earlier planned slot unreferenced: refuse rather than register it)
+            for (k, _shape, _off), node in zip(planned[1][:-1], dec.row_nodes):
+                if params.get(k) is not dec.row_built.get(id(node)):
                     raise _WireError(na.FA_ERR_DATA, f"decoded array {k!r} is not in its planned slot")
             staged = None
             if stage_to_device and torch.cuda.is_available() and row.is_pinned():

@@ -296,3 +296,20 @@ def test_encode_frame_boundaries():
         for obj in ({"b": rng.bytes(n)}, {"params": {"w": rng.standard_normal(n // 8 + 1), "c": np.int64(n)}},
                     [rng.bytes(n), rng.bytes(3), rng.bytes(n // 2)]):
             assert wire.pickle_b64(obj) == base64.b64encode(pickle.dumps(obj)).decode(), n
+
+
+def test_repeated_key_in_pickled_params_decodes_like_pickle():
+    """A hand-edited pickle whose params dict names a key twice (pickle.loads keeps the last
+    value): the pinned-row path must not register a row with an unreferenced slot; the result
+    equals pickle.loads either way."""
+    rng = np.random.default_rng(2)
+    obj = {"agg_weight": 1.0, "params": {"wq": rng.random(300, dtype=np.float32),
+                                         "wz": rng.random(500, dtype=np.float32)}}
+    raw = pickle.dumps(obj)
+    assert raw.count(b"\x8c\x02wz") == 1
+    raw = raw.replace(b"\x8c\x02wz", b"\x8c\x02wq")
+    want = pickle.loads(raw)
+    assert list(want["params"]) == ["wq"] and want["params"]["wq"].shape == (500,)
+    got = wire.Encrypt(fast_min_chars=0).decode(base64.b64encode(raw).decode())
+    same(got, want)
+    assert id(got["params"]) not in wire._ROWS  # not handed to the engine as a pinned row
