@@ -45,20 +45,27 @@ class _NativeRows:
     value is not a plain C-contiguous array of its planned dtype (torch tensors, views of other
     layouts...), and the caller then packs those rows from Python."""
 
-    def __init__(self, pieces, hosts, w_local_lst, rows):
+    def __init__(self, pieces, hosts, w_local_lst, rows, memo=None):
         self.fn = na.load_pyhost()
         # plain dicts only (dict / OrderedDict, whose item lookup the C side reproduces)
         self.clients = [w if type(w) in (dict, collections.OrderedDict) else None for w in w_local_lst]
-        self.keys = tuple(s.key for s, *_ in pieces)
-        hp = [(h.data_ptr(), h.stride(0)) for h in hosts]
-        # per piece: itemsize, numel, src lo, src hi, format, dst base, dst row stride (elements),
-        # dst off -> the byte table fa_py_pack_rows reads (7 rows of pieces, then the skip row)
-        t = np.array([(s.src_dtype.itemsize, s.numel, a, b, _FMT[s.src_dtype]) + hp[sh.index] + (d,)
-                      for s, a, b, sh, d in pieces], dtype=np.int64).reshape(-1, 8).T
-        item = t[0]
-        self.desc = np.concatenate([t[1] * item, t[2] * item, (t[3] - t[2]) * item, t[4], t[5],
-                                    t[6] * item, t[7] * item,
-                                    np.fromiter((r is not None for r in rows), dtype=np.int64, count=len(rows))])
+        hp = tuple((h.data_ptr(), h.stride(0)) for h in hosts)
+        key = ("native_rows", hp)
+        cached = memo.get(key) if memo is not None else None
+        if cached is None:
+            # per piece: itemsize, numel, src lo, src hi, format, dst base, dst row stride
+            # (elements), dst off -> the byte table fa_py_pack_rows reads (7 rows of pieces)
+            t = np.array([(s.src_dtype.itemsize, s.numel, a, b, _FMT[s.src_dtype]) + hp[sh.index] + (d,)
+                          for s, a, b, sh, d in pieces], dtype=np.int64).reshape(-1, 8).T
+            item = t[0]
+            table = np.concatenate([t[1] * item, t[2] * item, (t[3] - t[2]) * item, t[4], t[5],
+                                    t[6] * item, t[7] * item])
+            cached = (tuple(s.key for s, *_ in pieces), table)
+            if memo is not None:
+                memo[key] = cached
+        self.keys, table = cached
+        # ... then one skip flag per client row
+        self.desc = np.concatenate([table, np.fromiter((r is not None for r in rows), dtype=np.int64, count=len(rows))])
         self.ptr = self.desc.ctypes.data
 
     @staticmethod
@@ -101,6 +108,9 @@ class BucketPlan:
     key_segment: dict  # key -> Segment
     n_clients: int
     input_kind: str  # "numpy" | "torch"
+    # derived per-plan data of the packer (pieces, native pack tables); plans are reused across
+    # rounds (make_plan's cache), so this is computed once per model layout and staging buffer
+    memo: dict = field(default_factory=dict, compare=False, repr=False)
 
     @property
     def f32(self):
@@ -313,7 +323,10 @@ class Packer:
             shards = self.shards(plan, kind)
             devs = [self.device_bucket(("in", kind, sh.index), (plan.n_clients, sh.width), tdt, sh.device)
                     for sh in shards]
-            pieces = self._pieces(g, shards)
+            pk = ("pieces", kind, tuple((sh.index, sh.c0, sh.c1) for sh in shards))
+            pieces = plan.memo.get(pk)
+            if pieces is None:
+                pieces = plan.memo[pk] = self._pieces(g, shards)
             if plan.input_kind == "torch" and all(w_local_lst[0][s.key].device.type == "cuda" for s in g.segments):
                 for n, w in enumerate(w_local_lst):
                     for s, a, b, sh, d in pieces:
@@ -360,7 +373,8 @@ class Packer:
         into a pinned row of this layout (`rows[n]`) skip the pack and are DMA'd from there."""
         rows = rows if rows is not None else [None] * plan.n_clients
         host_np = [h.numpy() if h is not None else None for h in hosts]
-        native = _NativeRows(pieces, hosts, w_local_lst, rows) if _NativeRows.usable(pieces, hosts) else None
+        native = (_NativeRows(pieces, hosts, w_local_lst, rows, plan.memo)
+                  if _NativeRows.usable(pieces, hosts) else None)
 
         def fill(n):
             if rows[n] is not None:
