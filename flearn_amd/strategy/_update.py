@@ -7,12 +7,70 @@ runs one fa_opt_apply launch, with the reference's operation order and precision
 """
 from __future__ import annotations
 
+import concurrent.futures
+
 import numpy as np
 import torch
 
 from .. import _native as na
 from ..bucket import ALIGN
 from .utils import _ERR
+
+_FMT = {np.dtype(np.float32): ord("f"), np.dtype(np.float64): ord("d")}
+_PART_BYTES = 16 << 20  # host copies are split into parts of about this size, one per pool task
+_POOL = None
+
+
+def _pool() -> concurrent.futures.ThreadPoolExecutor:
+    global _POOL
+    if _POOL is None:
+        _POOL = concurrent.futures.ThreadPoolExecutor(8, thread_name_prefix="fa-update")
+    return _POOL
+
+
+def _run(tasks):
+    """Run zero-argument callables (copies that release the GIL) on the pool; their results."""
+    if len(tasks) == 1:
+        return [tasks[0]()]
+    return [f.result() for f in [_pool().submit(t) for t in tasks]]
+
+
+class _DictPack:
+    """Copies one dict's arrays into a flat staging buffer at the layout's offsets with
+    fa_py_pack_rows (csrc/fa_pyhost.c), in byte-balanced parts run on the pool; False when a
+    value is not a C-contiguous array of the expected dtype (the caller then copies in Python)."""
+
+    def __init__(self, lay, dtype, dst_ptr):
+        self.fn = na.load_pyhost()
+        item, fmt = np.dtype(dtype).itemsize, _FMT[np.dtype(dtype)]
+        parts, cur, size = [], [], 0
+        for k, _s, o, n in lay:
+            cur.append((k, n, o))
+            size += n * item
+            if size >= _PART_BYTES:
+                parts.append(cur)
+                cur, size = [], 0
+        if cur:
+            parts.append(cur)
+        self.parts = []
+        for part in parts:  # desc table: total, src_lo, nbytes, fmt, dst_base, dst_row, dst_off; skip
+            m = len(part)
+            desc = np.zeros(7 * m + 1, dtype=np.int64)
+            nb = np.array([n for _, n, _ in part], dtype=np.int64) * item
+            desc[0:m] = nb
+            desc[2 * m:3 * m] = nb
+            desc[3 * m:4 * m] = fmt
+            desc[4 * m:5 * m] = dst_ptr
+            desc[6 * m:7 * m] = np.array([o for _, _, o in part], dtype=np.int64) * item
+            self.parts.append((tuple(k for k, _, _ in part), desc))
+
+    def __call__(self, d: dict) -> bool:
+        if type(d) is not dict:
+            d = dict(d)
+        clients = [d]
+        return all(rc == 0 for rc in _run([
+            (lambda keys=keys, desc=desc: self.fn(clients, keys, len(keys), desc.ctypes.data, 0, 1))
+            for keys, desc in self.parts]))
 
 
 class DeviceUpdater:
@@ -22,6 +80,7 @@ class DeviceUpdater:
         self.params = dict(beta=beta, eta=eta, tau=tau, beta2=beta2)
         self.layout = None  # [(key, shape, offset, numel)]
         self.v = None
+        self._stage = None  # pinned staging of the current layout (local, global, result)
 
     def _layout(self, w_glob):
         lay, off = [], 0
@@ -33,7 +92,7 @@ class DeviceUpdater:
         return lay, off
 
     def reset(self):
-        self.layout, self.v = None, None
+        self.layout, self.v, self._stage = None, None, None
 
     def state(self):
         """v_t as the reference exposes it: {key: ndarray}."""
@@ -69,13 +128,18 @@ class DeviceUpdater:
         if self.layout != lay or self.v is None or self.v.dtype != tdt:
             self.layout = lay
             self.v = torch.zeros(total, dtype=tdt, device=dev)  # np.zeros_like(delta) on first use
-        lh = torch.zeros(total, dtype=torch.float32, pin_memory=True)
-        gh = torch.zeros(total, dtype=tdt, pin_memory=True)
-        for k, s, o, n in lay:
-            lh.numpy()[o : o + n] = local[k].reshape(-1)
-            gh.numpy()[o : o + n] = glob[k].reshape(-1)
+            self._stage = None
+        st = self._staging(lay, total, tdt, dev)
+        lh, gh, oh, pack_l, pack_g = st
         with torch.cuda.device(dev):
+            # local -> pinned -> device, then the global model while the local one is in flight
+            if not pack_l(local):
+                for k, s, o, n in lay:
+                    lh.numpy()[o : o + n] = local[k].reshape(-1)
             ld = lh.to(dev, non_blocking=True)
+            if not pack_g(glob):
+                for k, s, o, n in lay:
+                    gh.numpy()[o : o + n] = glob[k].reshape(-1)
             gd = gh.to(dev, non_blocking=True)
             out = torch.empty(total, dtype=tdt, device=dev)
             from ..aggregator import apply_update
@@ -83,7 +147,24 @@ class DeviceUpdater:
             params = dict(self.params, **override)
             kw = {"out64": out} if tdt == torch.float64 else {"out32": out}
             apply_update(self.op, ld, gd, self.v, **kw, **params)
-            host = out.cpu().numpy()
-        for k, s, o, n in lay:  # in place, like the reference (avgm.py:34-35, opt.py:62-63)
-            w_local[k] = host[o : o + n].reshape(s).copy()
+            oh.copy_(out, non_blocking=True)
+            torch.cuda.current_stream(dev).synchronize()  # staging is reused by the next call
+        # one fresh array for the new w_local, filled from the pinned result by the pool
+        src = oh.numpy()
+        fresh = np.empty(total, dtype=src.dtype)
+        step = 1 << 22
+        _run([(lambda a=a: np.copyto(fresh[a : a + step], src[a : a + step])) for a in range(0, total, step)])
+        for k, s, o, n in lay:  # replaced per key, like the reference (avgm.py:34-35, opt.py:62-63)
+            w_local[k] = fresh[o : o + n].reshape(s)
         return w_local
+
+    def _staging(self, lay, total, tdt, dev):
+        """Pinned staging for this layout, reused across calls (zeroed once: only the segments
+        are ever written, so the alignment gaps stay zero)."""
+        if getattr(self, "_stage", None) is None:
+            lh = torch.zeros(total, dtype=torch.float32, pin_memory=True)
+            gh = torch.zeros(total, dtype=tdt, pin_memory=True)
+            oh = torch.empty(total, dtype=tdt, pin_memory=True)
+            gdt = np.float64 if tdt == torch.float64 else np.float32
+            self._stage = (lh, gh, oh, _DictPack(lay, np.float32, lh.data_ptr()), _DictPack(lay, gdt, gh.data_ptr()))
+        return self._stage

@@ -789,3 +789,31 @@ def test_host_pack_mixed_upload_kinds(shards, cuda):
         ups = upload([Upload(c) if i == 9 else c for i, c in enumerate(clients)], weights)
         got = s.server(ups, 0)["w_glob"]
         assert_dict_bitwise(got, want, f"mixed x{shards}")
+
+
+@pytest.mark.parametrize("op", ["avgm", "adagrad", "yogi"])
+def test_client_side_update_large_and_fallback_values(op, cuda):
+    """The client update on a model above the copy-part size (parallel native packs) and with
+    values the byte copy hands back to Python (a Fortran-order local array, a strided global
+    view, a 0-d entry): bit-exact against the oracle over 3 rounds, state included."""
+    rng = np.random.default_rng(21)
+    shapes = {"a": (1024, 3000), "b": (3000,), "c": (700, 900), "d": (), "e": (5, 7)}
+    prev = {k: rng.standard_normal(sh).astype(np.float32) for k, sh in shapes.items()}
+    prev["c"] = np.asfortranarray(prev["c"])
+    s = AVGM() if op == "avgm" else OPT()
+    v = None
+    for r in range(3):
+        glob = {k: rng.standard_normal(sh) for k, sh in shapes.items()}
+        wide = rng.standard_normal((5, 14))
+        glob["e"] = wide[:, ::2]
+        if op == "avgm":
+            want, v = oracle.mean_momentum(prev, glob, v, 0.9)
+            got = s.mean_momentum(dict(prev), glob, 0.9)
+        else:
+            want, v = oracle.adaptive_opt(prev, glob, v, op)
+            got = s.adaptive_opt(dict(prev), glob, op)
+        assert_dict_bitwise(got, want, f"{op} w{r}")
+        assert_dict_bitwise(s.v_t, v, f"{op} v{r}")
+        prev = {k: np.asarray(got[k]).astype(np.float32) for k in shapes}
+        if r == 0:
+            prev["c"] = np.asfortranarray(prev["c"])

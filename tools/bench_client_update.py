@@ -1,0 +1,69 @@
+"""Client-side FedAVGM / FedOPT update (flearn's client_receive math) on the GPU vs the
+reference's numpy, per call, for one model: host fp32 w_local + host float64 w_glob in, new
+w_local out — AVGM.mean_momentum (avgm.py:19-36) / OPT.adaptive_opt (opt.py:23-65).
+
+    python tools/bench_client_update.py [--layout resnet50] [--rounds 4]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+REPO = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(REPO))
+
+import flearn_amd  # noqa: E402
+from flearn_amd import layouts  # noqa: E402
+from _refavg import ReferenceClientUpdate  # noqa: E402
+
+
+def model(lay, seed, dtype):
+    p = layouts.fp32_elems(lay)
+    flat = np.random.default_rng(seed).standard_normal(p).astype(dtype)
+    sd = layouts.synthetic_state_dict(lay, flat.astype(np.float32), counter=1)
+    return {k: v.astype(dtype) for k, v in sd.items() if isinstance(v, np.ndarray) and v.dtype == np.float32}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--layout", default="resnet50")
+    ap.add_argument("--rounds", type=int, default=4)
+    ap.add_argument("--ref-rounds", type=int, default=2)
+    a = ap.parse_args()
+    lay = layouts.get(a.layout)
+    w_local0 = model(lay, 1, np.float32)
+    globs = [model(lay, 10 + r, np.float64) for r in range(a.rounds)]
+    p = sum(v.size for v in w_local0.values())
+    res = {"layout": a.layout, "params": p}
+    for method in ("avgm", "adagrad"):
+        s = flearn_amd.AVGM() if method == "avgm" else flearn_amd.OPT()
+        fn = ((lambda wl, wg: s.mean_momentum(wl, wg, 0.9)) if method == "avgm"
+              else (lambda wl, wg: s.adaptive_opt(wl, wg, "adagrad")))
+        ts = []
+        for r in range(a.rounds):
+            wl = dict(w_local0)
+            t0 = time.perf_counter()
+            fn(wl, globs[r])
+            ts.append(time.perf_counter() - t0)
+        ref = ReferenceClientUpdate(method)
+        rs = []
+        for r in range(a.ref_rounds):
+            wl = dict(w_local0)
+            t0 = time.perf_counter()
+            ref(wl, globs[r])
+            rs.append(time.perf_counter() - t0)
+        med = float(np.median(ts[1:]))
+        res[method] = {"flearn_amd_s": round(med, 4), "first_call_s": round(ts[0], 4),
+                       "reference_s": round(float(np.median(rs[1:] if len(rs) > 1 else rs)), 4),
+                       "speedup": round(float(np.median(rs[1:] if len(rs) > 1 else rs)) / med, 1)}
+    res["note"] = "host arrays in and out (PCIe-inclusive); reference = its numpy ops on 1 core; median after round 0"
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
