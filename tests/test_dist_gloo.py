@@ -73,3 +73,10 @@ def test_sharded_reduce_four_ranks():
     """More ranks than the GPU box's CI can rehearse on one card: world 4, uneven stripes."""
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     mp.spawn(_worker, args=(4, _free_port(), 5, 70_001, 2, "mean", (3, 1)), nprocs=4, join=True)
+
+
+def test_sharded_reduce_eight_ranks():
+    """The driver's scaling run at G=8 with bench's default stripes (3:1), fused Adagrad, and a
+    width whose last rank's slices are partly padding."""
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    mp.spawn(_worker, args=(8, _free_port(), 3, 40_001, 2, "adagrad", (3, 1)), nprocs=8, join=True)
