@@ -1,7 +1,11 @@
 """Device-resident FedAVG-family aggregation throughput on MI355X (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c5]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config ns|c2|c3|c4|c5|c1k]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
+
+`--gpus N` with no launcher env starts the N ranks itself (flearn_amd/launch.py: fresh children
+through torch.distributed.run, before any HIP call in the parent); it fails loudly when fewer
+than N GPUs are visible and never measures a smaller world than asked.
 
 One "step" = one server aggregation over device-resident client uploads: the fused HIP reduce of
 N clients x P fp32 parameters (+ the fused AVGM/Adagrad update for c3/c5) into the fp32 global
@@ -9,7 +13,9 @@ model, and for N>1 GPUs the RCCL all-gather that reassembles it on every GPU.  I
 synthetic (splitmix64 U(-1,1), generated on device), weights are Python 1.0 — flearn's default
 (Client.py:157) — so the arithmetic is FA_MODE_W32_DIV64, bit-identical to the reference.
 
-Configs (BASELINE.json):  c2  FedAVG    100 x ResNet-18 (11,699,112 fp32)      [default]
+Configs (BASELINE.json):  ns  FedAVG    100 x ResNet-50 (25,610,152 fp32)      [default: the
+                              north star's "100 clients x 25 M fp32 at 1 GPU" headline shape]
+                          c2  FedAVG    100 x ResNet-18 (11,699,112 fp32)
                           c3  FedAVGM   100 x ResNet-50 (25,610,152 fp32)
                           c4  FedAVG   1000 x ResNet-18
                           c5  FedOPT-Adagrad 100 x ViT-B/16 (86,567,656 fp32)
@@ -41,7 +47,7 @@ sys.path.insert(0, str(REPO))
 
 from flearn_amd import _native as na  # noqa: E402
 from flearn_amd import aggregator as agg  # noqa: E402
-from flearn_amd import layouts  # noqa: E402
+from flearn_amd import launch, layouts  # noqa: E402
 from flearn_amd.dist import ShardedReducer, ShardPlan, hip_reduce_fn  # noqa: E402
 
 METRIC = "device-resident GiB/s, FedAVG N-client weighted tensor reduce; %HBM peak"
@@ -51,12 +57,17 @@ DEFAULT_STRIPES = 2  # N>1: stripe 0's all-gather overlaps stripe 1's reduce ...
 DEFAULT_STRIPE_WEIGHTS = (3, 1)  # ... and the small last stripe leaves little of the gather exposed
 
 CONFIGS = {
+    "ns": dict(layout="resnet50", clients=100, op="mean",
+               workload="NS: FedAVG reduce, 100 clients x ResNet-50 state_dict (25,610,152 fp32 / 267 tensors) "
+                        "- the north star's 100 x 25 M headline shape"),
     "c2": dict(layout="resnet18", clients=100, op="mean",
                workload="C2: FedAVG reduce, 100 clients x ResNet-18 state_dict (11,699,112 fp32 / 102 tensors)"),
     "c3": dict(layout="resnet50", clients=100, op="avgm",
                workload="C3: FedAVGM (server momentum fused into reduce), 100 clients x ResNet-50 (25,610,152 fp32)"),
     "c4": dict(layout="resnet18", clients=1000, op="mean",
                workload="C4: FedAVG reduce, 1000 clients x ResNet-18 (11,699,112 fp32)"),
+    "c1k": dict(layout="lenet5", clients=1000, op="mean",
+                workload="C1k: FedAVG reduce, 1000 clients x LeNet5 (44,426 fp32) - small-P / deep-N shape"),
     "c5": dict(layout="vit_b_16", clients=100, op="adagrad",
                workload="C5: FedOPT-Adagrad fused with reduce, 100 clients x ViT-B/16 (86,567,656 fp32)"),
 }
@@ -128,7 +139,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--config", default="ns", choices=sorted(CONFIGS))
     ap.add_argument("--stripes", type=int, default=None, help="reduce/gather pipeline depth (N>1)")
     ap.add_argument("--stripe-weights", default=None,
                     help="relative stripe widths, e.g. 3,1 (default for 2 stripes); 'equal' for equal")
@@ -139,11 +150,16 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
+    # one process per GPU: with no launcher env, --gpus N > 1 starts the N ranks here, BEFORE any
+    # HIP call in this process (na.lib(), torch.cuda.set_device, ...), and exits with their status
+    if args.emulate_world is not None and args.gpus != 1:
+        raise SystemExit("--emulate-world is a single-process mode (use --gpus 1)")
+    rc = launch.ensure_ranks(args.gpus, __file__, sys.argv[1:])
+    if rc is not None:
+        sys.exit(rc)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
     na.lib()
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
