@@ -17,7 +17,7 @@ from pathlib import Path
 import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 
 LIB_PATH = Path(__file__).resolve().parent / "lib" / "libflearn_amd.so"
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 FA_OK = 0
 FA_ERR_ARG, FA_ERR_ALIGN, FA_ERR_LAUNCH = -1, -2, -3
@@ -35,6 +35,9 @@ EXPORTS = (
     "fa_reduce_f64",
     "fa_reduce_i64",
     "fa_opt_apply",
+    "fa_rows_plan",
+    "fa_reduce_f32_rows",
+    "fa_gather_rows",
     "fa_fill_uniform_f32",
     "fa_b64_decoded_size",
     "fa_b64_decode",
@@ -53,6 +56,13 @@ class NativeUnavailable(RuntimeError):
 
 class NativeError(RuntimeError):
     """A C-ABI call returned an error code."""
+
+
+class Piece(ctypes.Structure):
+    """struct fa_piece (include/flearn_amd.h)."""
+
+    _fields_ = [("col", ctypes.c_int64), ("seg_off", ctypes.c_int64), ("seg", ctypes.c_int32),
+                ("n_cols", ctypes.c_int32), ("reserved", ctypes.c_int64)]
 
 
 class Epilogue(ctypes.Structure):
@@ -117,6 +127,11 @@ def load(require_gpu: bool = False):
                 "fa_reduce_f64": ([P, I64, I32, P, D, I64, I64, P, P], ctypes.c_int),
                 "fa_reduce_i64": ([P, I64, I32, P, D, I64, I64, P, P], ctypes.c_int),
                 "fa_opt_apply": ([I32, ctypes.POINTER(Epilogue), P, P, I64, P, P, P], ctypes.c_int),
+                "fa_rows_plan": ([I32, P, P, I32, I32, P, I64, ctypes.POINTER(I64), ctypes.POINTER(I32)],
+                                 ctypes.c_int),
+                "fa_reduce_f32_rows": ([P, I32, I32, P, D, P, I64, I32, P, ctypes.POINTER(Epilogue), P, P, P],
+                                       ctypes.c_int),
+                "fa_gather_rows": ([P, I64, I32, I32, P, P, I32, P], ctypes.c_int),
                 "fa_fill_uniform_f32": ([P, I64, I32, I64, ctypes.c_uint64, I64, I64, P], ctypes.c_int),
                 "fa_b64_decoded_size": ([P, I64], I64),
                 "fa_b64_decode": ([P, I64, P, I64, I32], ctypes.c_int),

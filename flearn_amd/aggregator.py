@@ -22,7 +22,7 @@ import numpy as np
 import torch
 
 from . import _native as na
-from .bucket import BucketPlan, Packer, make_plan
+from .bucket import BucketPlan, Packer, RowTable, make_plan
 from .semantics import KIND_F32, KIND_F64, KIND_I64, Numerics
 
 _F64 = np.dtype(np.float64)
@@ -76,13 +76,21 @@ def reduce_stack(
     col_begin.  weights: fp32 for MODE_W32_*, f64 for MODE_W64 (device tensors).
     op=OP_DYN: FedDyn with h (fp32, in place) and v = theta (in place); prev unused."""
     L = na.lib()
-    _check_cuda(stack, "stack", torch.float32, 2)
-    if stack.stride(1) != 1:
-        raise ValueError("stack rows must be contiguous")
+    rows = isinstance(stack, RowTable)  # device uploads read in place (fa_reduce_f32_rows)
+    if rows:
+        if stack.elem_size != 4 or not stack.aligned:
+            raise ValueError("row table is not an aligned fp32 bucket")
+        if col_begin != 0 or (n_cols is not None and n_cols != stack.shape[1]):
+            raise ValueError("a row table is reduced over its whole bucket")
+        if n_clients is not None and n_clients != stack.shape[0]:
+            raise ValueError("a row table is reduced over all of its clients")
+    else:
+        _check_cuda(stack, "stack", torch.float32, 2)
+        if stack.stride(1) != 1:
+            raise ValueError("stack rows must be contiguous")
     n = stack.shape[0] if n_clients is None else n_clients
     if not 1 <= n <= stack.shape[0]:
         raise ValueError("n_clients out of range")
-    stride = stack.stride(0)
     ncols = stack.shape[1] - col_begin if n_cols is None else n_cols
     if col_begin < 0 or ncols < 0 or col_begin + ncols > stack.shape[1]:
         raise ValueError("column window out of range")
@@ -110,8 +118,19 @@ def reduce_stack(
         if prev.numel() < ncols or v.numel() < ncols:
             raise ValueError("prev / v too small")
         epi = _epilogue(op, prev, v, beta, eta, tau, beta2)
+    if rows:
+        pieces, npieces, grid = stack.piece_table(op)
+        rc = L.fa_reduce_f32_rows(
+            stack.ptrs.data_ptr(), n, mode, weights.data_ptr(), float(denom), pieces.data_ptr(), npieces, grid,
+            stack.work.data_ptr(),
+            ctypes.byref(epi) if epi is not None else None, _ptr(out32), _ptr(out64),
+            na.stream_handle(stack.device),
+        )
+        na.check(rc, "fa_reduce_f32_rows")
+        stack.release()
+        return
     rc = L.fa_reduce_f32(
-        stack.data_ptr(), stride, n, mode, weights.data_ptr(), float(denom), col_begin, ncols,
+        stack.data_ptr(), stack.stride(0), n, mode, weights.data_ptr(), float(denom), col_begin, ncols,
         ctypes.byref(epi) if epi is not None else None, _ptr(out32), _ptr(out64),
         na.stream_handle(stack.device),
     )
@@ -563,13 +582,25 @@ class Aggregator:
 
     def _finish(self, plan: BucketPlan, results: dict):
         if self.output == "device":
-            glob = {}
-            for k in plan.keys:
-                s = plan.key_segment[k]
-                lo, hi = s.offset, s.offset + s.numel
-                pieces = [t[max(lo, sh.c0) - sh.c0 : min(hi, sh.c1) - sh.c0].to(self.device)
-                          for sh, t in results[plan.key_group[k]] if max(lo, sh.c0) < min(hi, sh.c1)]
-                flat = pieces[0].clone() if len(pieces) == 1 else torch.cat(pieces)
-                glob[k] = flat.view(s.shape)
-            return glob
+            return assemble_on_device(plan, results, self.device)
         return self.packer.unpack(plan, results, as_torch=plan.input_kind == "torch")
+
+
+def assemble_on_device(plan: BucketPlan, results: dict, device) -> dict:
+    """output="device": the global model as fresh tensors on `device`.  Per bucket kind ONE fresh
+    buffer of the bucket's stride is filled with one copy per column shard (a peer copy over
+    xGMI for shards on other GPUs; a plain device copy for the local one), and every key is a
+    view of it — not one slice copy per (key, shard).  results: kind -> [(shard, tensor)]."""
+    device = torch.device(device)
+    full = {}
+    for kind, parts in results.items():
+        dt = parts[0][1].dtype
+        buf = torch.empty(plan.groups[kind].stride, dtype=dt, device=device)
+        for sh, t in parts:
+            buf[sh.c0 : sh.c1].copy_(t[: sh.width], non_blocking=True)
+        full[kind] = buf
+    glob = {}
+    for k in plan.keys:
+        s = plan.key_segment[k]
+        glob[k] = full[plan.key_group[k]][s.offset : s.offset + s.numel].view(s.shape)
+    return glob

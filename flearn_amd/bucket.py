@@ -18,6 +18,7 @@ from __future__ import annotations
 
 import collections
 import concurrent.futures
+import ctypes
 import math
 import threading
 from dataclasses import dataclass, field
@@ -266,11 +267,13 @@ class Packer:
         self.device = self.devices[0]
         self.workers = workers
         self._pinned = {}
+        self._pin_events = {}  # pinned staging key -> event after its last queued H2D
         self._dev = {}
         self._shards = {}
         self._pool = None
         self.last_wire_rows = 0
         self.last_wire_staged = 0
+        self.last_row_tables = {}  # kind -> "rows" | "gather" | "copy" for device-resident uploads
 
     def _executor(self) -> concurrent.futures.ThreadPoolExecutor:
         """One persistent pool per Packer: creating threads per call costs ~0.3 ms, which is the
@@ -286,6 +289,14 @@ class Packer:
             t = torch.zeros(math.prod(shape), dtype=dtype, **kw)
             cache[key] = t
         return t[: math.prod(shape)].view(shape)
+
+    def hold(self, objs, device) -> None:
+        """Keep `objs` (uploads read by queued launches) alive until the work queued so far on
+        `device`'s current stream is done; earlier holds whose events completed are dropped."""
+        self._held = [(e, o) for e, o in getattr(self, "_held", []) if not e.query()]
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(device))
+        self._held.append((ev, objs))
 
     def device_bucket(self, tag, shape, dtype, device=None):
         """A reusable device buffer (contents undefined)."""
@@ -318,6 +329,7 @@ class Packer:
         Returns kind -> [(shard, device stack [N, shard.width])]."""
         out = {}
         self.last_wire_staged = 0
+        self.last_row_tables = {}
         for kind, g in plan.groups.items():
             tdt = _TORCH[g.store_dtype]
             shards = self.shards(plan, kind)
@@ -328,9 +340,19 @@ class Packer:
             if pieces is None:
                 pieces = plan.memo[pk] = self._pieces(g, shards)
             if plan.input_kind == "torch" and all(w_local_lst[0][s.key].device.type == "cuda" for s in g.segments):
-                for n, w in enumerate(w_local_lst):
-                    for s, a, b, sh, d in pieces:
-                        devs[sh.index][n, d : d + (b - a)].copy_(w[s.key].reshape(-1)[a:b])
+                table = self.row_table(plan, g, w_local_lst, shards)
+                if table is not None and kind == KIND_F32 and len(shards) == 1 and table.aligned:
+                    out[kind] = [(shards[0], table)]  # read in place by fa_reduce_f32_rows
+                    self.last_row_tables[kind] = "rows"
+                    continue
+                if table is not None and len(shards) == 1:
+                    table.gather_into(devs[0])  # one launch for the whole bucket
+                    self.last_row_tables[kind] = "gather"
+                else:  # column shards over several devices: per-piece copies
+                    self.last_row_tables[kind] = "copy"
+                    for n, w in enumerate(w_local_lst):
+                        for s, a, b, sh, d in pieces:
+                            devs[sh.index][n, d : d + (b - a)].copy_(w[s.key].reshape(-1)[a:b])
             else:
                 rows = self._wire_rows(g, w_local_lst) if kind == KIND_F32 else [None] * plan.n_clients
                 if len(shards) == 1 and all(r is not None for r in rows):
@@ -342,11 +364,41 @@ class Packer:
                 if all(r is not None for r in rows):
                     hosts = [None] * len(shards)  # every row already sits in pinned memory
                 else:
-                    hosts = [self._buf(self._pinned, ("in", kind, sh.index), (plan.n_clients, sh.width), tdt,
-                                       pin_memory=True) for sh in shards]
+                    hkeys = [("in", kind, sh.index) for sh in shards]
+                    for hk in hkeys:  # the previous round's H2D from this staging must be done
+                        ev = self._pin_events.pop(hk, None)
+                        if ev is not None:
+                            ev.synchronize()
+                    hosts = [self._buf(self._pinned, hk, (plan.n_clients, sh.width), tdt, pin_memory=True)
+                             for hk, sh in zip(hkeys, shards)]
                 self._pack_pipelined(plan, pieces, w_local_lst, shards, hosts, devs, rows)
+                if hosts[0] is not None:
+                    for hk, sh in zip(hkeys, shards):
+                        ev = torch.cuda.Event()
+                        ev.record(torch.cuda.current_stream(sh.device))
+                        self._pin_events[hk] = ev
             out[kind] = list(zip(shards, devs))
         return out
+
+    def row_table(self, plan: BucketPlan, g: Group, w_local_lst, shards):
+        """RowTable of device-resident uploads for bucket group g, or None when some value is
+        not a contiguous tensor of its dtype on the bucket's (single) device."""
+        if len(shards) != 1:
+            return None
+        dev = shards[0].device
+        dt = _TORCH[g.store_dtype]
+        segs = [s for s in g.segments if s.numel > 0]
+        ptrs = np.empty((len(segs), plan.n_clients), dtype=np.int64)
+        keep = []
+        for j, s in enumerate(segs):
+            row = ptrs[j]
+            for n, w in enumerate(w_local_lst):
+                t = w[s.key]
+                if t.dtype != dt or t.device != dev or not t.is_contiguous():
+                    return None
+                row[n] = t.data_ptr()
+                keep.append(t)
+        return RowTable(self, plan, g, segs, ptrs, keep, dev)
 
     def _wire_stack(self, g: Group, w_local_lst, device):
         from .wire import wire_device_stack
@@ -474,3 +526,80 @@ class Packer:
             else:
                 glob[k] = arr
         return glob
+
+
+class RowTable:
+    """Device-resident uploads read where they lie (flearn's run2 path hands the server torch
+    tensors, flearn/server/Communicator.py:287-292): a device table of per-(key, client) tensor
+    pointers, [segments][clients], plus the bucket's piece table (fa_rows_plan, cached on the
+    plan).  fa_reduce_f32_rows reads every upload once in one launch, with no pack copy; the
+    8-byte kinds (BN counters) and unaligned fp32 tensors take one fa_gather_rows launch into a
+    device stack instead of N*K copy kernels.  `shape` = (clients, stride) like a stack.
+
+    The tensors are referenced until the launches that read them have completed (an event
+    recorded after them is checked at the next use of the packer), so the caching allocator
+    cannot hand their memory to another stream meanwhile."""
+
+    def __init__(self, packer: Packer, plan: BucketPlan, g: Group, segs, ptrs: np.ndarray, keep, device):
+        self.packer, self.plan, self.group, self.segs = packer, plan, g, segs
+        self.device = torch.device(device)
+        self.shape = (plan.n_clients, g.stride)
+        self.aligned = bool(ptrs.size == 0 or not (ptrs % 16).any())
+        self.n_pieces = 0
+        self.pieces = None
+        itemsize = np.dtype(g.store_dtype).itemsize
+        self.elem_size = itemsize
+        # the pointer table: reused pinned staging (waited on before it is rewritten), then H2D
+        key = ("rows", g.kind, str(self.device))
+        ev = packer._pin_events.pop(key, None)
+        if ev is not None:
+            ev.synchronize()
+        host = packer._buf(packer._pinned, key, (max(ptrs.size, 1),), torch.int64, pin_memory=True)
+        host[: ptrs.size].numpy()[:] = ptrs.reshape(-1)
+        self.ptrs = packer.device_bucket(key, (max(ptrs.size, 1),), torch.int64, self.device)
+        self.ptrs.copy_(host, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.device))
+        packer._pin_events[key] = ev
+        self.keep = keep
+        self.work = packer.device_bucket(("rows_work", str(self.device)), (1,), torch.int32, self.device)
+
+    def piece_table(self, op: int):
+        """(device fa_piece array, slot count, grid) for this bucket layout and epilogue, cached
+        on the plan."""
+        mk = ("row_pieces", self.group.kind, int(op), str(self.device))
+        hit = self.plan.memo.get(mk)
+        if hit is None:
+            L = na.load()
+            cols = np.array([s.offset for s in self.segs], dtype=np.int64)
+            lens = np.array([s.numel for s in self.segs], dtype=np.int64)
+            cnt, grid = ctypes.c_int64(), ctypes.c_int32()
+            with torch.cuda.device(self.device):  # the default grid follows this device's CUs
+                na.check(L.fa_rows_plan(len(self.segs), cols.ctypes.data, lens.ctypes.data, int(op), 0, None, 0,
+                                        ctypes.byref(cnt), ctypes.byref(grid)), "fa_rows_plan")
+                arr = np.zeros((max(cnt.value, 1), ctypes.sizeof(na.Piece)), dtype=np.uint8)
+                na.check(L.fa_rows_plan(len(self.segs), cols.ctypes.data, lens.ctypes.data, int(op), grid.value,
+                                        arr.ctypes.data, cnt.value, ctypes.byref(cnt), ctypes.byref(grid)),
+                         "fa_rows_plan")
+            dev = torch.from_numpy(arr.reshape(-1)).to(self.device)  # once per layout
+            hit = self.plan.memo[mk] = (dev, cnt.value, grid.value)
+        return hit
+
+    def gather_into(self, stack: torch.Tensor) -> None:
+        """One launch: every (key, client) tensor into its segment of the device stack [N, stride]."""
+        L = na.load()
+        mk = ("row_segs", self.group.kind, str(self.device))
+        segs = self.plan.memo.get(mk)
+        if segs is None:
+            t = np.array([s.offset for s in self.segs] + [s.numel for s in self.segs], dtype=np.int64)
+            segs = self.plan.memo[mk] = torch.from_numpy(t).to(self.device)
+        na.check(L.fa_gather_rows(stack.data_ptr(), stack.stride(0), self.shape[0], self.elem_size,
+                                  self.ptrs.data_ptr(), segs.data_ptr(), len(self.segs),
+                                  na.stream_handle(self.device)), "fa_gather_rows")
+        self.release()
+
+    def release(self) -> None:
+        """Call after the launches that read the uploads are queued: the packer keeps them alive
+        until those launches have completed."""
+        self.packer.hold(self.keep, self.device)
+        self.keep = []

@@ -464,15 +464,95 @@ __device__ __forceinline__ typename vec4<typename P::acc_t>::type quad_mul(
     return (AV)(typename P::acc_t)w * __builtin_convertvector(x, AV);
 }
 
+// Row addressing of the pipeline: a contiguous client stack (row i at tile0 + i*row_bytes), or a
+// table of per-client device pointers (row i at ptr[i] + off: uploads read where they lie).
+struct StackRows {
+  const char* tile0;
+  int64_t row_bytes;
+  __device__ __forceinline__ const char* operator()(int i) const { return tile0 + (int64_t)i * row_bytes; }
+};
+struct PtrRows {
+  const float* const* __restrict__ ptr;  // wave-uniform index: scalar loads
+  int64_t off_bytes;
+  __device__ __forceinline__ const char* operator()(int i) const {
+    return reinterpret_cast<const char*>(ptr[i]) + off_bytes;
+  }
+};
+
+// The rolling register pipeline over rows 0..n-1 of one piece (nq full quads, `bytes` = nq*16
+// per row; lane l owns quads l, l+64W, ...): acc[v] = sum_i w[i]*x[i] in list order.
+template <class P, int V, int D, int W, bool NT, class R>
+__device__ __forceinline__ void rows_sweep(const R& row, uint32_t bytes, int n,
+                                           const typename P::w_t* __restrict__ w,
+                                           typename vec4<typename P::acc_t>::type (&acc)[V]) {
+  typedef typename vec4<float>::type XV;
+  const int voff = (int)threadIdx.x * 16;
+  XV x[D][V];
+#pragma unroll
+  for (int d = 0; d < D; ++d)
+    if (1 + d < n) {
+      const __amdgpu_buffer_rsrc_t r = row_rsrc(row(1 + d), bytes);
+#pragma unroll
+      for (int v = 0; v < V; ++v) x[d][v] = buf_load_quad<NT>(r, voff + v * 64 * W * 16, 0);
+    }
+  {
+    const __amdgpu_buffer_rsrc_t r = row_rsrc(row(0), bytes);
+    const typename P::w_t w0 = w[0];
+#pragma unroll
+    for (int v = 0; v < V; ++v) acc[v] = quad_mul<P>(w0, buf_load_quad<NT>(r, voff + v * 64 * W * 16, 0));
+  }
+  // rows 1..n-1: slot d holds row i+d; consume it, refill it with row i+d+D (steady state:
+  // every refill is a real row, so no branch)
+  int i = 1;
+  for (; i + 2 * D <= n; i += D) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      const typename P::w_t wi = w[i + d];
+#pragma unroll
+      for (int v = 0; v < V; ++v) acc[v] = quad_axpy<P>(acc[v], wi, x[d][v]);
+      // pin the order "consume slot d, then refill it": if the scheduler hoists the refill
+      // (or the products of later slots) the old values need copies, and the copies wait for
+      // every in-flight row — the pipeline collapses into batches
+      __builtin_amdgcn_sched_barrier(0);
+      const __amdgpu_buffer_rsrc_t r = row_rsrc(row(i + d + D), bytes);
+#pragma unroll
+      for (int v = 0; v < V; ++v) x[d][v] = buf_load_quad<NT>(r, voff + v * 64 * W * 16, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  // drain: fewer than 2*D rows left (wave-uniform branches)
+#pragma unroll
+  for (int d = 0; d < D; ++d) {
+    if (i + d < n) {
+      const typename P::w_t wi = w[i + d];
+#pragma unroll
+      for (int v = 0; v < V; ++v) acc[v] = quad_axpy<P>(acc[v], wi, x[d][v]);
+      if (i + d + D < n) {
+        const __amdgpu_buffer_rsrc_t r = row_rsrc(row(i + d + D), bytes);
+#pragma unroll
+        for (int v = 0; v < V; ++v) x[d][v] = buf_load_quad<NT>(r, voff + v * 64 * W * 16, 0);
+      }
+    }
+  }
+#pragma unroll
+  for (int d = 0; d < D; ++d) {
+    if (i + D + d < n) {
+      const typename P::w_t wi = w[i + D + d];
+#pragma unroll
+      for (int v = 0; v < V; ++v) acc[v] = quad_axpy<P>(acc[v], wi, x[d][v]);
+    }
+  }
+}
+
 // Row-pipelined grid.  Built for deep, narrow windows (many clients, few columns: the per-rank
 // column shards of a multi-GPU aggregation, e.g. 800 clients x 365 K columns), where the
 // sub-tile kernels run out of column parallelism and a batch of rows that is issued, drained
 // and re-issued keeps only half its bytes in flight on average.  Here:
 //   * a block is W waves; lane l owns quads l, l+64W, ..., l+(V-1)*64W of the block's piece of
 //     every row (V*W KiB contiguous per row), so each wave instruction reads 1 KiB of one row;
-//   * rows are a rolling register pipeline D rows deep: row i+D is loaded right after row i is
-//     consumed, so D*V loads stay in flight per lane for the whole sweep (s_waitcnt
-//     vmcnt((D-1)*V) in the steady state, no drain per batch);
+//   * rows are a rolling register pipeline D rows deep (rows_sweep): row i+D is loaded right
+//     after row i is consumed, so D*V loads stay in flight per lane for the whole sweep
+//     (s_waitcnt vmcnt((D-1)*V) in the steady state, no drain per batch);
 //   * loads go through per-row buffer descriptors whose range check covers the window's end, so
 //     a partial last piece needs no per-lane branches (the slot offset rides in voffset, which
 //     the range check always covers); the one ragged quad (ncols % 4) goes to reduce_ragged.
@@ -484,72 +564,14 @@ __device__ __forceinline__ void rows_piece(const float* __restrict__ stack, int6
                                            int64_t qend) {
   // the piece is quads [qb, qend), qend - qb <= 64*W*V
   typedef typename P::acc_t A;
-  typedef typename vec4<float>::type XV;
   typedef typename vec4<A>::type AV;
   const int64_t qfull = ncols / 4;
   const int64_t left = (qend < qfull ? qend : qfull) - qb;
   const int nq = left <= 0 ? 0 : (int)left;  // full quads of the piece
   if (nq > 0) {
-    const char* tile0 = reinterpret_cast<const char*>(stack + col0 + qb * 4);
-    const uint32_t bytes = (uint32_t)nq * 16u;
-    const int64_t row_bytes = stride * 4;
-    const int voff = (int)threadIdx.x * 16;
-    XV x[D][V];
-#pragma unroll
-    for (int d = 0; d < D; ++d)
-      if (1 + d < n) {
-        const __amdgpu_buffer_rsrc_t r = row_rsrc(tile0 + (int64_t)(1 + d) * row_bytes, bytes);
-#pragma unroll
-        for (int v = 0; v < V; ++v) x[d][v] = buf_load_quad<NT>(r, voff + v * 64 * W * 16, 0);
-      }
     AV acc[V];
-    {
-      const __amdgpu_buffer_rsrc_t r = row_rsrc(tile0, bytes);
-      const typename P::w_t w0 = w[0];
-#pragma unroll
-      for (int v = 0; v < V; ++v) acc[v] = quad_mul<P>(w0, buf_load_quad<NT>(r, voff + v * 64 * W * 16, 0));
-    }
-    // rows 1..n-1: slot d holds row i+d; consume it, refill it with row i+d+D (steady state:
-    // every refill is a real row, so no branch)
-    int i = 1;
-    for (; i + 2 * D <= n; i += D) {
-#pragma unroll
-      for (int d = 0; d < D; ++d) {
-        const typename P::w_t wi = w[i + d];
-#pragma unroll
-        for (int v = 0; v < V; ++v) acc[v] = quad_axpy<P>(acc[v], wi, x[d][v]);
-        // pin the order "consume slot d, then refill it": if the scheduler hoists the refill
-        // (or the products of later slots) the old values need copies, and the copies wait for
-        // every in-flight row — the pipeline collapses into batches
-        __builtin_amdgcn_sched_barrier(0);
-        const __amdgpu_buffer_rsrc_t r = row_rsrc(tile0 + (int64_t)(i + d + D) * row_bytes, bytes);
-#pragma unroll
-        for (int v = 0; v < V; ++v) x[d][v] = buf_load_quad<NT>(r, voff + v * 64 * W * 16, 0);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    }
-    // drain: fewer than 2*D rows left (wave-uniform branches)
-#pragma unroll
-    for (int d = 0; d < D; ++d) {
-      if (i + d < n) {
-        const typename P::w_t wi = w[i + d];
-#pragma unroll
-        for (int v = 0; v < V; ++v) acc[v] = quad_axpy<P>(acc[v], wi, x[d][v]);
-        if (i + d + D < n) {
-          const __amdgpu_buffer_rsrc_t r = row_rsrc(tile0 + (int64_t)(i + d + D) * row_bytes, bytes);
-#pragma unroll
-          for (int v = 0; v < V; ++v) x[d][v] = buf_load_quad<NT>(r, voff + v * 64 * W * 16, 0);
-        }
-      }
-    }
-#pragma unroll
-    for (int d = 0; d < D; ++d) {
-      if (i + D + d < n) {
-        const typename P::w_t wi = w[i + D + d];
-#pragma unroll
-        for (int v = 0; v < V; ++v) acc[v] = quad_axpy<P>(acc[v], wi, x[d][v]);
-      }
-    }
+    rows_sweep<P, V, D, W, NT>(StackRows{reinterpret_cast<const char*>(stack + col0 + qb * 4), stride * 4},
+                               (uint32_t)nq * 16u, n, w, acc);
 #pragma unroll
     for (int v = 0; v < V; ++v) {
       const int q = v * 64 * W + (int)threadIdx.x;
@@ -559,6 +581,92 @@ __device__ __forceinline__ void rows_piece(const float* __restrict__ stack, int6
   // the window's ragged last quad (ncols % 4 != 0), in the piece that holds it
   if (threadIdx.x == 0 && qfull * 4 < ncols && qfull >= qb && qfull < qend)
     reduce_ragged<P, T, OP>(stack + col0, stride, n, w, qfull, qfull + 1, ncols, e);
+}
+
+// A segment's ragged last quad (1-3 elements) read through the row-pointer table.
+template <class P, typename T, int OP>
+__device__ __attribute__((noinline)) void reduce_ragged_ptr(const float* const* __restrict__ rp,
+                                                            int64_t off, int n,
+                                                            const typename P::w_t* __restrict__ w,
+                                                            int64_t col, int valid, const Epi<T>& e) {
+  typedef typename P::acc_t A;
+  typename vec4<A>::type acc;
+  {
+    const typename vec4<float>::type x = load_quad_guarded(rp[0] + off, valid);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[j] = P::mul(w[0], x[j]);
+  }
+#pragma unroll 1
+  for (int i = 1; i < n; ++i) {
+    const typename vec4<float>::type x = load_quad_guarded(rp[i] + off, valid);
+    const typename P::w_t wi = w[i];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[j] = add<A>(acc[j], P::mul(wi, x[j]));
+  }
+  finish_quad<T, OP, A>(e, col, valid, acc);
+}
+
+// Segmented row-pointer reduce (fa_reduce_f32_rows): uploads that are separate device tensors
+// per (client, key) are read where they lie — no pack copy.  Work = pieces (fa_rows_plan): each
+// is a column range of ONE segment, so every row of a piece is one contiguous range of one
+// tensor and gets one buffer descriptor; client order and epilogue are the row pipeline's.
+//   * scheduling: pieces come largest first; block b starts with piece b and then claims the
+//     next unclaimed one from a device counter (claimed at the START of its current piece, so
+//     the atomic's latency hides behind the sweep).  Blocks finish within about one small piece
+//     of each other whatever the mix of tensor sizes — a static split of 100 ResNet-sized
+//     uploads left a ~10% tail (tools/tune_rows.py);
+//   * narrow pieces (<= W KiB of a row: BN vectors, biases) are latency-bound, not
+//     bandwidth-bound: they take a one-quad-per-lane sweep V*D rows deep instead of D, so a
+//     64-element tensor of 100 clients costs ~7 HBM round trips instead of ~50.
+// The counter must be 0 at launch (the host clears it on the stream before each launch).
+template <class P, typename T, int OP, int V, int D, int W, bool NT>
+__global__ __launch_bounds__(64 * W) void reduce_kernel_segrows(const float* const* __restrict__ rows, int n,
+                                                                const typename P::w_t* __restrict__ w,
+                                                                const fa_piece* __restrict__ pieces,
+                                                                int64_t npieces, int* __restrict__ next, Epi<T> e) {
+  typedef typename P::acc_t A;
+  typedef typename vec4<A>::type AV;
+  __shared__ int s_next;
+  int64_t p = blockIdx.x;
+  while (p < npieces) {
+    int claimed = 0;
+    if (threadIdx.x == 0) claimed = (int)gridDim.x + atomicAdd(next, 1);
+    const fa_piece pc = pieces[p];
+    const float* const* rp = rows + (int64_t)pc.seg * n;
+    const int nq = pc.n_cols >> 2;
+    const PtrRows row{rp, pc.seg_off * 4};
+    if (nq > 64 * W) {
+      AV acc[V];
+      rows_sweep<P, V, D, W, NT>(row, (uint32_t)nq * 16u, n, w, acc);
+#pragma unroll
+      for (int v = 0; v < V; ++v) {
+        const int q = v * 64 * W + (int)threadIdx.x;
+        if (q < nq) finish_quad<T, OP, A>(e, pc.col + (int64_t)q * 4, 4, acc[v]);
+      }
+    } else if (nq > 0) {
+      AV acc[1];
+      rows_sweep<P, 1, V * D, W, NT>(row, (uint32_t)nq * 16u, n, w, acc);
+      if ((int)threadIdx.x < nq) finish_quad<T, OP, A>(e, pc.col + (int64_t)threadIdx.x * 4, 4, acc[0]);
+    }
+    if ((pc.n_cols & 3) && threadIdx.x == 0)
+      reduce_ragged_ptr<P, T, OP>(rp, pc.seg_off + (int64_t)nq * 4, n, w, pc.col + (int64_t)nq * 4, pc.n_cols & 3, e);
+    if (threadIdx.x == 0) s_next = claimed;
+    __syncthreads();
+    p = s_next;
+    __syncthreads();  // s_next is rewritten in the next iteration
+  }
+}
+
+// fa_gather_rows: block (s, i) copies client i's tensor of segment s into its stack row.
+template <typename E>
+__global__ __launch_bounds__(kThreads) void gather_rows_kernel(E* __restrict__ stack, int64_t stride, int n,
+                                                               const E* const* __restrict__ rows,
+                                                               const int64_t* __restrict__ segs, int nseg) {
+  const int s = blockIdx.x, i = blockIdx.y;
+  const int64_t col = segs[s], len = segs[nseg + s];
+  const E* src = rows[(int64_t)s * n + i];
+  E* dst = stack + (int64_t)i * stride + col;
+  for (int64_t k = threadIdx.x; k < len; k += kThreads) dst[k] = src[k];
 }
 
 // Work split: the window's 1-KiB chunks are cut into equal pieces of pc <= W*V chunks, as many

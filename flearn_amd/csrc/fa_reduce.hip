@@ -13,7 +13,9 @@
 
 #include <stdint.h>
 
+#include <algorithm>
 #include <string>
+#include <vector>
 
 #include "fa_device.hpp"
 #include "flearn_amd.h"
@@ -183,6 +185,46 @@ int launch_reduce(const typename P::x_t* stack, int64_t stride, int n, const voi
     hipLaunchKernelGGL(kern, dim3((unsigned)(grid > 0 ? grid : 1)), dim3(kThreads), 0, s, stack, stride, n, wt,
                        col0, ncols, e);
     return launch_check();
+  }
+}
+
+// Segmented row-pointer reduce (fa_reduce_f32_rows).  fa_rows_plan cuts every segment into pieces
+// of at most kSegPieceChunks KiB of a row, largest first; blocks claim them dynamically (see
+// reduce_kernel_segrows).  A block keeps one 64-KiB piece row in flight (plain mean: 4 waves x
+// 16 KiB; fused epilogues: 8 waves x 8 KiB) and narrow pieces V rows of one quad per lane.
+// One block per CU (tools/tune_rows.py, profiles/r02/tune_rows: 64-KiB pieces on 256 blocks beat
+// 32-KiB pieces two rows deep and 192 / 384 blocks on 100 x ResNet-18 and 100 x ResNet-50).  Plain mean: 4 waves x 8 KiB, D = 2; fused epilogues: 8 waves
+// x 4 KiB, D = 2.
+constexpr int kSegPieceChunks = 64;
+constexpr double kSegBlocksPerCU = 1.0;
+
+template <class P, typename T, int OP>
+int launch_segrows(const float* const* rows, int n, const void* w, const fa_piece* pieces, int64_t npieces,
+                   int grid, int32_t* work, const Epi<T>& e, hipStream_t s) {
+  const typename P::w_t* wt = static_cast<const typename P::w_t*>(w);
+  if constexpr (OP == FA_OP_MEAN) {
+    constexpr int W = 4, V = kSegPieceChunks / W;  // 16 KiB per wave, one row in flight
+    hipLaunchKernelGGL((reduce_kernel_segrows<P, T, OP, V, kPieceChunks / (V * W), W, kNT>), dim3((unsigned)grid),
+                       dim3(64 * W), 0, s, rows, n, wt, pieces, npieces, work, e);
+  } else {
+    constexpr int W = 8, V = kSegPieceChunks / W;
+    hipLaunchKernelGGL((reduce_kernel_segrows<P, T, OP, V, kPieceChunks / (V * W), W, kNT>), dim3((unsigned)grid),
+                       dim3(64 * W), 0, s, rows, n, wt, pieces, npieces, work, e);
+  }
+  return launch_check();
+}
+
+template <class P, typename T>
+int dispatch_segrows(int op, const float* const* rows, int n, const void* w, const fa_piece* pieces,
+                     int64_t npieces, int grid, int32_t* work, const Epi<T>& e, hipStream_t s) {
+  switch (op) {
+    case FA_OP_MEAN: return launch_segrows<P, T, FA_OP_MEAN>(rows, n, w, pieces, npieces, grid, work, e, s);
+    case FA_OP_AVGM: return launch_segrows<P, T, FA_OP_AVGM>(rows, n, w, pieces, npieces, grid, work, e, s);
+    case FA_OP_ADAGRAD: return launch_segrows<P, T, FA_OP_ADAGRAD>(rows, n, w, pieces, npieces, grid, work, e, s);
+    case FA_OP_YOGI: return launch_segrows<P, T, FA_OP_YOGI>(rows, n, w, pieces, npieces, grid, work, e, s);
+    case FA_OP_ADAM: return launch_segrows<P, T, FA_OP_ADAM>(rows, n, w, pieces, npieces, grid, work, e, s);
+    case FA_OP_DYN: return launch_segrows<P, T, FA_OP_DYN>(rows, n, w, pieces, npieces, grid, work, e, s);
+    default: return fail(FA_ERR_ARG, "unknown epilogue op");
   }
 }
 
@@ -369,6 +411,96 @@ int fa_opt_apply(int32_t prec, const fa_epilogue* epi, const float* local, const
     return fail(FA_ERR_ARG, "unknown precision");
   }
 #undef FA_APPLY
+  return launch_check();
+}
+
+int fa_rows_plan(int32_t n_segments, const int64_t* seg_col, const int64_t* seg_len, int32_t op,
+                 int32_t grid_hint, fa_piece* pieces, int64_t cap, int64_t* n_pieces, int32_t* grid) {
+  if (n_segments < 0 || (n_segments > 0 && (!seg_col || !seg_len)) || !n_pieces || !grid)
+    return fail(FA_ERR_ARG, "bad rows plan arguments");
+  if (op < FA_OP_MEAN || op > FA_OP_DYN) return fail(FA_ERR_ARG, "unknown epilogue op");
+  constexpr int64_t kMaxCols = (int64_t)kSegPieceChunks * 256;  // columns per piece
+  int64_t count = 0;
+  for (int32_t s = 0; s < n_segments; ++s) {
+    if (seg_len[s] < 0 || seg_col[s] < 0 || seg_col[s] % 4 != 0)
+      return fail(FA_ERR_ARG, "segment columns must be >= 0 and 4-aligned");
+    count += (seg_len[s] + kMaxCols - 1) / kMaxCols;
+  }
+  int64_t g = grid_hint > 0 ? grid_hint : (int64_t)(device_cus() * kSegBlocksPerCU + 0.5);
+  if (g > count) g = count;
+  *grid = (int32_t)g;
+  *n_pieces = count;
+  if (!pieces) return FA_OK;
+  if (cap < count) return fail(FA_ERR_SIZE, "piece array too small");
+  int64_t k = 0;
+  for (int32_t s = 0; s < n_segments; ++s) {
+    const int64_t len = seg_len[s];
+    for (int64_t off = 0; off < len; off += kMaxCols) {  // full pieces, then the segment's remainder
+      fa_piece& p = pieces[k++];
+      p.col = seg_col[s] + off;
+      p.seg_off = off;
+      p.seg = s;
+      p.n_cols = (int32_t)(len - off < kMaxCols ? len - off : kMaxCols);
+      p.reserved = 0;
+    }
+  }
+  // largest first (stable: equal pieces keep bucket order, so neighbouring blocks start on
+  // neighbouring columns): the dynamically claimed tail is made of the smallest pieces
+  std::stable_sort(pieces, pieces + k, [](const fa_piece& a, const fa_piece& b) { return a.n_cols > b.n_cols; });
+  return FA_OK;
+}
+
+int fa_reduce_f32_rows(const float* const* rows, int32_t n_clients, int32_t mode, const void* weights,
+                       double denom, const fa_piece* pieces, int64_t n_pieces, int32_t grid, int32_t* work,
+                       const fa_epilogue* epi, float* out32, double* out64, void* stream) {
+  if (n_clients <= 0) return fail(FA_ERR_ARG, "n_clients must be >= 1");
+  if (n_pieces < 0 || (n_pieces > 0 && (!rows || !pieces || !work))) return fail(FA_ERR_ARG, "null rows, pieces or work");
+  if (n_pieces > 0 && (grid <= 0 || grid > n_pieces)) return fail(FA_ERR_ARG, "grid must be in [1, n_pieces]");
+  if (!weights) return fail(FA_ERR_ARG, "null weights");
+  if (!out32 && !out64) return fail(FA_ERR_ARG, "no output");
+  if (n_pieces == 0) return FA_OK;
+  const int op = epi ? epi->op : FA_OP_MEAN;
+  int rc;
+  if ((rc = check_columns(out32, out64, epi ? epi->prev : nullptr, epi ? epi->v : nullptr,
+                          mode == FA_MODE_W32_DIV32 ? sizeof(float) : sizeof(double), epi ? epi->h : nullptr)))
+    return rc;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (hipMemsetAsync(work, 0, sizeof(int32_t), s) != hipSuccess) return fail(FA_ERR_LAUNCH, "clearing the piece counter");
+  if (mode == FA_MODE_W32_DIV64) {
+    Epi<double> e;
+    if ((rc = make_epi<double>(epi, denom, n_clients, out32, out64, &e))) return rc;
+    return dispatch_segrows<AccF32, double>(op, rows, n_clients, weights, pieces, n_pieces, grid, work, e, s);
+  }
+  if (mode == FA_MODE_W32_DIV32) {
+    Epi<float> e;
+    if ((rc = make_epi<float>(epi, denom, n_clients, out32, out64, &e))) return rc;
+    return dispatch_segrows<AccF32, float>(op, rows, n_clients, weights, pieces, n_pieces, grid, work, e, s);
+  }
+  if (mode == FA_MODE_W64) {
+    Epi<double> e;
+    if ((rc = make_epi<double>(epi, denom, n_clients, out32, out64, &e))) return rc;
+    return dispatch_segrows<AccF32W64, double>(op, rows, n_clients, weights, pieces, n_pieces, grid, work, e, s);
+  }
+  return fail(FA_ERR_ARG, "unknown reduce mode");
+}
+
+int fa_gather_rows(void* stack, int64_t row_stride, int32_t n_clients, int32_t elem_size,
+                   const void* const* rows, const int64_t* segs, int32_t n_segments, void* stream) {
+  if (n_clients < 0 || n_segments < 0 || row_stride < 0) return fail(FA_ERR_ARG, "bad gather sizes");
+  if (n_clients == 0 || n_segments == 0) return FA_OK;
+  if (!stack || !rows || !segs) return fail(FA_ERR_ARG, "null gather pointer");
+  if (n_clients > 65535) return fail(FA_ERR_ARG, "too many clients for one gather");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const dim3 grid((unsigned)n_segments, (unsigned)n_clients);
+  if (elem_size == 4) {
+    hipLaunchKernelGGL(gather_rows_kernel<uint32_t>, grid, dim3(kThreads), 0, s, static_cast<uint32_t*>(stack),
+                       row_stride, n_clients, reinterpret_cast<const uint32_t* const*>(rows), segs, n_segments);
+  } else if (elem_size == 8) {
+    hipLaunchKernelGGL(gather_rows_kernel<uint64_t>, grid, dim3(kThreads), 0, s, static_cast<uint64_t*>(stack),
+                       row_stride, n_clients, reinterpret_cast<const uint64_t* const*>(rows), segs, n_segments);
+  } else {
+    return fail(FA_ERR_ARG, "elem_size must be 4 or 8");
+  }
   return launch_check();
 }
 

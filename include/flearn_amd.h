@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define FA_ABI_VERSION 3
+#define FA_ABI_VERSION 4
 
 /* return codes */
 #define FA_OK 0
@@ -120,6 +120,52 @@ int fa_reduce_i64(const int64_t* stack, int64_t row_stride, int32_t n_clients,
  *   local  : [n] fp32 w_local; glob : [n] the received w_glob.                                */
 int fa_opt_apply(int32_t prec, const fa_epilogue* epi, const float* local, const void* glob,
                  int64_t n, float* out32, double* out64, void* stream);
+
+/* ---- device-resident uploads read in place (row-pointer form) --------------------------------
+ * flearn's simulator path hands the server torch tensors (run2, flearn/server/Communicator.py:
+ * 287-292, then Server.ensemble -> strategy.server, flearn/server/Server.py:140): on the GPU
+ * every (client, key) tensor is its own allocation.  Instead of packing N*K tensors into a
+ * stack, these read them where they lie.  A SEGMENT is one key: columns [seg_col, +seg_len) of
+ * the logical bucket (the index of out32 / out64 / prev / v / h), stored for client i at
+ * rows[s * n_clients + i] (a device pointer to seg_len contiguous elements).                    */
+
+/* One unit of work of fa_reduce_f32_rows: logical columns [col, col + n_cols) = elements
+ * [seg_off, seg_off + n_cols) of segment seg.  Built by fa_rows_plan.                          */
+typedef struct fa_piece {
+  int64_t col;
+  int64_t seg_off;
+  int32_t seg;
+  int32_t n_cols;
+  int64_t reserved;
+} fa_piece;
+
+/* HOST function: the work plan of fa_reduce_f32_rows: every segment cut into pieces of at most
+ * 64 KiB of a row, largest first, and the grid to launch (grid_hint <= 0: the library's default
+ * for the current device, never more than the piece count).  seg_col[s] must be a multiple of 4.
+ * pieces == NULL or cap too small: *n_pieces / *grid report the sizes (FA_ERR_SIZE when
+ * pieces != NULL).                                                                             */
+int fa_rows_plan(int32_t n_segments, const int64_t* seg_col, const int64_t* seg_len, int32_t op,
+                 int32_t grid_hint, fa_piece* pieces, int64_t cap, int64_t* n_pieces, int32_t* grid);
+
+/* fa_reduce_f32 over row pointers: same modes, weights, epilogues and bit-exact client order,
+ * one launch, HBM traffic = the uploads once + the outputs / state.  Replaces server_ensemble
+ * (strategy.py:102-130) for device-resident fp32 uploads.
+ *   rows   : device array [n_segments * n_clients] of device pointers, each 16-byte aligned;
+ *   pieces : device copy of fa_rows_plan's n_pieces pieces (same op), launched on its grid;
+ *   work   : device int32 scratch (1 element): the blocks' piece counter, cleared on the stream
+ *            before the launch; one launch at a time may use it.
+ * Columns outside every segment (alignment gaps of the bucket) are not written.               */
+int fa_reduce_f32_rows(const float* const* rows, int32_t n_clients, int32_t mode, const void* weights,
+                       double denom, const fa_piece* pieces, int64_t n_pieces, int32_t grid, int32_t* work,
+                       const fa_epilogue* epi, float* out32, double* out64, void* stream);
+
+/* One-launch gather of device tensors into a client stack (elem_size 4 or 8):
+ *   stack[i * row_stride + seg_col[s] + e] = rows[s * n_clients + i][e],  e < seg_len[s].
+ * For the small kinds (int64 / float64 buffers: BN num_batches_tracked) and fp32 tensors that
+ * are not 16-byte aligned.  segs: device int64 array [2 * n_segments] = seg_col..., seg_len....
+ * Any alignment (element-wise copies).                                                         */
+int fa_gather_rows(void* stack, int64_t row_stride, int32_t n_clients, int32_t elem_size,
+                   const void* const* rows, const int64_t* segs, int32_t n_segments, void* stream);
 
 /* Synthetic client data: dst[r*row_stride + c] = U(-1,1) from splitmix64 of
  * (seed, row_begin + r, col_global_begin + c) — the bench/test generator; the CPU oracle

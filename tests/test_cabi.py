@@ -124,3 +124,76 @@ def test_apply_and_fill_validation(L):
     assert L.fa_opt_apply(na.PREC_F64, None, FAKE, FAKE, 8, FAKE, None, None) == header_define("FA_ERR_ARG")
     assert L.fa_fill_uniform_f32(FAKE, 64, 70000, 64, 1, 0, 0, None) == header_define("FA_ERR_ARG")
     assert L.fa_fill_uniform_f32(FAKE, 8, 1, 64, 1, 0, 0, None) == header_define("FA_ERR_ARG")
+
+
+def test_piece_struct_layout_matches_c(tmp_path):
+    src = tmp_path / "piece.c"
+    src.write_text('#include <stddef.h>\n#include <stdio.h>\n#include "flearn_amd.h"\n'
+                   'int main(void){printf("%zu %zu %zu %zu %zu\\n", sizeof(fa_piece), offsetof(fa_piece,col),'
+                   'offsetof(fa_piece,seg_off),offsetof(fa_piece,seg),offsetof(fa_piece,n_cols));return 0;}\n')
+    exe = tmp_path / "piece"
+    subprocess.run(["gcc", "-I", str(HEADER.parent), str(src), "-o", str(exe)], check=True)
+    c = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True).stdout.split()]
+    P = na.Piece
+    assert c == [ctypes.sizeof(P), P.col.offset, P.seg_off.offset, P.seg.offset, P.n_cols.offset]
+
+
+def _plan(L, cols, lens, op=0, grid=0):
+    S = len(cols)
+    c = (ctypes.c_int64 * max(S, 1))(*cols)
+    n = (ctypes.c_int64 * max(S, 1))(*lens)
+    cnt, g = ctypes.c_int64(-1), ctypes.c_int32(-1)
+    assert L.fa_rows_plan(S, c, n, op, grid, None, 0, ctypes.byref(cnt), ctypes.byref(g)) == 0
+    arr = (na.Piece * max(cnt.value, 1))()
+    if cnt.value:
+        small, g2 = ctypes.c_int64(), ctypes.c_int32()
+        assert L.fa_rows_plan(S, c, n, op, grid, arr, cnt.value - 1, ctypes.byref(small),
+                              ctypes.byref(g2)) == header_define("FA_ERR_SIZE")
+    assert L.fa_rows_plan(S, c, n, op, grid, arr, cnt.value, ctypes.byref(cnt), ctypes.byref(g)) == 0
+    return [(p.col, p.seg_off, p.seg, p.n_cols) for p in arr[: cnt.value]], g.value
+
+
+@pytest.mark.parametrize("grid", [192, 7, 0])
+def test_rows_plan_covers_every_segment_once(L, grid):
+    """fa_rows_plan (host): pieces tile each segment exactly, stay inside one segment, start on
+    64-KiB boundaries within it (full pieces, then the remainder), largest first; the grid never
+    exceeds the piece count."""
+    lens = [1, 3, 4, 63, 64, 255, 256, 257, 8191, 8192, 8193, 2_359_296, 0, 100_003]
+    cols, c = [], 0
+    for n in lens:
+        cols.append(c)
+        c += -(-max(n, 1) // 64) * 64
+    pieces, g = _plan(L, cols, lens, grid=grid)
+    assert 1 <= g <= len(pieces) and (grid == 0 or g == min(grid, len(pieces)))
+    assert [p[3] for p in pieces] == sorted((p[3] for p in pieces), reverse=True)
+    for s, (c0, n) in enumerate(zip(cols, lens)):
+        mine = sorted((p for p in pieces if p[2] == s), key=lambda p: p[1])
+        assert sum(p[3] for p in mine) == n
+        off = 0
+        for col, seg_off, _, w in mine:
+            assert seg_off == off and col == c0 + off and 0 < w <= 16384 and seg_off % 16384 == 0
+            off += w
+    assert len([p for p in pieces if p[2] == lens.index(2_359_296)]) == 2_359_296 // 16384
+
+
+def test_rows_plan_empty(L):
+    assert _plan(L, [0, 64], [0, 0]) == ([], 0)
+
+
+def test_rows_entry_points_validate(L):
+    cnt, g = ctypes.c_int64(), ctypes.c_int32()
+    c = (ctypes.c_int64 * 1)(2)  # not 4-aligned
+    n = (ctypes.c_int64 * 1)(8)
+    assert L.fa_rows_plan(1, c, n, 0, 0, None, 0, ctypes.byref(cnt), ctypes.byref(g)) == header_define("FA_ERR_ARG")
+    assert L.fa_rows_plan(1, c, n, 9, 0, None, 0, ctypes.byref(cnt), ctypes.byref(g)) == header_define("FA_ERR_ARG")
+    err = header_define("FA_ERR_ARG")
+    assert L.fa_reduce_f32_rows(FAKE, 0, 0, FAKE, 1.0, FAKE, 1, 1, FAKE, None, FAKE, None, None) == err
+    assert L.fa_reduce_f32_rows(None, 2, 0, FAKE, 1.0, FAKE, 1, 1, FAKE, None, FAKE, None, None) == err
+    assert L.fa_reduce_f32_rows(FAKE, 2, 0, FAKE, 1.0, FAKE, 1, 1, None, None, FAKE, None, None) == err  # work
+    assert L.fa_reduce_f32_rows(FAKE, 2, 0, FAKE, 1.0, FAKE, 1, 1, FAKE, None, None, None, None) == err
+    assert L.fa_reduce_f32_rows(FAKE, 2, 0, FAKE, 1.0, FAKE, 4, 5, FAKE, None, FAKE, None, None) == err  # grid
+    assert L.fa_reduce_f32_rows(FAKE, 2, 0, FAKE, 1.0, FAKE, 1, 1, FAKE, None, FAKE + 4, None, None) == header_define("FA_ERR_ALIGN")
+    assert L.fa_reduce_f32_rows(FAKE, 2, 0, FAKE, 1.0, FAKE, 0, 0, FAKE, None, FAKE, None, None) == 0  # no pieces
+    assert L.fa_gather_rows(FAKE, 64, 2, 2, FAKE, FAKE, 1, None) == err  # element size
+    assert L.fa_gather_rows(FAKE, 64, 70000, 4, FAKE, FAKE, 1, None) == err
+    assert L.fa_gather_rows(FAKE, 64, 0, 4, FAKE, FAKE, 1, None) == 0

@@ -2,6 +2,7 @@
 C oracle.  Bar: bit-exact (every output dtype, NaN position and sign of zero) — the kernels run
 the reference's fp32/f64 operation sequence with no contraction."""
 import math
+import os
 
 import numpy as np
 import pytest
@@ -391,28 +392,65 @@ def test_deterministic(cuda):
     assert torch.equal(a, b)
 
 
+# BASELINE-size cases: full HIP run at the production grid, compared on EVERY element (C2, the
+# north-star 100 x ResNet-50 shape, C3 fused AVGM) or on 64+ dense windows that include every
+# stripe / rank boundary of the default 8-GPU plan and the row-major kernel's piece-group
+# boundaries (C4, C5: 35-47 GB stacks).  Inputs are counter-based, so the host regenerates any
+# column range; the C oracle reduces it in threads (ctypes releases the GIL).
 # ---------------------------------------------------------------------------------------------
-# BASELINE-size cases: full HIP run, spot-checked column windows regenerated on the host
-# ---------------------------------------------------------------------------------------------
+
+_HOST_WORKERS = min(16, os.cpu_count() or 1)  # the GPU box's CPU share
 
 
-def _spot_windows(p, width=4096):
-    starts = [0, (p // 3) & ~63, (p // 2) & ~63, max(0, (p - width) & ~63)]
-    return [(s, min(width, p - s)) for s in starts]
+def _oracle_columns(n, c0, width, seed, op, prev_h):
+    g = oracle.c_reduce(oracle.MODE_W32_DIV64, oracle.fill_uniform(n, width, seed, row0=0, col0=c0),
+                        np.ones(n, np.float32), float(n))
+    if op != "mean":
+        g = oracle.c_update(op, g, prev_h[c0 : c0 + width], np.zeros(width))
+    return g.astype(np.float32)
 
 
-@pytest.mark.slow
-@pytest.mark.parametrize("layout,n,op", [("resnet18", 100, "mean"), ("resnet50", 100, "avgm"),
-                                         ("vit_b_16", 100, "adagrad"), ("resnet18", 1000, "mean")])
-def test_baseline_config_spot_parity(layout, n, op, cuda):
-    """Configs 2-5 at full size on one GPU: the kernel runs over the whole bucket; column windows
-    at the start / middle / end are recomputed by the C oracle from regenerated inputs."""
+def _rowmajor_piece_starts(p, cus=256):
+    """Column starts of the row-major kernel's pieces and KG groups (mirror of fa_reduce.hip
+    rowmajor_geometry + reduce_kernel_rowmajor's split), for placing check windows on them."""
+    chunks = ((p + 3) // 4 + 63) // 64
+    for d in range(0, cus - 160 + 1):
+        for g in ([192 + d] if d == 0 else [192 + d, 192 - d]):
+            if not 160 <= g <= cus:
+                continue
+            k = -(-chunks // (g * 64))
+            if k < 2:
+                return []
+            for kg in (4, 3, 2, 5):
+                if k % kg == 0 and (kg != 5 or k == 5):
+                    pc = -(-chunks // (g * k))
+                    starts = {pj * pc * 256 for pj in range(0, g * k, max(1, g // 4))}  # a sample of pieces
+                    starts |= {(g0 * g) * pc * 256 for g0 in range(0, k, kg)}  # group starts (block 0)
+                    starts |= {((g0 + kg) * g - 1) * pc * 256 for g0 in range(0, k, kg)}  # group ends
+                    return sorted(s for s in starts if s < p)
+    return []
+
+
+def _dense_windows(p, width=4096, count=64):
+    from flearn_amd.dist import ShardPlan
+
+    starts = {(i * (p - width) // (count - 1)) & ~63 for i in range(count)}
+    for r in range(8):  # stripe / rank boundaries of bench's default G=8 plan (2 stripes, 3:1)
+        plan = ShardPlan.make(p, 8, r, 2, weights=(3, 1))
+        for c in range(plan.stripes):
+            g0 = plan.global_begin(c)
+            starts |= {max(0, g0 - width // 2), min(g0 + plan.shard_of(c), p) - width // 2}
+    starts |= {max(0, s - width // 2) for s in _rowmajor_piece_starts(p)}
+    return sorted({(max(0, min(s, p - width)) & ~3, min(width, p)) for s in starts})
+
+
+def _run_config(layout, n, op, cuda, seed=1234):
     p = layouts.padded_f32_stride(layouts.get(layout))
     x = torch.empty((n, p), dtype=torch.float32, device=cuda)
-    agg.fill_uniform(x, seed=1234)
+    agg.fill_uniform(x, seed=seed)
     w = torch.ones(n, dtype=torch.float32, device=cuda)
     out32 = torch.empty(p, dtype=torch.float32, device=cuda)
-    kw = {}
+    kw, prev_h = {}, None
     if op != "mean":
         prev = torch.empty((1, p), dtype=torch.float32, device=cuda)
         agg.fill_uniform(prev, seed=1)
@@ -423,15 +461,52 @@ def test_baseline_config_spot_parity(layout, n, op, cuda):
     got = out32.cpu().numpy()
     del x
     torch.cuda.empty_cache()
-    for c0, width in _spot_windows(p):
-        cols = oracle.fill_uniform(n, width, 1234, row0=0, col0=c0)
-        g = oracle.c_reduce(oracle.MODE_W32_DIV64, cols, np.ones(n, np.float32), float(n))
-        if op != "mean":
-            g = oracle.c_update(op, g, prev_h[c0 : c0 + width], np.zeros(width))
-        assert bitwise_equal(got[c0 : c0 + width], g.astype(np.float32)), (layout, c0)
+    return p, got, prev_h
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("layout,n,op", [("resnet18", 100, "mean"), ("resnet50", 100, "mean"),
+                                         ("resnet50", 100, "avgm")])
+def test_baseline_config_full_parity(layout, n, op, cuda):
+    """C2, the north-star shape and C3: every one of the P outputs bit-equal to the C oracle."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    p, got, prev_h = _run_config(layout, n, op, cuda)
+    chunk = 1 << 16
+    bad = []
+
+    def job(c0):
+        width = min(chunk, p - c0)
+        if not bitwise_equal(got[c0 : c0 + width], _oracle_columns(n, c0, width, 1234, op, prev_h)):
+            bad.append(c0)
+
+    with ThreadPoolExecutor(_HOST_WORKERS) as ex:
+        list(ex.map(job, range(0, p, chunk)))
+    assert not bad, (layout, op, sorted(bad)[:8])
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("layout,n,op", [("vit_b_16", 100, "adagrad"), ("resnet18", 1000, "mean")])
+def test_baseline_config_window_parity(layout, n, op, cuda):
+    """C5 and C4 at full size: >= 64 evenly spaced 4096-column windows plus every 8-GPU stripe /
+    rank boundary and the row-major kernel's piece-group boundaries."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    p, got, prev_h = _run_config(layout, n, op, cuda)
+    wins = _dense_windows(p)
+    assert len(wins) >= 64
+
+    def job(win):
+        c0, width = win
+        return c0 if not bitwise_equal(got[c0 : c0 + width], _oracle_columns(n, c0, width, 1234, op, prev_h)) else None
+
+    with ThreadPoolExecutor(_HOST_WORKERS) as ex:
+        bad = [c for c in ex.map(job, wins) if c is not None]
+    assert not bad, (layout, op, bad[:8])
     assert np.isfinite(got).all()
 
 
+# ---------------------------------------------------------------------------------------------
 # ---------------------------------------------------------------------------------------------
 # multi-GPU code path on one GPU: a 1-rank RCCL group runs the exact all-gather call sequence
 # ---------------------------------------------------------------------------------------------

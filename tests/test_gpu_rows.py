@@ -1,0 +1,178 @@
+"""GPU parity of device-resident uploads read in place (fa_reduce_f32_rows / fa_gather_rows).
+
+flearn's simulator path hands the server torch tensors (run2: flearn/server/Communicator.py:
+287-292 -> Server.ensemble -> strategy.server, Server.py:140).  On the GPU each (client, key)
+tensor is its own allocation; the engine reads them through a device table of pointers in one
+launch instead of packing N*K tensors.  Bar: bit-exact against the reference's fixtures and
+against the stack kernel (itself bit-exact vs the C oracle) on the same data."""
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from flearn_amd import AVG, AVGM, OPT, Dyn
+from flearn_amd import _native as na
+from flearn_amd import aggregator as agg
+from flearn_amd import layouts
+from golden_io import Golden, bitwise_equal
+
+pytestmark = pytest.mark.gpu
+
+
+def _to_cuda(c, cuda):
+    return {k: (v.to(cuda) if isinstance(v, torch.Tensor) else torch.from_numpy(np.asarray(v)).to(cuda))
+            for k, v in c.items()}
+
+
+def _upload(clients, weights):
+    return [{"agg_weight": w, "params": c} for w, c in zip(weights, clients)]
+
+
+def _host(v):
+    return v.detach().cpu().numpy() if isinstance(v, torch.Tensor) else np.asarray(v)
+
+
+@pytest.mark.parametrize("name", ["avg_torch_n3", "avg_w1_n10", "avg_w1_n100", "avg_pyint_n100", "avg_np32_n10",
+                                  "avg_np64_n10", "avg_npint64_n10", "avg_special_n5", "avg_negzero_n1",
+                                  "avg_bnmodel_pyint_n4", "avg_bnmodel_pyfloat_n4", "trace_lenet5_round0",
+                                  "avg_lenet5_n10"])
+def test_device_uploads_read_in_place(name, cuda):
+    g = Golden(name)
+    clients = [_to_cuda(c, cuda) for c in g.clients()]
+    s = AVG()
+    got = s.server(_upload(clients, g.weights()), 0)["w_glob"]
+    packer = s.engine.packer
+    assert packer.last_row_tables.get("f32") == "rows", packer.last_row_tables  # no pack copy
+    for k, w in g.output().items():
+        assert bitwise_equal(_host(got[k]), np.asarray(w)), (name, k)
+
+
+def test_unaligned_device_uploads_take_one_gather(cuda):
+    """Views at odd element offsets cannot feed 16-B buffer loads: one fa_gather_rows launch
+    packs them, and the result is still bit-exact."""
+    g = Golden("avg_w1_n10")
+    clients = []
+    for c in g.clients():
+        flat = torch.empty(sum(v.size for v in c.values()) + 1, dtype=torch.float32, device=cuda)
+        d, off = {}, 1  # every view starts 4 bytes past an allocation boundary
+        for k, v in c.items():
+            d[k] = flat[off : off + v.size].view(v.shape)
+            d[k].copy_(torch.from_numpy(v))
+            off += v.size
+        clients.append(d)
+    s = AVG()
+    got = s.server(_upload(clients, g.weights()), 0)["w_glob"]
+    assert s.engine.packer.last_row_tables.get("f32") == "gather"
+    for k, w in g.output().items():
+        assert bitwise_equal(_host(got[k]), np.asarray(w)), k
+
+
+def _separate_tensors(stack, layout):
+    """Per-client dicts of separate device tensors (one allocation each), from a device stack."""
+    out = []
+    for i in range(stack.shape[0]):
+        d, off = {}, 0
+        for k, shape, t in layout:
+            if t != "f32":
+                continue
+            n = int(np.prod(shape, dtype=np.int64))
+            d[k] = stack[i, off : off + n].clone().view(shape)
+            off += -(-max(n, 1) // 64) * 64
+        out.append(d)
+    return out
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("layout_name,n,op", [("resnet18", 100, "mean"), ("resnet50", 24, "avgm"),
+                                              ("resnet18", 30, "adagrad")])
+def test_device_upload_baseline_size(layout_name, n, op, cuda):
+    """C2-size device uploads (100 x ResNet-18, 10,200 separate tensors) and fused optimizer
+    steps through the row-pointer kernel: bit-equal to the stack kernel on the same data."""
+    layout = layouts.get(layout_name)
+    stride = layouts.padded_f32_stride(layout)
+    x = torch.empty((n, stride), dtype=torch.float32, device=cuda)
+    agg.fill_uniform(x, seed=99)
+    clients = _separate_tensors(x, layout)
+    w = torch.ones(n, dtype=torch.float32, device=cuda)
+    want = torch.empty(stride, dtype=torch.float32, device=cuda)
+    kw, s = {}, AVG(output="float32")
+    if op != "mean":
+        prev = torch.empty((1, stride), dtype=torch.float32, device=cuda)
+        agg.fill_uniform(prev, seed=5)
+        kw = dict(op=na.OP_BY_NAME[op], prev=prev[0].clone(), v=torch.zeros(stride, dtype=torch.float64, device=cuda))
+        s = AVGM(server_side=True, output="float32") if op == "avgm" else OPT(server_side=True, method=op,
+                                                                              output="float32")
+        glob0 = {}
+        off = 0
+        ph = prev[0].cpu().numpy()
+        for k, shape, t in layout:
+            if t == "f32":
+                m = int(np.prod(shape, dtype=np.int64))
+                glob0[k] = ph[off : off + m].reshape(shape)
+                off += -(-max(m, 1) // 64) * 64
+        s.server_opt.init_global(glob0)
+    agg.reduce_stack(x, w, na.MODE_W32_DIV64, float(n), out32=want, **kw)
+    got = s.server(_upload(clients, [1.0] * n), 0)["w_glob"]
+    assert s.engine.packer.last_row_tables.get("f32") == "rows"
+    want_h = want.cpu().numpy()
+    off = 0
+    for k, shape, t in layout:
+        if t != "f32":
+            continue
+        m = int(np.prod(shape, dtype=np.int64))
+        assert bitwise_equal(np.asarray(got[k]).reshape(-1), want_h[off : off + m]), k
+        off += -(-max(m, 1) // 64) * 64
+
+
+@pytest.mark.parametrize("name", ["avgm_pyfloat_rounds3", "adagrad_np32_rounds3", "yogi_pyfloat_rounds3"])
+def test_fused_optimizer_device_uploads(name, cuda):
+    from golden_io import decode_weight, regenerate
+
+    g = Golden(name)
+    op = g.meta["op"]
+    s = AVGM(server_side=True) if op == "avgm" else OPT(server_side=True, method=op)
+    s.server_opt.init_global({k[6:]: v for k, v in g.arrays.items() if k.startswith("prev0:")})
+    layout = [(k, tuple(sh)) for k, sh in g.meta["gen"]["layout"]]
+    for r in range(g.meta["rounds"]):
+        clients = [_to_cuda(c, cuda) for c in regenerate(layout, 6, g.meta["gen"]["seeds"][r])]
+        weights = [decode_weight(e) for e in g.meta["round_weights"][r]]
+        got = s.server(_upload(clients, weights), r)["w_glob"]
+        assert s.engine.packer.last_row_tables.get("f32") == "rows"
+        for k, w in g.output(f"w{r}").items():
+            assert bitwise_equal(_host(got[k]), np.asarray(w)), (name, r, k)
+
+
+def test_dyn_device_uploads(cuda):
+    from golden_io import decode_weight
+
+    g = Golden("dyn_pyfloat_rounds3")
+    h = {k[6:]: v.copy() for k, v in g.arrays.items() if k.startswith("hinit:")}
+    d = Dyn(h)
+    keys = g.meta["client_keys"]
+    for r in range(g.meta["rounds"]):
+        clients = [_to_cuda({k: g.arrays[f"r{r}x{i}:{k}"].copy() for k in keys}, cuda) for i in range(g.meta["n_clients"])]
+        weights = [decode_weight(e) for e in g.meta["round_weights"][r]]
+        got = d.server(_upload(clients, weights), r)["w_glob"]
+        assert d.engine.packer.last_row_tables.get("f32") == "rows"
+        for k, w in g.output(f"w{r}").items():
+            assert bitwise_equal(_host(got[k]), np.asarray(w)), (r, k)
+        for k, w in g.output(f"h{r}").items():
+            assert bitwise_equal(_host(d.h[k]), np.asarray(w)), (r, k)
+
+
+def test_back_to_back_device_output_rounds_with_host_uploads(cuda):
+    """rounds queued back to back with output='device' (no host sync in between)
+    must not let round k+1's pack overwrite pinned staging that round k's H2D still reads."""
+    n, p = 24, 1_500_000
+    layout = [("w", (p,), "f32")]
+    s = AVG(output="device")
+    outs, wants = [], []
+    for r in range(4):
+        flat = oracle.fill_uniform(n, p, seed=1000 + r)
+        clients = [{"w": flat[i]} for i in range(n)]
+        outs.append(s.server(_upload(clients, [1.0] * n), r)["w_glob"]["w"])
+        wants.append(oracle.c_reduce(oracle.MODE_W32_DIV64, flat, np.ones(n, np.float32), float(n)).astype(np.float32))
+    torch.cuda.synchronize()
+    for r, (o, w) in enumerate(zip(outs, wants)):
+        assert bitwise_equal(o.cpu().numpy(), w), r
+    assert layout

@@ -313,3 +313,51 @@ def test_plan_cache_reuses_only_identical_metadata_and_weights():
     c = dict(a, w=torch.ones(2, 3))
     with pytest.raises(TypeError):
         make_plan([1.0, 2.0], [a, c])
+
+
+def test_device_output_is_one_copy_per_shard_and_views(monkeypatch):
+    """output="device" reassembly (aggregator.assemble_on_device), on CPU tensors standing in for
+    per-device shard outputs: one copy per (kind, shard) into one fresh buffer per kind, and every
+    key a view of that buffer at its segment offset."""
+    from flearn_amd.aggregator import assemble_on_device
+    from flearn_amd.bucket import split_columns
+
+    rng = np.random.default_rng(0)
+    shapes = {"conv.weight": (6, 1, 5, 5), "bn.weight": (6,), "fc.weight": (10, 84), "fc.bias": (10,),
+              "bn.num_batches_tracked": ()}
+    clients = []
+    for _ in range(3):
+        c = {k: rng.standard_normal(s).astype(np.float32) for k, s in shapes.items() if s}
+        c["bn.num_batches_tracked"] = np.array(7, dtype=np.int64)
+        clients.append(c)
+    plan = make_plan([1.0, 2.0, 3.0], clients)
+    f32 = plan.groups[KIND_F32]
+    full32 = torch.arange(f32.stride, dtype=torch.float32)
+    shards = split_columns(f32.stride, ["cpu", "cpu", "cpu"])
+    results = {KIND_F32: [(sh, full32[sh.c0 : sh.c1].clone()) for sh in shards]}
+    for kind in plan.groups:
+        if kind != KIND_F32:
+            st = plan.groups[kind].stride
+            results[kind] = [(split_columns(st, ["cpu"])[0], torch.full((st,), 5.0, dtype=torch.float64))]
+    copies = []
+    orig = torch.Tensor.copy_
+
+    def counting_copy(self, src, non_blocking=False):
+        copies.append((self.numel(), src.numel()))
+        return orig(self, src, non_blocking)
+
+    monkeypatch.setattr(torch.Tensor, "copy_", counting_copy)
+    glob = assemble_on_device(plan, results, "cpu")
+    assert len(copies) == len(shards) + len(plan.groups) - 1  # one per shard of every kind, no per-key copies
+    base = {kind: None for kind in plan.groups}
+    for k in plan.keys:
+        s = plan.key_segment[k]
+        t = glob[k]
+        assert tuple(t.shape) == tuple(s.shape)
+        kind = plan.key_group[k]
+        if kind == KIND_F32:
+            assert torch.equal(t.reshape(-1), full32[s.offset : s.offset + s.numel])
+        ptr = t.untyped_storage().data_ptr()
+        assert base[kind] in (None, ptr)  # all keys of a kind view one fresh buffer
+        base[kind] = ptr
+    assert base[KIND_F32] != full32.untyped_storage().data_ptr()

@@ -1,0 +1,45 @@
+// tune_rows.hip — geometry sweep of the row-pointer (device-upload) reduce; TOOL, not product.
+//
+// Built as tools/libtune_rows.so (hipcc, see tools/gpu_tune_rows.sh) and driven from Python
+// (tools/tune_rows.py) with piece tables built there: the product kernel
+// (fa_device.hpp reduce_kernel_segrows, dynamic piece claiming) at several V / D / W.
+// Earlier sweeps of this file (profiles/r02/tune_rows/) also held a column-major kernel with
+// the row pointers prefetched one refill ahead (no gain) and a row-major kernel over groups of
+// pieces (slower: one step in flight behind a pointer load).
+#include <hip/hip_runtime.h>
+
+#include "../flearn_amd/csrc/fa_device.hpp"
+
+namespace {
+using namespace fa;
+
+template <int V, int D, int W>
+int launch(const float* const* rows, int n, const float* w, const fa_piece* pieces, int64_t npieces, int grid,
+           int* work, const Epi<double>& e, hipStream_t s) {
+  if (hipMemsetAsync(work, 0, sizeof(int), s) != hipSuccess) return -3;
+  hipLaunchKernelGGL((reduce_kernel_segrows<AccF32, double, 0, V, D, W, true>), dim3((unsigned)grid), dim3(64 * W), 0, s,
+                     rows, n, w, pieces, npieces, work, e);
+  return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+}  // namespace
+
+// variant -> (V, D, W) of reduce_kernel_segrows; the piece width is chosen by the caller
+extern "C" int tune_rows_launch(int variant, const float* const* rows, int n, const float* w, const fa_piece* pieces,
+                                int64_t npieces, int grid, int* work, double denom, float* out32, void* stream) {
+  Epi<double> e{};
+  e.denom = denom;
+  e.out32 = out32;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  switch (variant) {
+    case 0: return launch<8, 2, 4>(rows, n, w, pieces, npieces, grid, work, e, s);
+    case 1: return launch<16, 1, 4>(rows, n, w, pieces, npieces, grid, work, e, s);
+    case 2: return launch<8, 1, 8>(rows, n, w, pieces, npieces, grid, work, e, s);
+    case 3: return launch<8, 2, 8>(rows, n, w, pieces, npieces, grid, work, e, s);
+    case 4: return launch<8, 4, 4>(rows, n, w, pieces, npieces, grid, work, e, s);
+    case 5: return launch<4, 4, 4>(rows, n, w, pieces, npieces, grid, work, e, s);
+    case 6: return launch<4, 2, 8>(rows, n, w, pieces, npieces, grid, work, e, s);
+    case 7: return launch<16, 2, 4>(rows, n, w, pieces, npieces, grid, work, e, s);
+    default: return -1;
+  }
+}
