@@ -32,6 +32,7 @@ EXPORTS = (
     "fa_abi_version",
     "fa_last_error",
     "fa_reduce_f32",
+    "fa_reduce_f32_splitn",
     "fa_reduce_f64",
     "fa_reduce_i64",
     "fa_opt_apply",
@@ -124,6 +125,8 @@ def load(require_gpu: bool = False):
                 "fa_last_error": ([], ctypes.c_char_p),
                 "fa_reduce_f32": ([P, I64, I32, I32, P, D, I64, I64, ctypes.POINTER(Epilogue), P, P, P],
                                   ctypes.c_int),
+                "fa_reduce_f32_splitn": ([P, I64, I32, I32, P, D, I64, I64, ctypes.POINTER(Epilogue), P, P, P],
+                                         ctypes.c_int),
                 "fa_reduce_f64": ([P, I64, I32, P, D, I64, I64, P, P], ctypes.c_int),
                 "fa_reduce_i64": ([P, I64, I32, P, D, I64, I64, P, P], ctypes.c_int),
                 "fa_opt_apply": ([I32, ctypes.POINTER(Epilogue), P, P, I64, P, P, P], ctypes.c_int),

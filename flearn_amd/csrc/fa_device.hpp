@@ -484,9 +484,9 @@ struct PtrRows {
 template <class P, int V, int D, int W, bool NT, class R>
 __device__ __forceinline__ void rows_sweep(const R& row, uint32_t bytes, int n,
                                            const typename P::w_t* __restrict__ w,
-                                           typename vec4<typename P::acc_t>::type (&acc)[V]) {
+                                           typename vec4<typename P::acc_t>::type (&acc)[V],
+                                           int voff = (int)threadIdx.x * 16) {
   typedef typename vec4<float>::type XV;
-  const int voff = (int)threadIdx.x * 16;
   XV x[D][V];
 #pragma unroll
   for (int d = 0; d < D; ++d)
@@ -655,6 +655,93 @@ __global__ __launch_bounds__(64 * W) void reduce_kernel_segrows(const float* con
     p = s_next;
     __syncthreads();  // s_next is rewritten in the next iteration
   }
+}
+
+// Split-N reduce (fa_reduce_f32_splitn) for windows too narrow to fill the chip with one
+// sequential sweep per column (LeNet5-sized models of many clients: 44 K columns x 1000 rows is
+// 174 one-KiB row chunks for 256 CUs, each walking 1000 rows).  Here the CLIENTS are split too:
+//   * a block owns one 1-KiB chunk of the window (64 quads) and W client splits: wave v sums the
+//     contiguous rows [v*n/W, (v+1)*n/W) in list order (the split's first product initialises its
+//     sum) through the row pipeline (rows_sweep, D rows in flight; the split index is made
+//     wave-uniform with readfirstlane so every row keeps ONE scalar buffer descriptor);
+//   * the W partial sums of a quad are staged in LDS and combined by a FIXED binary tree in
+//     split order, ((p0+p1)+(p2+p3))+..., one barrier per level;
+//   * then the epilogue of the row pipeline (divide, optional optimizer update, stores).
+// Deterministic (the tree does not depend on scheduling) but NOT the reference's sequential
+// order: opt-in, checked at <= 1e-6 normwise relative error per tensor (tests/test_gpu_splitn.py).
+// Needs n >= W (every split non-empty; the host falls back to the sequential kernel otherwise).
+template <class P, typename T, int OP, int W, int D, bool NT, bool STRIDED = false>
+__global__ __launch_bounds__(64 * W) void reduce_kernel_splitn(const float* __restrict__ stack, int64_t stride, int n,
+                                                               const typename P::w_t* __restrict__ w, int64_t col0,
+                                                               int64_t ncols, Epi<T> e) {
+  typedef typename P::acc_t A;
+  typedef typename vec4<A>::type AV;
+  __shared__ AV part[W][64];
+  const int lane = (int)threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);  // the split: wave-uniform
+  const int64_t qfull = ncols / 4;
+  const int64_t qb = (int64_t)blockIdx.x * 64;  // first quad of the chunk
+  const int64_t left = qfull - qb;
+  const int nq = left <= 0 ? 0 : (left < 64 ? (int)left : 64);
+  // split wv: contiguous rows [r0, r1), or (STRIDED) rows wv, wv+W, wv+2W, ... so that all
+  // splits read neighbouring rows at the same time
+  const int r0 = STRIDED ? wv : (int)((int64_t)wv * n / W);
+  const int r1 = STRIDED ? n : (int)((int64_t)(wv + 1) * n / W);
+  constexpr int RS = STRIDED ? W : 1;  // row step of a split
+  AV acc = {A(0), A(0), A(0), A(0)};
+  if (nq > 0) {
+    // this split's rows through a D-deep rolling pipeline with NO guarded loads: a slot past the
+    // split's end re-reads its last row (a cache hit) and the product is discarded by a select,
+    // so the loads stay unconditional and the ramp is not serialised by waitcnt merges
+    typedef typename vec4<float>::type XV;
+    const char* tile0 = reinterpret_cast<const char*>(stack + col0 + qb * 4) + (int64_t)r0 * stride * 4;
+    const int64_t row_bytes = stride * 4 * RS;
+    const uint32_t bytes = (uint32_t)nq * 16u;
+    const int voff = lane * 16;
+    const int cnt = (r1 - r0 + RS - 1) / RS;  // >= 1
+    const typename P::w_t* ws = w + r0;
+    XV x[D];
+#pragma unroll
+    for (int d = 0; d < D; ++d)
+      x[d] = buf_load_quad<NT>(row_rsrc(tile0 + (int64_t)(d < cnt ? d : cnt - 1) * row_bytes, bytes), voff, 0);
+    acc = quad_mul<P>(ws[0], x[0]);
+    {
+      const int r = D < cnt ? D : cnt - 1;
+      x[0] = buf_load_quad<NT>(row_rsrc(tile0 + (int64_t)r * row_bytes, bytes), voff, 0);
+    }
+#pragma unroll
+    for (int d = 1; d < D; ++d) {  // rows 1..D-1
+      const AV t = quad_axpy<P>(acc, ws[(d < cnt ? d : 0) * RS], x[d]);
+      acc = d < cnt ? t : acc;
+      __builtin_amdgcn_sched_barrier(0);
+      const int r = d + D < cnt ? d + D : cnt - 1;
+      x[d] = buf_load_quad<NT>(row_rsrc(tile0 + (int64_t)r * row_bytes, bytes), voff, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    for (int base = D; base < cnt; base += D) {
+#pragma unroll
+      for (int d = 0; d < D; ++d) {
+        const int i = base + d;
+        const AV t = quad_axpy<P>(acc, ws[(i < cnt ? i : 0) * RS], x[d]);
+        acc = i < cnt ? t : acc;
+        __builtin_amdgcn_sched_barrier(0);
+        const int r = i + D < cnt ? i + D : cnt - 1;
+        x[d] = buf_load_quad<NT>(row_rsrc(tile0 + (int64_t)r * row_bytes, bytes), voff, 0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  }
+  part[wv][lane] = acc;
+  __syncthreads();
+#pragma unroll
+  for (int h = 1; h < W; h *= 2) {  // fixed tree over the splits, one level per barrier
+    if ((wv % (2 * h)) == 0 && wv + h < W) part[wv][lane] = part[wv][lane] + part[wv + h][lane];
+    __syncthreads();
+  }
+  if (wv == 0 && lane < nq) finish_quad<T, OP, A>(e, (qb + lane) * 4, 4, part[0][lane]);
+  // the window's ragged last quad (ncols % 4 != 0): the sequential path, in the chunk that holds it
+  if (threadIdx.x == 0 && qfull * 4 < ncols && qfull >= qb && qfull < qb + 64)
+    reduce_ragged<P, T, OP>(stack + col0, stride, n, w, qfull, qfull + 1, ncols, e);
 }
 
 // fa_gather_rows: block (s, i) copies client i's tensor of segment s into its stack row.

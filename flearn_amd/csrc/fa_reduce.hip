@@ -228,6 +228,35 @@ int dispatch_segrows(int op, const float* const* rows, int n, const void* w, con
   }
 }
 
+// Split-N geometry (tools/tune_splitn.py): one 1-KiB chunk of every row per block, kSplitW client
+// splits (one per wave), each a rolling pipeline kSplitD rows deep.
+constexpr int kSplitW = 8, kSplitD = 8;
+constexpr int kSplitS = kSplitW;
+
+template <class P, typename T, int OP>
+int launch_splitn(const float* stack, int64_t stride, int n, const void* w, int64_t col0, int64_t ncols,
+                  const Epi<T>& e, hipStream_t s) {
+  if (n < 2 * kSplitS) return launch_reduce<P, T, OP>(stack, stride, n, w, col0, ncols, e, s);  // nothing to split
+  const int64_t chunks = ((ncols + 3) / 4 + 63) / 64;
+  hipLaunchKernelGGL((reduce_kernel_splitn<P, T, OP, kSplitW, kSplitD, kNT>), dim3((unsigned)chunks),
+                     dim3(64 * kSplitW), 0, s, stack, stride, n, static_cast<const typename P::w_t*>(w), col0, ncols, e);
+  return launch_check();
+}
+
+template <class P, typename T>
+int dispatch_splitn(int op, const float* stack, int64_t stride, int n, const void* w, int64_t col0, int64_t ncols,
+                    const Epi<T>& e, hipStream_t s) {
+  switch (op) {
+    case FA_OP_MEAN: return launch_splitn<P, T, FA_OP_MEAN>(stack, stride, n, w, col0, ncols, e, s);
+    case FA_OP_AVGM: return launch_splitn<P, T, FA_OP_AVGM>(stack, stride, n, w, col0, ncols, e, s);
+    case FA_OP_ADAGRAD: return launch_splitn<P, T, FA_OP_ADAGRAD>(stack, stride, n, w, col0, ncols, e, s);
+    case FA_OP_YOGI: return launch_splitn<P, T, FA_OP_YOGI>(stack, stride, n, w, col0, ncols, e, s);
+    case FA_OP_ADAM: return launch_splitn<P, T, FA_OP_ADAM>(stack, stride, n, w, col0, ncols, e, s);
+    case FA_OP_DYN: return launch_splitn<P, T, FA_OP_DYN>(stack, stride, n, w, col0, ncols, e, s);
+    default: return fail(FA_ERR_ARG, "unknown epilogue op");
+  }
+}
+
 template <class P, typename T>
 int dispatch_op(int op, const typename P::x_t* stack, int64_t stride, int n, const void* w,
                 int64_t col0, int64_t ncols, const Epi<T>& e, hipStream_t s) {
@@ -336,6 +365,35 @@ int fa_reduce_f32(const float* stack, int64_t row_stride, int32_t n_clients, int
     if ((rc = make_epi<double>(epi, denom, n_clients, out32, out64, &e))) return rc;
     return dispatch_op<AccF32W64, double>(op, stack, row_stride, n_clients, weights, col_begin,
                                           n_cols, e, s);
+  }
+  return fail(FA_ERR_ARG, "unknown reduce mode");
+}
+
+int fa_reduce_f32_splitn(const float* stack, int64_t row_stride, int32_t n_clients, int32_t mode,
+                         const void* weights, double denom, int64_t col_begin, int64_t n_cols,
+                         const fa_epilogue* epi, float* out32, double* out64, void* stream) {
+  int rc = check_common(stack, row_stride, n_clients, weights, col_begin, n_cols, out32, out64);
+  if (rc) return rc;
+  if (n_cols == 0) return FA_OK;
+  const int op = epi ? epi->op : FA_OP_MEAN;
+  if ((rc = check_columns(out32, out64, epi ? epi->prev : nullptr, epi ? epi->v : nullptr,
+                          mode == FA_MODE_W32_DIV32 ? sizeof(float) : sizeof(double), epi ? epi->h : nullptr)))
+    return rc;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (mode == FA_MODE_W32_DIV64) {
+    Epi<double> e;
+    if ((rc = make_epi<double>(epi, denom, n_clients, out32, out64, &e))) return rc;
+    return dispatch_splitn<AccF32, double>(op, stack, row_stride, n_clients, weights, col_begin, n_cols, e, s);
+  }
+  if (mode == FA_MODE_W32_DIV32) {
+    Epi<float> e;
+    if ((rc = make_epi<float>(epi, denom, n_clients, out32, out64, &e))) return rc;
+    return dispatch_splitn<AccF32, float>(op, stack, row_stride, n_clients, weights, col_begin, n_cols, e, s);
+  }
+  if (mode == FA_MODE_W64) {
+    Epi<double> e;
+    if ((rc = make_epi<double>(epi, denom, n_clients, out32, out64, &e))) return rc;
+    return dispatch_splitn<AccF32W64, double>(op, stack, row_stride, n_clients, weights, col_begin, n_cols, e, s);
   }
   return fail(FA_ERR_ARG, "unknown reduce mode");
 }

@@ -14,7 +14,6 @@ import torch
 
 from .. import _native as na
 from ..bucket import ALIGN
-from .utils import _ERR
 
 _FMT = {np.dtype(np.float32): ord("f"), np.dtype(np.float64): ord("d")}
 _PART_BYTES = 16 << 20  # host copies are split into parts of about this size, one per pool task
@@ -80,6 +79,7 @@ class DeviceUpdater:
         self.params = dict(beta=beta, eta=eta, tau=tau, beta2=beta2)
         self.layout = None  # [(key, shape, offset, numel)]
         self.v = None
+        self.v_host = {}  # v_t of the keys computed on the host (integer buffers, scalars)
         self._stage = None  # pinned staging of the current layout (local, global, result)
 
     def _layout(self, w_glob):
@@ -92,40 +92,84 @@ class DeviceUpdater:
         return lay, off
 
     def reset(self):
-        self.layout, self.v, self._stage = None, None, None
+        """Forget v_t (device and host keys): the next call starts from zeros, as a fresh
+        strategy object would."""
+        self.layout, self.v, self._stage, self.v_host = None, None, None, {}
 
     def state(self):
         """v_t as the reference exposes it: {key: ndarray}."""
-        if self.v is None:
-            return {}
-        host = self.v.cpu().numpy()
-        return {k: host[o : o + n].reshape(s).copy() for k, s, o, n in self.layout}
+        out = {}
+        if self.v is not None:
+            host = self.v.cpu().numpy()
+            out = {k: host[o : o + n].reshape(s).copy() for k, s, o, n in self.layout}
+        out.update(self.v_host)
+        return out
 
     def __call__(self, w_local, w_glob, **override):
         na.lib()
-        glob = {}
+        glob, local, host_keys = {}, {}, []
         for k, g in w_glob.items():
             if isinstance(g, torch.Tensor):
                 g = g.detach().cpu().numpy()
-            if not isinstance(g, np.ndarray):
-                raise SystemError(_ERR, type(g))
-            glob[k] = g
-        dts = {g.dtype for g in glob.values()}
-        if len(dts) != 1 or dts.pop() not in (np.float64, np.float32):
-            raise TypeError("w_glob values must all be float64 (or all float32) arrays")
-        gdt = next(iter(glob.values())).dtype
-        local = {}
-        for k in glob:
             lv = w_local[k]
             if isinstance(lv, torch.Tensor):
                 lv = lv.detach().cpu().numpy()
-            if not isinstance(lv, np.ndarray) or lv.dtype != np.float32 or lv.shape != glob[k].shape:
-                raise TypeError(f"w_local[{k!r}] must be an fp32 array shaped like w_glob[{k!r}]")
-            local[k] = lv
+            # the device handles fp32 parameters against a float64 / float32 global model; anything
+            # else (BN num_batches_tracked: int64 local, numpy-scalar global) takes the reference's
+            # numpy ops on the host, key by key, as avgm.py / opt.py compute them
+            if (isinstance(g, np.ndarray) and g.ndim >= 1 and g.dtype in (np.float64, np.float32)
+                    and isinstance(lv, np.ndarray) and lv.dtype == np.float32 and lv.shape == g.shape):
+                glob[k], local[k] = g, lv
+            else:
+                host_keys.append(k)
+        if glob:
+            gdt = next(iter(glob.values())).dtype
+            for k in [k for k, g in glob.items() if g.dtype != gdt]:  # one device precision per call
+                host_keys.append(k)
+                del glob[k], local[k]
+            self._device_step(w_local, glob, local, gdt, **override)
+        if host_keys:
+            self._host_step(w_local, w_glob, host_keys, **override)
+        return w_local
+
+    def _host_step(self, w_local, w_glob, keys, **override):
+        """The reference's per-key numpy arithmetic (avgm.py:19-36 / opt.py:23-65) for the keys the
+        device path does not take; their v_t lives on the host (np.zeros_like(delta) first)."""
+        p = dict(self.params, **override)
+        vh = self.v_host
+        for k in keys:
+            lv = w_local[k]
+            if isinstance(lv, torch.Tensor):
+                lv = lv.detach().cpu().numpy()
+            g = w_glob[k]
+            if isinstance(g, torch.Tensor):
+                g = g.detach().cpu().numpy()
+            delta = g - lv
+            v = vh.get(k)
+            if v is None:
+                v = np.zeros_like(delta)
+            if self.op == na.OP_AVGM:
+                v = delta + p["beta"] * v
+                w_local[k] = lv + v
+            else:
+                sq = np.multiply(delta, delta)
+                if self.op == na.OP_ADAGRAD:
+                    v = v + sq
+                elif self.op == na.OP_YOGI:
+                    v = v - (1 - p["beta2"]) * sq * np.sign(v - sq)
+                else:
+                    v = p["beta2"] * v + (1 - p["beta2"]) * sq
+                w_local[k] = lv + p["eta"] * delta / (np.sqrt(v) + p["tau"])
+            vh[k] = v
+
+    def _device_step(self, w_local, glob, local, gdt, **override):
         lay, total = self._layout(glob)
         dev = torch.device(self.device) if self.device is not None else torch.device("cuda", torch.cuda.current_device())
         tdt = torch.float64 if gdt == np.float64 else torch.float32
-        if self.layout != lay or self.v is None or self.v.dtype != tdt:
+        if self.v is not None and (self.layout != lay or self.v.dtype != tdt):
+            raise ValueError("the model layout or w_glob's dtype changed between rounds: v_t no longer matches; "
+                             "call reset() to start the optimizer state afresh")
+        if self.v is None:
             self.layout = lay
             self.v = torch.zeros(total, dtype=tdt, device=dev)  # np.zeros_like(delta) on first use
             self._stage = None
@@ -156,7 +200,6 @@ class DeviceUpdater:
         _run([(lambda a=a: np.copyto(fresh[a : a + step], src[a : a + step])) for a in range(0, total, step)])
         for k, s, o, n in lay:  # replaced per key, like the reference (avgm.py:34-35, opt.py:62-63)
             w_local[k] = fresh[o : o + n].reshape(s)
-        return w_local
 
     def _staging(self, lay, total, tdt, dev):
         """Pinned staging for this layout, reused across calls (zeroed once: only the segments

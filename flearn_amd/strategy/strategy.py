@@ -90,9 +90,12 @@ class Strategy(ABC):
         agg_weight_lst, w_local_lst = self.server_pre_processing(ensemble_params_lst)
         try:
             return self.server_ensemble(agg_weight_lst, w_local_lst, key_lst=key_lst, server_opt=server_opt)
-        except NativeUnavailable:
-            raise  # an environment problem, not bad client data: never masked
-        except Exception as e:  # the reference's convention (avg.py:28-31)
+        except RuntimeError:
+            # NativeUnavailable / NativeError (a failed launch), torch.OutOfMemoryError, HIP runtime
+            # errors: a device or environment problem, not bad client data — never turned into
+            # the "check that the client model parameters are valid" exit
+            raise
+        except Exception as e:  # the reference's convention (avg.py:28-31) for what numpy would raise
             self.server_exception(e)
 
     @abstractmethod

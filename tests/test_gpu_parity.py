@@ -892,3 +892,41 @@ def test_client_side_update_large_and_fallback_values(op, cuda):
         prev = {k: np.asarray(got[k]).astype(np.float32) for k in shapes}
         if r == 0:
             prev["c"] = np.asfortranarray(prev["c"])
+
+
+@pytest.mark.parametrize("op", ["avgm", "adagrad", "adam"])
+def test_client_side_update_bn_model(op, cuda):
+    """A BatchNorm model: the server's w_glob holds np.float64 scalars for the int64
+    num_batches_tracked counters and the client's state_dict int64 0-d arrays.  The fp32 keys run
+    on the device, the counters through the reference's numpy ops on the host; all keys and the
+    state equal the numpy restatement over 3 rounds."""
+    g = Golden("avg_bnmodel_pyfloat_n4")
+    prev = {k: np.asarray(v).copy() for k, v in g.clients()[0].items()}
+    s = AVGM() if op == "avgm" else OPT()
+    v = None
+    glob = g.output()
+    for r in range(3):
+        if op == "avgm":
+            want, v = oracle.mean_momentum(dict(prev), glob, v, 0.9)
+            got = s.mean_momentum(dict(prev), glob, 0.9)
+        else:
+            want, v = oracle.adaptive_opt(dict(prev), glob, v, op)
+            got = s.adaptive_opt(dict(prev), glob, op)
+        assert set(got) == set(want)
+        for k in want:
+            assert type(got[k]) is type(want[k]), (k, type(got[k]), type(want[k]))
+        assert_dict_bitwise(got, want, f"{op} w{r}")
+        assert_dict_bitwise(s.v_t, v, f"{op} v{r}")
+        prev = {k: (np.asarray(got[k]).astype(np.float32) if np.asarray(got[k]).dtype == np.float64 and
+                    np.ndim(got[k]) else prev[k]) for k in prev}
+        glob = {k: (val * 1.01 if np.ndim(val) else val) for k, val in glob.items()}
+
+
+def test_client_side_update_refuses_a_changed_layout(cuda):
+    s = AVGM()
+    a = {"w": np.ones(10, np.float32)}
+    s.mean_momentum(dict(a), {"w": np.zeros(10)}, 0.9)
+    with pytest.raises(ValueError, match="reset"):
+        s.mean_momentum({"w": np.ones(12, np.float32)}, {"w": np.zeros(12)}, 0.9)
+    s._updater.reset()
+    s.mean_momentum({"w": np.ones(12, np.float32)}, {"w": np.zeros(12)}, 0.9)

@@ -43,3 +43,39 @@ extern "C" int tune_rows_launch(int variant, const float* const* rows, int n, co
     default: return -1;
   }
 }
+
+// split-N variants (fa_device.hpp reduce_kernel_splitn<W, D>) on a [n, stride] stack
+namespace {
+template <int W, int D, bool ST = false>
+int launch_sn(const float* stack, int64_t stride, int n, const float* w, int64_t ncols, const Epi<double>& e,
+              hipStream_t s) {
+  const int64_t chunks = ((ncols + 3) / 4 + 63) / 64;
+  hipLaunchKernelGGL((reduce_kernel_splitn<AccF32, double, 0, W, D, true, ST>), dim3((unsigned)chunks), dim3(64 * W), 0,
+                     s, stack, stride, n, w, (int64_t)0, ncols, e);
+  return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+}  // namespace
+
+extern "C" int tune_splitn_launch(int variant, const float* stack, int64_t stride, int n, const float* w, int64_t ncols,
+                                  double denom, float* out32, void* stream) {
+  Epi<double> e{};
+  e.denom = denom;
+  e.out32 = out32;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  switch (variant) {
+    case 0: return launch_sn<4, 8>(stack, stride, n, w, ncols, e, s);
+    case 1: return launch_sn<4, 16>(stack, stride, n, w, ncols, e, s);
+    case 2: return launch_sn<8, 8>(stack, stride, n, w, ncols, e, s);
+    case 3: return launch_sn<8, 16>(stack, stride, n, w, ncols, e, s);
+    case 4: return launch_sn<16, 8>(stack, stride, n, w, ncols, e, s);
+    case 5: return launch_sn<16, 4>(stack, stride, n, w, ncols, e, s);
+    case 6: return launch_sn<2, 16>(stack, stride, n, w, ncols, e, s);
+    case 7: return launch_sn<16, 16>(stack, stride, n, w, ncols, e, s);
+    case 8: return launch_sn<4, 8, true>(stack, stride, n, w, ncols, e, s);
+    case 9: return launch_sn<8, 8, true>(stack, stride, n, w, ncols, e, s);
+    case 10: return launch_sn<16, 8, true>(stack, stride, n, w, ncols, e, s);
+    case 11: return launch_sn<8, 16, true>(stack, stride, n, w, ncols, e, s);
+    case 12: return launch_sn<16, 4, true>(stack, stride, n, w, ncols, e, s);
+    default: return -1;
+  }
+}
