@@ -148,6 +148,8 @@ def main():
                     help="single process: time rank 0's reduce of a G-GPU job (no gather)")
     ap.add_argument("--cpu-sample", type=int, default=None, help="clients in the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--reorder", action="store_true",
+                    help="allow the split-N kernel (deterministic, <= 1e-6 normwise, not bit-exact)")
     args = ap.parse_args()
 
     # one process per GPU: with no launcher env, --gpus N > 1 starts the N ranks here, BEFORE any
@@ -204,7 +206,7 @@ def main():
         v = torch.zeros(cols, dtype=torch.float64, device=dev)
         epi = dict(op=na.OP_BY_NAME[cfg["op"]], prev=prev, v=v)
         local_out = prev  # the fused step advances the global model in place
-    fn = hip_reduce_fn(stack, weights, na.MODE_W32_DIV64, denom, **epi)
+    fn = hip_reduce_fn(stack, weights, na.MODE_W32_DIV64, denom, reorder=args.reorder, **epi)
     red = ShardedReducer(plan, fn, dev, local_out=local_out, gather=world > 1)
 
     # ---- warmup + timed steps ----
@@ -294,6 +296,8 @@ def main():
                 "params": p_real,
                 "layout": cfg["layout"],
                 "epilogue": cfg["op"],
+                "order": ("split-N allowed (fixed-order tree of client splits, <= 1e-6 normwise)" if args.reorder
+                          else "reference client order (bit-exact)"),
                 "parallelism": ("single GPU" if g_eff == 1 else
                                 f"element-range shards x{g_eff} + RCCL all-gather ({stripes} stripes"
                                 + (f", widths {'/'.join(str(x) for x in plan.widths)}" if stripes > 1 else "") + ")"

@@ -70,11 +70,15 @@ def reduce_stack(
     beta2: float = 0.99,
     h: torch.Tensor | None = None,
     alpha: float = 0.01,
+    reorder: bool = False,
 ) -> None:
     """Weighted mean of the fp32 client stack [N, stride] over columns [col_begin, +n_cols)
     (+ fused update), queued on torch's current stream.  out32/out64/prev/v/h are indexed from
     col_begin.  weights: fp32 for MODE_W32_*, f64 for MODE_W64 (device tensors).
-    op=OP_DYN: FedDyn with h (fp32, in place) and v = theta (in place); prev unused."""
+    op=OP_DYN: FedDyn with h (fp32, in place) and v = theta (in place); prev unused.
+    reorder=True: allow fa_reduce_f32_splitn (client splits + a fixed tree: deterministic, within
+    1e-6 normwise of the reference, not bit-exact) where it is faster — narrow windows, many
+    clients; stack input only."""
     L = na.lib()
     rows = isinstance(stack, RowTable)  # device uploads read in place (fa_reduce_f32_rows)
     if rows:
@@ -129,12 +133,13 @@ def reduce_stack(
         na.check(rc, "fa_reduce_f32_rows")
         stack.release()
         return
-    rc = L.fa_reduce_f32(
+    fn = L.fa_reduce_f32_splitn if reorder else L.fa_reduce_f32
+    rc = fn(
         stack.data_ptr(), stack.stride(0), n, mode, weights.data_ptr(), float(denom), col_begin, ncols,
         ctypes.byref(epi) if epi is not None else None, _ptr(out32), _ptr(out64),
         na.stream_handle(stack.device),
     )
-    na.check(rc, "fa_reduce_f32")
+    na.check(rc, "fa_reduce_f32_splitn" if reorder else "fa_reduce_f32")
 
 
 def reduce_stack_f64(stack, weights, denom, out64, n_clients=None):
@@ -510,16 +515,34 @@ class Aggregator:
     devices: the HIP devices the f32 bucket is split over (column shards); each ingests its
     columns through its own PCIe link.  Default: torch's current device only."""
 
-    def __init__(self, device=None, output: str = "reference", workers: int = 8, devices=None):
+    def __init__(self, device=None, output: str = "reference", workers: int = 8, devices=None, group=None,
+                 reorder: bool = False):
         na.lib()  # fail loudly right away if the HIP path is unavailable
         if output not in OUTPUTS:
             raise ValueError(f"output must be one of {OUTPUTS}")
+        if group is not None and devices is not None and len(devices) > 1:
+            raise ValueError("group (one GPU per process) and devices (several GPUs in this process) exclude each other")
         if devices is None:
             devices = [torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())]
         self.devices = [torch.device(d) for d in devices]
         self.device = self.devices[0]
         self.output = output
+        self.reorder = reorder  # allow the split-N kernel (not bit-exact; <= 1e-6 normwise)
         self.packer = Packer(self.devices, workers)
+        # group: this process is one rank of a column-sharded aggregation (flearn_amd.dist): it
+        # packs and reduces only its columns of the fp32 bucket and an RCCL all-gather over xGMI
+        # reassembles the global model on every rank.  True = the default process group.
+        self.group = None
+        if group is not None:
+            import torch.distributed as dist
+
+            self.group = None if group is True else group
+            if not dist.is_initialized():
+                raise RuntimeError("group= needs torch.distributed initialised (one process per GPU)")
+            self.packer.rank_cols = (dist.get_rank(self.group), dist.get_world_size(self.group))
+            self._dist = True
+        else:
+            self._dist = False
         self.last_plan: BucketPlan | None = None
         self._wcache = {}  # (device, dtype, bytes) -> device weights: a pageable H2D per round saved
 
@@ -557,7 +580,20 @@ class Aggregator:
             results[kind] = res
         if server_opt is not None and first_means:
             server_opt.adopt(plan, [sh for sh, _ in stacks[KIND_F32]], first_means)
+        if self._dist and KIND_F32 in results:
+            results[KIND_F32] = self._gather_columns(plan, results[KIND_F32])
         return self._finish(plan, results)
+
+    def _gather_columns(self, plan: BucketPlan, parts):
+        """Column-sharded group: every rank's reduced columns -> the whole f32 bucket on every
+        rank, one all_gather_into_tensor (RCCL over xGMI; equal padded widths)."""
+        from .bucket import Shard, rank_width
+        from .dist import gather_columns
+
+        (sh, out), = parts
+        stride = plan.groups[KIND_F32].stride
+        full = gather_columns(out[: sh.width], rank_width(stride, self.packer.rank_cols[1]), stride, self.group)
+        return [(Shard(0, self.device, 0, stride), full)]
 
     def _reduce_f32(self, g, sh, stack, w, server_opt, fused, first_means):
         nm = g.numerics
@@ -565,17 +601,24 @@ class Aggregator:
         out64 = (self.packer.device_bucket(("out64", KIND_F32, sh.index), (sh.width,), torch.float64, sh.device)
                  if want64 else None)
         if isinstance(server_opt, DynState):
+            if self._dist:
+                raise NotImplementedError("FedDyn with a column-sharded process group (h would need a gather)")
             return server_opt.step(self, sh, stack, w, nm, want64)
+        if sh.width == 0:  # a rank whose column range is empty (tiny model, many ranks)
+            dt = torch.float64 if want64 else torch.float32
+            return torch.empty(0, dtype=dt, device=sh.device)
         if server_opt is not None and fused:
             # fused: prev is updated in place to fl32(w) — the model clients load next round
             prev, v = server_opt.state[sh.index]
             reduce_stack(stack, w, nm.mode, nm.denom, out32=prev, out64=out64, op=server_opt.op, prev=prev, v=v,
-                         beta=server_opt.beta, eta=server_opt.eta, tau=server_opt.tau, beta2=server_opt.beta2)
+                         beta=server_opt.beta, eta=server_opt.eta, tau=server_opt.tau, beta2=server_opt.beta2,
+                         reorder=self.reorder and not isinstance(stack, RowTable))
             return out64 if want64 else prev
         out32 = None
         if not want64 or server_opt is not None:
             out32 = self.packer.device_bucket(("out32", KIND_F32, sh.index), (sh.width,), torch.float32, sh.device)
-        reduce_stack(stack, w, nm.mode, nm.denom, out32=out32, out64=out64)
+        reduce_stack(stack, w, nm.mode, nm.denom, out32=out32, out64=out64,
+                     reorder=self.reorder and not isinstance(stack, RowTable))
         if server_opt is not None:
             first_means[sh.index] = out32
         return out64 if want64 else out32

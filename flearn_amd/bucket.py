@@ -246,6 +246,12 @@ class Shard:
         return self.c1 - self.c0
 
 
+def rank_width(stride: int, world: int) -> int:
+    """Columns per rank of a column-sharded process group: equal, ALIGN-aligned (the last ranks'
+    ranges may be short or empty; the all-gather pads them)."""
+    return -(-stride // (world * ALIGN)) * ALIGN
+
+
 def split_columns(stride: int, devices) -> list:
     """Near-equal ALIGN-aligned column ranges of a stride-wide bucket, one per device."""
     k = len(devices)
@@ -274,6 +280,7 @@ class Packer:
         self.last_wire_rows = 0
         self.last_wire_staged = 0
         self.last_row_tables = {}  # kind -> "rows" | "gather" | "copy" for device-resident uploads
+        self.rank_cols = None  # (rank, world): pack only this rank's columns of the f32 bucket
 
     def _executor(self) -> concurrent.futures.ThreadPoolExecutor:
         """One persistent pool per Packer: creating threads per call costs ~0.3 ms, which is the
@@ -307,9 +314,15 @@ class Packer:
         g = plan.groups[kind]
         if kind != KIND_F32:
             return [Shard(0, self.device, 0, g.stride)]
-        key = (g.stride, tuple(str(d) for d in self.devices))
+        key = (g.stride, tuple(str(d) for d in self.devices), self.rank_cols)
         if key not in self._shards:
-            self._shards[key] = split_columns(g.stride, self.devices)
+            if self.rank_cols is not None:  # one rank of a column-sharded process group
+                rank, world = self.rank_cols
+                w = rank_width(g.stride, world)
+                c0 = min(rank * w, g.stride)
+                self._shards[key] = [Shard(0, self.device, c0, min(c0 + w, g.stride))]
+            else:
+                self._shards[key] = split_columns(g.stride, self.devices)
         return self._shards[key]
 
     @staticmethod
@@ -382,8 +395,8 @@ class Packer:
 
     def row_table(self, plan: BucketPlan, g: Group, w_local_lst, shards):
         """RowTable of device-resident uploads for bucket group g, or None when some value is
-        not a contiguous tensor of its dtype on the bucket's (single) device."""
-        if len(shards) != 1:
+        not a contiguous tensor of its dtype on the bucket's (single, whole-bucket) device."""
+        if len(shards) != 1 or shards[0].c0 != 0 or shards[0].c1 != g.stride:
             return None
         dev = shards[0].device
         dt = _TORCH[g.store_dtype]

@@ -583,29 +583,6 @@ __device__ __forceinline__ void rows_piece(const float* __restrict__ stack, int6
     reduce_ragged<P, T, OP>(stack + col0, stride, n, w, qfull, qfull + 1, ncols, e);
 }
 
-// A segment's ragged last quad (1-3 elements) read through the row-pointer table.
-template <class P, typename T, int OP>
-__device__ __attribute__((noinline)) void reduce_ragged_ptr(const float* const* __restrict__ rp,
-                                                            int64_t off, int n,
-                                                            const typename P::w_t* __restrict__ w,
-                                                            int64_t col, int valid, const Epi<T>& e) {
-  typedef typename P::acc_t A;
-  typename vec4<A>::type acc;
-  {
-    const typename vec4<float>::type x = load_quad_guarded(rp[0] + off, valid);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[j] = P::mul(w[0], x[j]);
-  }
-#pragma unroll 1
-  for (int i = 1; i < n; ++i) {
-    const typename vec4<float>::type x = load_quad_guarded(rp[i] + off, valid);
-    const typename P::w_t wi = w[i];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[j] = add<A>(acc[j], P::mul(wi, x[j]));
-  }
-  finish_quad<T, OP, A>(e, col, valid, acc);
-}
-
 // Segmented row-pointer reduce (fa_reduce_f32_rows): uploads that are separate device tensors
 // per (client, key) are read where they lie — no pack copy.  Work = pieces (fa_rows_plan): each
 // is a column range of ONE segment, so every row of a piece is one contiguous range of one
@@ -633,23 +610,25 @@ __global__ __launch_bounds__(64 * W) void reduce_kernel_segrows(const float* con
     if (threadIdx.x == 0) claimed = (int)gridDim.x + atomicAdd(next, 1);
     const fa_piece pc = pieces[p];
     const float* const* rp = rows + (int64_t)pc.seg * n;
-    const int nq = pc.n_cols >> 2;
+    // a segment's ragged last quad rides in the vector path: the range check is per dword
+    // (`bytes` = exactly the piece's columns), its missing elements load as 0 and are not stored
+    const int nq = (pc.n_cols + 3) >> 2;
+    const uint32_t bytes = (uint32_t)pc.n_cols * 4u;
     const PtrRows row{rp, pc.seg_off * 4};
     if (nq > 64 * W) {
       AV acc[V];
-      rows_sweep<P, V, D, W, NT>(row, (uint32_t)nq * 16u, n, w, acc);
+      rows_sweep<P, V, D, W, NT>(row, bytes, n, w, acc);
 #pragma unroll
       for (int v = 0; v < V; ++v) {
         const int q = v * 64 * W + (int)threadIdx.x;
-        if (q < nq) finish_quad<T, OP, A>(e, pc.col + (int64_t)q * 4, 4, acc[v]);
+        if (q < nq) finish_quad<T, OP, A>(e, pc.col + (int64_t)q * 4, pc.n_cols - q * 4 < 4 ? pc.n_cols - q * 4 : 4, acc[v]);
       }
     } else if (nq > 0) {
       AV acc[1];
-      rows_sweep<P, 1, V * D, W, NT>(row, (uint32_t)nq * 16u, n, w, acc);
-      if ((int)threadIdx.x < nq) finish_quad<T, OP, A>(e, pc.col + (int64_t)threadIdx.x * 4, 4, acc[0]);
+      rows_sweep<P, 1, V * D, W, NT>(row, bytes, n, w, acc);
+      const int q = (int)threadIdx.x;
+      if (q < nq) finish_quad<T, OP, A>(e, pc.col + (int64_t)q * 4, pc.n_cols - q * 4 < 4 ? pc.n_cols - q * 4 : 4, acc[0]);
     }
-    if ((pc.n_cols & 3) && threadIdx.x == 0)
-      reduce_ragged_ptr<P, T, OP>(rp, pc.seg_off + (int64_t)nq * 4, n, w, pc.col + (int64_t)nq * 4, pc.n_cols & 3, e);
     if (threadIdx.x == 0) s_next = claimed;
     __syncthreads();
     p = s_next;
@@ -679,10 +658,13 @@ __global__ __launch_bounds__(64 * W) void reduce_kernel_splitn(const float* __re
   __shared__ AV part[W][64];
   const int lane = (int)threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);  // the split: wave-uniform
-  const int64_t qfull = ncols / 4;
+  // the chunk's columns, its last quad possibly partial: the raw buffer range check is per dword
+  // on gfx950 (tools/probe_oob.py, profiles/r02/oob.json), so `bytes` = exactly the chunk's
+  // columns and the missing elements of a ragged last quad load as 0 and are never stored
   const int64_t qb = (int64_t)blockIdx.x * 64;  // first quad of the chunk
-  const int64_t left = qfull - qb;
-  const int nq = left <= 0 ? 0 : (left < 64 ? (int)left : 64);
+  const int64_t cleft = ncols - qb * 4;
+  const int tcols = cleft <= 0 ? 0 : (cleft < 256 ? (int)cleft : 256);
+  const int nq = (tcols + 3) / 4;  // quads, the last possibly partial
   // split wv: contiguous rows [r0, r1), or (STRIDED) rows wv, wv+W, wv+2W, ... so that all
   // splits read neighbouring rows at the same time
   const int r0 = STRIDED ? wv : (int)((int64_t)wv * n / W);
@@ -696,7 +678,7 @@ __global__ __launch_bounds__(64 * W) void reduce_kernel_splitn(const float* __re
     typedef typename vec4<float>::type XV;
     const char* tile0 = reinterpret_cast<const char*>(stack + col0 + qb * 4) + (int64_t)r0 * stride * 4;
     const int64_t row_bytes = stride * 4 * RS;
-    const uint32_t bytes = (uint32_t)nq * 16u;
+    const uint32_t bytes = (uint32_t)tcols * 4u;
     const int voff = lane * 16;
     const int cnt = (r1 - r0 + RS - 1) / RS;  // >= 1
     const typename P::w_t* ws = w + r0;
@@ -738,10 +720,10 @@ __global__ __launch_bounds__(64 * W) void reduce_kernel_splitn(const float* __re
     if ((wv % (2 * h)) == 0 && wv + h < W) part[wv][lane] = part[wv][lane] + part[wv + h][lane];
     __syncthreads();
   }
-  if (wv == 0 && lane < nq) finish_quad<T, OP, A>(e, (qb + lane) * 4, 4, part[0][lane]);
-  // the window's ragged last quad (ncols % 4 != 0): the sequential path, in the chunk that holds it
-  if (threadIdx.x == 0 && qfull * 4 < ncols && qfull >= qb && qfull < qb + 64)
-    reduce_ragged<P, T, OP>(stack + col0, stride, n, w, qfull, qfull + 1, ncols, e);
+  if (wv == 0 && lane < nq) {
+    const int64_t c = (qb + lane) * 4;
+    finish_quad<T, OP, A>(e, c, ncols - c < 4 ? (int)(ncols - c) : 4, part[0][lane]);
+  }
 }
 
 // fa_gather_rows: block (s, i) copies client i's tensor of segment s into its stack row.

@@ -228,16 +228,23 @@ int dispatch_segrows(int op, const float* const* rows, int n, const void* w, con
   }
 }
 
-// Split-N geometry (tools/tune_splitn.py): one 1-KiB chunk of every row per block, kSplitW client
-// splits (one per wave), each a rolling pipeline kSplitD rows deep.
-constexpr int kSplitW = 8, kSplitD = 8;
+// Split-N geometry (tools/tune_splitn.py, profiles/r02/tune_splitn): one 1-KiB chunk of every row
+// per block, kSplitW client splits (one per wave), each a rolling pipeline kSplitD rows deep.
+// 1000 x 44,416 fp32: 28.7 us vs 50.2 us sequential; 4000 x 44,416: 111 vs 184 us; but
+// 1000 x 1 M (3907 chunks): 738 vs 572 us — so the split form is used only for windows of fewer
+// 1-KiB chunks than CUs, and with at least 2 * kSplitW clients.  And at most kSplitMaxN clients:
+// a reordered fp32 sum differs from the sequential one by about the sequential sum's own rounding
+// error, which grows like sqrt(N) — U(-1,1) uploads: 5.9e-7 normwise at N = 1000, 1.18e-6 at
+// N = 4000 (tune_splitn) — and the contract is <= 1e-6.
+constexpr int kSplitW = 4, kSplitD = 8, kSplitMaxN = 2048;
 constexpr int kSplitS = kSplitW;
 
 template <class P, typename T, int OP>
 int launch_splitn(const float* stack, int64_t stride, int n, const void* w, int64_t col0, int64_t ncols,
                   const Epi<T>& e, hipStream_t s) {
-  if (n < 2 * kSplitS) return launch_reduce<P, T, OP>(stack, stride, n, w, col0, ncols, e, s);  // nothing to split
   const int64_t chunks = ((ncols + 3) / 4 + 63) / 64;
+  if (n < 2 * kSplitS || n > kSplitMaxN || chunks >= device_cus())  // see kSplitMaxN
+    return launch_reduce<P, T, OP>(stack, stride, n, w, col0, ncols, e, s);
   hipLaunchKernelGGL((reduce_kernel_splitn<P, T, OP, kSplitW, kSplitD, kNT>), dim3((unsigned)chunks),
                      dim3(64 * kSplitW), 0, s, stack, stride, n, static_cast<const typename P::w_t*>(w), col0, ncols, e);
   return launch_check();

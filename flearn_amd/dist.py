@@ -137,9 +137,10 @@ class ShardedReducer:
         return self.full[: p.n_cols]
 
 
-def hip_reduce_fn(stack, weights, mode, denom, **epilogue):
+def hip_reduce_fn(stack, weights, mode, denom, reorder=False, **epilogue):
     """reduce_fn over a device-resident local stack [N, local_cols] with the fused HIP kernel.
-    Epilogue state tensors (prev, v), if any, are local-column tensors and are sliced alike."""
+    Epilogue state tensors (prev, v), if any, are local-column tensors and are sliced alike.
+    reorder: allow the split-N kernel (aggregator.reduce_stack)."""
     from .aggregator import reduce_stack
 
     prev, v = epilogue.pop("prev", None), epilogue.pop("v", None)
@@ -148,6 +149,23 @@ def hip_reduce_fn(stack, weights, mode, denom, **epilogue):
         kw = dict(epilogue)
         if prev is not None:
             kw.update(prev=prev[col_begin : col_begin + n_cols], v=v[col_begin : col_begin + n_cols])
-        reduce_stack(stack, weights, mode, denom, col_begin=col_begin, n_cols=n_cols, out32=out_slice, **kw)
+        reduce_stack(stack, weights, mode, denom, col_begin=col_begin, n_cols=n_cols, out32=out_slice, reorder=reorder,
+                     **kw)
 
     return fn
+
+
+def gather_columns(local: torch.Tensor, width: int, stride: int, group=None) -> torch.Tensor:
+    """Reassemble a column-sharded bucket (Aggregator(group=...)): rank r holds columns
+    [r*width, r*width + local.numel()) of a `stride`-wide bucket (the last ranks' ranges may be
+    short or empty).  One all_gather_into_tensor of `width` padded columns per rank; returns the
+    first `stride` columns of the gathered buffer (on every rank)."""
+    world = dist.get_world_size(group)
+    if local.numel() == width:
+        src = local
+    else:
+        src = torch.zeros(width, dtype=local.dtype, device=local.device)
+        src[: local.numel()] = local
+    full = torch.empty(world * width, dtype=local.dtype, device=local.device)
+    dist.all_gather_into_tensor(full, src, group=group)
+    return full[:stride]

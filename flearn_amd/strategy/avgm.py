@@ -16,8 +16,9 @@ from ._update import DeviceUpdater
 class AVGM(AVG):
     """Mean momentum (Hsu et al., arXiv:1909.06335)."""
 
-    def __init__(self, encrypt=None, output="reference", device=None, server_side=False, beta=0.9, devices=None):
-        super().__init__(encrypt, output, device, devices)
+    def __init__(self, encrypt=None, output="reference", device=None, server_side=False, beta=0.9, devices=None,
+                 group=None):
+        super().__init__(encrypt, output, device, devices, group)
         self.server_side = server_side
         self.beta = beta
         self._updater = None

@@ -7,8 +7,9 @@ from .utils import convert_to_tensor
 
 
 class LG_R(AVG):
-    def __init__(self, shared_key_layers=None, encrypt=None, output="reference", device=None, devices=None):
-        super().__init__(encrypt, output, device, devices)
+    def __init__(self, shared_key_layers=None, encrypt=None, output="reference", device=None, devices=None,
+                 group=None):
+        super().__init__(encrypt, output, device, devices, group)
         self.shared_key_layers = shared_key_layers
 
     def client(self, trainer, agg_weight=1.0):

@@ -19,8 +19,8 @@ class OPT(AVG):
     """Adaptive federated optimization (Reddi et al., arXiv:2003.00295)."""
 
     def __init__(self, encrypt=None, output="reference", device=None, server_side=False, method="adagrad",
-                 devices=None):
-        super().__init__(encrypt, output, device, devices)
+                 devices=None, group=None):
+        super().__init__(encrypt, output, device, devices, group)
         self.server_side = server_side
         self.method = method.lower()
         if self.method not in _METHODS:

@@ -11,6 +11,12 @@ Extra keyword arguments (all optional, defaults keep the reference's behaviour):
     device  : HIP device for the engine (default: torch's current device)
     devices : several HIP devices: the bucket's columns are split over them, each ingesting and
               reducing its share through its own PCIe link (per-GPU parallel H2D/D2H)
+    group   : one process per GPU (torch.distributed initialised, e.g. under torchrun): every
+              rank calls server() with the same uploads, packs and reduces only its columns, and
+              an RCCL all-gather over xGMI reassembles the global model on every rank
+              (flearn_amd.dist; True = the default process group)
+    reorder : (attribute, default False) allow the split-N kernel for narrow models with many
+              clients — deterministic and within 1e-6 normwise of the reference, not bit-exact
 """
 from __future__ import annotations
 
@@ -30,11 +36,12 @@ class BaseEncrypt:
 
 
 class Strategy(ABC):
-    def __init__(self, encrypt=None, output: str = "reference", device=None, devices=None):
+    def __init__(self, encrypt=None, output: str = "reference", device=None, devices=None, group=None):
         self.encrypt = BaseEncrypt() if encrypt is None else encrypt
         self.output = output
         self.device = device
         self.devices = devices
+        self.group = group
         self._engine = None
 
     # -- engine -----------------------------------------------------------------------------
@@ -46,7 +53,8 @@ class Strategy(ABC):
 
             d = self.__dict__
             self._engine = Aggregator(device=d.get("device"), output=d.get("output", "reference"),
-                                      devices=d.get("devices"))
+                                      devices=d.get("devices"), group=d.get("group"),
+                                      reorder=bool(d.get("reorder", False)))
         return self._engine
 
     # -- reference surface ------------------------------------------------------------------

@@ -80,3 +80,33 @@ def test_sharded_reduce_eight_ranks():
     width whose last rank's slices are partly padding."""
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     mp.spawn(_worker, args=(8, _free_port(), 3, 40_001, 2, "adagrad", (3, 1)), nprocs=8, join=True)
+
+
+def _gather_worker(rank, world, port, stride, dtype):
+    from flearn_amd.bucket import rank_width
+    from flearn_amd.dist import gather_columns
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        w = rank_width(stride, world)
+        assert w % 64 == 0 and w * world >= stride
+        c0 = min(rank * w, stride)
+        c1 = min(c0 + w, stride)
+        full_ref = torch.arange(stride, dtype=dtype) * 0.5 - 7
+        local = full_ref[c0:c1].clone()  # possibly short or empty on the last ranks
+        got = gather_columns(local, w, stride, None)
+        assert got.dtype == dtype and got.shape == (stride,)
+        assert torch.equal(got, full_ref)
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,stride,dtype", [(2, 44_480, torch.float64), (3, 64 * 7, torch.float32),
+                                                (4, 64, torch.float32)])
+def test_strategy_group_column_gather(world, stride, dtype):
+    """Aggregator(group=...) (the Strategy-level RCCL path behind Server.py:140): each rank's
+    equal ALIGN-aligned column range, short or empty on the last ranks, reassembled by one
+    all-gather into the whole bucket on every rank."""
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    mp.spawn(_gather_worker, args=(world, _free_port(), stride, dtype), nprocs=world, join=True)

@@ -930,3 +930,29 @@ def test_client_side_update_refuses_a_changed_layout(cuda):
         s.mean_momentum({"w": np.ones(12, np.float32)}, {"w": np.zeros(12)}, 0.9)
     s._updater.reset()
     s.mean_momentum({"w": np.ones(12, np.float32)}, {"w": np.zeros(12)}, 0.9)
+
+
+@pytest.mark.parametrize("name", ["avg_w1_n10", "avg_bnmodel_pyint_n4", "trace_lenet5_round0", "avg_torch_n3"])
+def test_strategy_group_mode_one_rank(name, cuda, tmp_path):
+    """AVG(group=True): the Strategy-level column-sharded path (pack this rank's columns, reduce,
+    RCCL all_gather_into_tensor) on a 1-rank RCCL group — the multi-GPU call sequence behind
+    flearn's Server.py:140, bit-exact against the reference's fixtures."""
+    import torch.distributed as dist
+
+    created = False
+    if not dist.is_initialized():
+        dist.init_process_group("nccl", init_method=f"file://{tmp_path}/pg", rank=0, world_size=1, device_id=cuda)
+        created = True
+    try:
+        g = Golden(name)
+        s = strategy_for(g)
+        s.group = True
+        got = s.server(upload(g.clients(), g.weights()), 0)["w_glob"]
+        assert_dict_bitwise(got, g.output(), name)
+        a = AVGM(server_side=True, group=True)
+        a.server_opt.init_global({k: np.asarray(v, np.float32) for k, v in g.output().items()
+                                  if np.asarray(v).dtype == np.float64 and np.ndim(v)})
+        a.server(upload(g.clients(), g.weights()), 1)
+    finally:
+        if created:
+            dist.destroy_process_group()

@@ -79,3 +79,22 @@ extern "C" int tune_splitn_launch(int variant, const float* stack, int64_t strid
     default: return -1;
   }
 }
+
+// probe: does a 16-B raw buffer load whose range covers only `bytes` (< 16) return the in-range
+// dwords (per-dword range check) or nothing?  out[0..3] = the load at offset `off`
+namespace {
+__global__ void oob_probe_kernel(const float* src, uint32_t bytes, int off, float* out) {
+  if (threadIdx.x == 0) {
+    const vec4<float>::type v = buf_load_quad<true>(row_rsrc(src, bytes), off, 0);
+    out[0] = v[0];
+    out[1] = v[1];
+    out[2] = v[2];
+    out[3] = v[3];
+  }
+}
+}  // namespace
+
+extern "C" int tune_oob_probe(const float* src, uint32_t bytes, int off, float* out, void* stream) {
+  hipLaunchKernelGGL(oob_probe_kernel, dim3(1), dim3(64), 0, static_cast<hipStream_t>(stream), src, bytes, off, out);
+  return hipGetLastError() == hipSuccess ? 0 : -3;
+}
