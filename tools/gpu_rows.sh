@@ -1,8 +1,8 @@
-# Round-2 pass for the row-pointer path: its GPU tests, bench_rows for c2 / ns / c3, and a
+# Row-pointer (device-upload) path: its GPU tests, bench_rows for c2 / ns / c3, and a
 # rocprofv3 kernel trace of the server() loop (no per-key copy kernels expected).
 set -e
 R=$GRAFT_REPO_ROOT
-O=$R/gpurun_out/${OUT:-r02_rows}
+O=$R/gpurun_out/${OUT:-rows}
 mkdir -p $O
 timeout -k 10 400 python -u -m pytest $R/tests/test_gpu_rows.py -x -v --timeout 120 --timeout-method thread -p no:cacheprovider > $O/pytest_rows.log 2>&1
 for c in c2 ns c3; do

@@ -1,0 +1,22 @@
+# Geometry sweeps of tools/tune_reduce.hip behind profiles/r01_rows/tune/<SET>/ (variants
+# interleaved in one process, bitwise-checked, bracketed by streaming-read and float4-copy roofs).
+#   SET=rm bash tools/gpu_tune_reduce.sh        (build: hipcc -O3 --offload-arch=gfx950 ... tools/tune_reduce.hip)
+set -e
+R=$GRAFT_REPO_ROOT
+SET=${SET:-rm}
+O=$R/gpurun_out/$SET
+mkdir -p $O
+T=$R/tools/tune_reduce
+case $SET in
+  narrow) SHAPES="200:5849600:mean 200:1462400:mean 400:2924800:mean 400:731200:mean 800:1462400:mean 800:365632:mean 100:1462400:mean 100:365632:mean 100:3201280:mean" ;;
+  epi) SHAPES="100:25610176:avgm 100:86567680:adagrad 100:3201280:avgm 800:1462400:avgm 100:11699136:adagrad 400:731200:adagrad" ;;
+  grid|inflight|misc) SHAPES="100:11699136:mean 1000:11699136:mean 100:25610176:avgm 100:86567680:adagrad 800:1462400:mean 400:731200:mean 200:5849600:mean" ;;
+  stagger) SHAPES="100:11699136:mean 200:11699136:mean 1000:11699136:mean 100:25610176:avgm" ;;
+  one) SHAPES="100:86567680:adagrad 100:25610176:avgm 100:11699136:mean 1000:11699136:mean" ;;
+  *) SHAPES="100:11699136:mean 1000:11699136:mean 200:11699136:mean 100:25610176:avgm 100:86567680:adagrad 800:1462400:mean" ;;
+esac
+for s in $SHAPES; do
+  IFS=: read -r n p op <<< "$s"
+  TUNE_SET=$SET timeout -k 10 200 $T $n $p 3 $op > $O/n${n}_p${p}_$op.txt 2>&1
+done
+echo done
