@@ -286,6 +286,111 @@ __device__ __forceinline__ vec4<float>::type buf_load_quad(__amdgpu_buffer_rsrc_
   return __builtin_bit_cast(vec4<float>::type, u);
 }
 
+// ---------------------------------------------------------------------------------------------
+// Piece epilogue through buffer descriptors.  A lane's slots of a piece are quads
+// q = threadIdx.x + v*STEP; the state operands (prev or h, v) are loaded for B slots at once,
+// UNCONDITIONALLY, through descriptors whose range is the piece's valid columns — the raw-buffer
+// range check is per dword on gfx950 (tools/probe_oob.py), so lanes past the end read 0 and their
+// stores are dropped, with no branch — then the B results are computed and stored.  With one
+// guarded generic load per quad (finish_quad) the compiler waited for each quad's loads, and for
+// the previous quad's stores, before the next: 24 serial HBM round trips at every piece-group end
+// of the fused FedAVGM kernel.
+// ---------------------------------------------------------------------------------------------
+template <typename T>
+__device__ __forceinline__ typename vec4<T>::type buf_load_tquad(__amdgpu_buffer_rsrc_t r, int q) {
+  if constexpr (sizeof(T) == 4) {
+    return __builtin_bit_cast(typename vec4<T>::type, __builtin_amdgcn_raw_buffer_load_b128(r, q * 16, 0, 0));
+  } else {
+    typedef double d2 __attribute__((ext_vector_type(2)));
+    const d2 lo = __builtin_bit_cast(d2, __builtin_amdgcn_raw_buffer_load_b128(r, q * 32, 0, 0));
+    const d2 hi = __builtin_bit_cast(d2, __builtin_amdgcn_raw_buffer_load_b128(r, q * 32 + 16, 0, 0));
+    return typename vec4<T>::type{lo[0], lo[1], hi[0], hi[1]};
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ void buf_store_tquad(__amdgpu_buffer_rsrc_t r, int q, typename vec4<T>::type v) {
+  if constexpr (sizeof(T) == 4) {
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, q * 16, 0, 0);
+  } else {
+    typedef double d2 __attribute__((ext_vector_type(2)));
+    const d2 lo = {v[0], v[1]}, hi = {v[2], v[3]};
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, lo), r, q * 32, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, hi), r, q * 32 + 16, 0, 0);
+  }
+}
+
+template <typename E>
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t col_rsrc(E* base, int64_t qbase, int cols) {
+  // a null array (no out32 / out64) gets an empty range: every access is dropped.  Scalar
+  // arithmetic only (a select between two descriptors is lowered to VGPRs, and every access
+  // through a VGPR descriptor becomes a readfirstlane loop)
+  // through readfirstlane: the Epi fields may have been reloaded from the private copy the kernel
+  // makes for the noinline ragged path, and the compiler then cannot prove them wave-uniform
+  const uint64_t a = (uint64_t)(uintptr_t)base + (uint64_t)(qbase * 4 * (int64_t)sizeof(E));
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)a);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(a >> 32));
+  const uint32_t n = (uint32_t)__builtin_amdgcn_readfirstlane(base ? cols * (int)sizeof(E) : 0);
+  return row_rsrc(reinterpret_cast<const void*>((uintptr_t)(((uint64_t)hi << 32) | lo)), n);
+}
+
+template <typename T, int OP, typename A, int V, int STEP, int B>
+__device__ __forceinline__ void finish_piece(const Epi<T>& e, int64_t qbase, int cols,
+                                             const typename vec4<A>::type (&acc)[V]) {
+  static_assert(V % B == 0, "batch must divide the slots");
+  if (cols <= 0) return;
+  const __amdgpu_buffer_rsrc_t rl = col_rsrc<const float>(OP == FA_OP_DYN ? e.h : e.prev, qbase, OP == FA_OP_MEAN ? 0 : cols);
+  const __amdgpu_buffer_rsrc_t rv = col_rsrc<T>(e.v, qbase, OP == FA_OP_MEAN ? 0 : cols);
+  const __amdgpu_buffer_rsrc_t r32 = col_rsrc<float>(e.out32, qbase, cols);
+  const __amdgpu_buffer_rsrc_t r64 = col_rsrc<double>(e.out64, qbase, cols);
+#pragma unroll
+  for (int b0 = 0; b0 < V; b0 += B) {
+    typename vec4<float>::type l[B];
+    typename vec4<T>::type vv[B];
+#pragma unroll
+    for (int b = 0; b < B; ++b) {
+      const int q = (int)threadIdx.x + (b0 + b) * STEP;
+      if constexpr (OP != FA_OP_MEAN) {
+        l[b] = buf_load_tquad<float>(rl, q);
+        vv[b] = buf_load_tquad<T>(rv, q);
+      } else {
+        l[b] = typename vec4<float>::type{0.f, 0.f, 0.f, 0.f};
+        vv[b] = typename vec4<T>::type{T(0), T(0), T(0), T(0)};
+      }
+    }
+#pragma unroll
+    for (int b = 0; b < B; ++b) {
+      const int q = (int)threadIdx.x + (b0 + b) * STEP;
+      const typename vec4<A>::type a = acc[b0 + b];
+      typename vec4<T>::type w;
+      if constexpr (OP == FA_OP_DYN) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const T g = (T)a[j] / e.denom;
+          const T d = g * e.n - vv[b][j];                // delta_theta = w_glob*N - theta   dyn.py:20-21
+          const float hn = (float)((T)l[b][j] - e.c * d);  // h -= alpha/N * delta (fp32 h)    dyn.py:26
+          const float ah = e.alpha32 * hn;               // alpha * h stays fp32              dyn.py:33
+          w[j] = g - (T)ah;                              // w_glob - alpha*h                  dyn.py:33
+          l[b][j] = hn;
+          vv[b][j] = w[j];                               // theta = w_glob                    dyn.py:34
+        }
+        buf_store_tquad<float>(rl, q, l[b]);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const T g = (T)a[j] / e.denom;  // np.divide(w_glob, np.sum(a))  strategy.py:127-129
+          T vj = vv[b][j];
+          w[j] = update<T, OP>(e, g, (T)l[b][j], vj);
+          vv[b][j] = vj;
+        }
+      }
+      if constexpr (OP != FA_OP_MEAN) buf_store_tquad<T>(rv, q, vv[b]);
+      if (e.out32) buf_store_tquad<float>(r32, q, typename vec4<float>::type{(float)w[0], (float)w[1], (float)w[2], (float)w[3]});
+      if (e.out64) buf_store_tquad<double>(r64, q, typename vec4<double>::type{(double)w[0], (double)w[1], (double)w[2], (double)w[3]});
+    }
+  }
+}
+
 template <class P, typename T, int OP, int V, int U, bool NT>
 __device__ __forceinline__ void reduce_subtile_buf(const float* __restrict__ base, int64_t stride,
                                                    int n, const typename P::w_t* __restrict__ w,
@@ -572,11 +677,7 @@ __device__ __forceinline__ void rows_piece(const float* __restrict__ stack, int6
     AV acc[V];
     rows_sweep<P, V, D, W, NT>(StackRows{reinterpret_cast<const char*>(stack + col0 + qb * 4), stride * 4},
                                (uint32_t)nq * 16u, n, w, acc);
-#pragma unroll
-    for (int v = 0; v < V; ++v) {
-      const int q = v * 64 * W + (int)threadIdx.x;
-      if (q < nq) finish_quad<T, OP, A>(e, (qb + q) * 4, 4, acc[v]);
-    }
+    finish_piece<T, OP, A, V, 64 * W, (V >= 2 ? 2 : V)>(e, qb, nq * 4, acc);
   }
   // the window's ragged last quad (ncols % 4 != 0), in the piece that holds it
   if (threadIdx.x == 0 && qfull * 4 < ncols && qfull >= qb && qfull < qend)
@@ -618,16 +719,11 @@ __global__ __launch_bounds__(64 * W) void reduce_kernel_segrows(const float* con
     if (nq > 64 * W) {
       AV acc[V];
       rows_sweep<P, V, D, W, NT>(row, bytes, n, w, acc);
-#pragma unroll
-      for (int v = 0; v < V; ++v) {
-        const int q = v * 64 * W + (int)threadIdx.x;
-        if (q < nq) finish_quad<T, OP, A>(e, pc.col + (int64_t)q * 4, pc.n_cols - q * 4 < 4 ? pc.n_cols - q * 4 : 4, acc[v]);
-      }
+      finish_piece<T, OP, A, V, 64 * W, (V >= 2 ? 2 : V)>(e, pc.col / 4, pc.n_cols, acc);
     } else if (nq > 0) {
       AV acc[1];
       rows_sweep<P, 1, V * D, W, NT>(row, bytes, n, w, acc);
-      const int q = (int)threadIdx.x;
-      if (q < nq) finish_quad<T, OP, A>(e, pc.col + (int64_t)q * 4, pc.n_cols - q * 4 < 4 ? pc.n_cols - q * 4 : 4, acc[0]);
+      finish_piece<T, OP, A, 1, 64 * W, 1>(e, pc.col / 4, pc.n_cols, acc);
     }
     if (threadIdx.x == 0) s_next = claimed;
     __syncthreads();
@@ -720,9 +816,9 @@ __global__ __launch_bounds__(64 * W) void reduce_kernel_splitn(const float* __re
     if ((wv % (2 * h)) == 0 && wv + h < W) part[wv][lane] = part[wv][lane] + part[wv + h][lane];
     __syncthreads();
   }
-  if (wv == 0 && lane < nq) {
-    const int64_t c = (qb + lane) * 4;
-    finish_quad<T, OP, A>(e, c, ncols - c < 4 ? (int)(ncols - c) : 4, part[0][lane]);
+  if (wv == 0) {
+    const AV r[1] = {part[0][lane]};
+    finish_piece<T, OP, A, 1, 64, 1>(e, qb, tcols, r);
   }
 }
 
@@ -778,7 +874,7 @@ __global__ __launch_bounds__(64 * W) void reduce_kernel_rows(const float* __rest
 // rolling register pipeline D steps deep (D divides KG, so every slot index is static).  The
 // whole grid then moves through the client rows together.  Per element the sum is still rows
 // 0..N-1 in order.
-template <class P, typename T, int OP, int V, int D, int W, int KG, bool NT>
+template <class P, typename T, int OP, int V, int D, int W, int KG, bool NT, int EPIB = (V >= 2 ? 2 : V)>
 __global__ __launch_bounds__(64 * W) void reduce_kernel_rowmajor(const float* __restrict__ stack,
                                                                  int64_t stride, int n,
                                                                  const typename P::w_t* __restrict__ w,
@@ -862,13 +958,18 @@ __global__ __launch_bounds__(64 * W) void reduce_kernel_rowmajor(const float* __
       }
     }
 #undef FA_RM_LOAD
+    if constexpr (EPIB == 0) {  // per-quad epilogue (tuning reference: tools/tune_reduce.hip set "epib")
 #pragma unroll
-    for (int j = 0; j < KG; ++j) {
+      for (int j = 0; j < KG; ++j) {
 #pragma unroll
-      for (int v = 0; v < V; ++v) {
-        const int q = v * 64 * W + (int)threadIdx.x;
-        if (q < nq[j]) finish_quad<T, OP, A>(e, (qb[j] + q) * 4, 4, acc[j][v]);
+        for (int v = 0; v < V; ++v) {
+          const int q = v * 64 * W + (int)threadIdx.x;
+          if (q < nq[j]) finish_quad<T, OP, A>(e, (qb[j] + q) * 4, 4, acc[j][v]);
+        }
       }
+    } else {
+#pragma unroll
+      for (int j = 0; j < KG; ++j) finish_piece<T, OP, A, V, 64 * W, EPIB>(e, qb[j], nq[j] * 4, acc[j]);
     }
   }
   // the window's ragged last quad (ncols % 4 != 0): the block that owns its piece

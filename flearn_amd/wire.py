@@ -64,6 +64,30 @@ _PyBytes_AsString.restype = ctypes.c_void_p
 _PyBytes_AsString.argtypes = [ctypes.py_object]
 
 
+
+def _probe_fill_in_place() -> bool:
+    """The encoders write base64 text straight into a fresh str from PyUnicode_New(n, 127): a
+    compact ASCII object whose UTF-8 view (PyUnicode_AsUTF8AndSize) IS its character buffer.
+    That holds for CPython's PEP 393 strings (3.3+); it is checked here once, on the running
+    interpreter, and the encoders fall back to base64.b64encode when it does not hold."""
+    import sys
+
+    if sys.implementation.name != "cpython" or sys.version_info < (3, 8):
+        return False
+    try:
+        probe = _PyUnicode_New(8, 127)
+        size = ctypes.c_ssize_t()
+        p = _AsUTF8AndSize(probe, ctypes.byref(size))
+        if not p or size.value != 8:
+            return False
+        ctypes.memmove(p, b"fA64prob", 8)
+        return probe == "fA64prob" and len(probe) == 8
+    except Exception:
+        return False
+
+
+_FILL_IN_PLACE = _probe_fill_in_place()
+
 _THREADS = max(1, min(16, os.cpu_count() or 1))
 _SERIAL_BYTES = 1 << 20  # below ~1 MB of payload, waking the pool costs more than it saves
 
@@ -102,6 +126,10 @@ def b64encode(raw) -> str:
     """base64.b64encode(raw).decode() with the native encoder, written into the new str."""
     L = na.load()
     mv = memoryview(raw).cast("B")
+    if not _FILL_IN_PLACE:
+        import base64
+
+        return base64.b64encode(mv).decode("ascii")
     n = mv.nbytes
     m = 4 * ((n + 2) // 3)
     out = _PyUnicode_New(m, 127)
@@ -134,6 +162,8 @@ def pickle_b64(obj) -> str:
     sink = _Chunks()
     pickle.Pickler(sink, protocol=pickle.DEFAULT_PROTOCOL).dump(obj)
     parts = sink.parts
+    if not _FILL_IN_PLACE:
+        return b64encode(b"".join(parts))
     k = len(parts)
     n = sum(map(len, parts))
     m = 4 * ((n + 2) // 3)

@@ -134,16 +134,16 @@ Variant make_rows(const float* stack, int64_t stride, int n, const float* w, int
           true, {}};
 }
 
-template <int V, int D, int W, int KG, int OP, typename T>
+template <int V, int D, int W, int KG, int OP, typename T, int EPIB = (V >= 2 ? 2 : V)>
 Variant make_rowmajor(const float* stack, int64_t stride, int n, const float* w, int64_t ncols, Epi<T> e,
                       double bytes, int64_t grid) {
   const int64_t chunks = ((ncols + 3) / 4 + 63) / 64;
   if (grid > chunks) grid = chunks;
   char name[96];
-  snprintf(name, sizeof name, "rowmajor V%d D%d W%d KG%d g%lld", V, D, W, KG, (long long)grid);
+  snprintf(name, sizeof name, "rowmajor V%d D%d W%d KG%d g%lld epib%d", V, D, W, KG, (long long)grid, EPIB);
   return {name, bytes,
           [=] {
-            hipLaunchKernelGGL((reduce_kernel_rowmajor<AccF32, T, OP, V, D, W, KG, true>), dim3((unsigned)grid),
+            hipLaunchKernelGGL((reduce_kernel_rowmajor<AccF32, T, OP, V, D, W, KG, true, EPIB>), dim3((unsigned)grid),
                                dim3(64 * W), 0, 0, stack, stride, n, w, (int64_t)0, ncols, e);
           },
           true, {}};
@@ -307,6 +307,19 @@ int main(int argc, char** argv) {
   vs.push_back(op == FA_OP_AVGM      ? make_rowmajor<V, D, W, KG, FA_OP_AVGM, double>(stack, stride, n, w, ncols, e, bytes, G)   \
                : op == FA_OP_ADAGRAD ? make_rowmajor<V, D, W, KG, FA_OP_ADAGRAD, double>(stack, stride, n, w, ncols, e, bytes, G) \
                                      : make_rowmajor<V, D, W, KG, FA_OP_MEAN, double>(stack, stride, n, w, ncols, e, bytes, G))
+#define RME(V, D, W, KG, G, EB)                                                                                      \
+  vs.push_back(op == FA_OP_AVGM      ? make_rowmajor<V, D, W, KG, FA_OP_AVGM, double, EB>(stack, stride, n, w, ncols, e, bytes, G)   \
+               : op == FA_OP_ADAGRAD ? make_rowmajor<V, D, W, KG, FA_OP_ADAGRAD, double, EB>(stack, stride, n, w, ncols, e, bytes, G) \
+                                     : make_rowmajor<V, D, W, KG, FA_OP_MEAN, double, EB>(stack, stride, n, w, ncols, e, bytes, G))
+  if (!strcmp(set, "epib")) {  // piece epilogue: per-quad guarded loads (0) vs batched buffer loads of B slots
+    RME(8, 1, 8, 4, 192, 0);
+    RME(8, 1, 8, 4, 192, 2);
+    RME(8, 1, 8, 4, 192, 4);
+    RME(8, 1, 8, 4, 192, 8);
+    RME(8, 1, 8, 3, 192, 0);
+    RME(8, 1, 8, 3, 192, 4);
+    RME(8, 1, 8, 2, 192, 4);
+  }
   if (!strcmp(set, "rmgrid")) {  // row-major: grid / group size around the product's choice
     RM(8, 1, 8, 5, 176);
     RM(8, 1, 8, 4, 192);
