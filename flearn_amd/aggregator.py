@@ -276,6 +276,7 @@ class ServerOptimizer:
         self.state = {}  # shard index -> (prev, v)
         self._sig = None
         self._pending_init = None
+        self.group = None  # (process group, world) when bound to a column-sharded Aggregator
 
     def init_global(self, glob: dict):
         """Set the previous global model (dict of arrays/tensors); v_t is reset to zeros."""
@@ -323,7 +324,19 @@ class ServerOptimizer:
         self._sig = self._signature(plan, shards)
 
     def v_t(self, plan: BucketPlan) -> dict:
-        """The state as the reference exposes it (self.v_t dict of arrays)."""
+        """The state as the reference exposes it (self.v_t dict of arrays).  With a column-sharded
+        process group (Aggregator(group=...)) every rank holds only its columns: this is then a
+        collective (an all-gather) that every rank must call."""
+        if self.group is not None:
+            from .bucket import rank_width
+            from .dist import gather_columns
+
+            (sh_v,) = [self.state[i][1] for i in sorted(self.state)]
+            group, world = self.group
+            stride = plan.f32.stride
+            full = gather_columns(sh_v, rank_width(stride, world), stride, group)
+            host = full.cpu().numpy()
+            return {s.key: host[s.offset : s.offset + s.numel].reshape(s.shape).copy() for s in plan.f32.segments}
         host = np.concatenate([self.state[i][1].cpu().numpy() for i in sorted(self.state)])
         return {s.key: host[s.offset : s.offset + s.numel].reshape(s.shape).copy() for s in plan.f32.segments}
 
@@ -561,6 +574,8 @@ class Aggregator:
         stacks = self.packer.pack(plan, w_local_lst)
         fused = False
         if server_opt is not None and KIND_F32 in plan.groups:
+            if self._dist and isinstance(server_opt, ServerOptimizer):
+                server_opt.group = (self.group, self.packer.rank_cols[1])
             fused = server_opt.prepare(plan, [sh for sh, _ in stacks[KIND_F32]])
         results = {}
         first_means = {}

@@ -953,6 +953,11 @@ def test_strategy_group_mode_one_rank(name, cuda, tmp_path):
         a.server_opt.init_global({k: np.asarray(v, np.float32) for k, v in g.output().items()
                                   if np.asarray(v).dtype == np.float64 and np.ndim(v)})
         a.server(upload(g.clients(), g.weights()), 1)
+        b = AVGM(server_side=True)  # the same round without the group: same v_t
+        b.server_opt.init_global({k: np.asarray(v, np.float32) for k, v in g.output().items()
+                                  if np.asarray(v).dtype == np.float64 and np.ndim(v)})
+        b.server(upload(g.clients(), g.weights()), 1)
+        assert_dict_bitwise(a.server_opt.v_t(a.engine.last_plan), b.server_opt.v_t(b.engine.last_plan), name)
     finally:
         if created:
             dist.destroy_process_group()

@@ -313,3 +313,20 @@ def test_repeated_key_in_pickled_params_decodes_like_pickle():
     got = wire.Encrypt(fast_min_chars=0).decode(base64.b64encode(raw).decode())
     same(got, want)
     assert id(got["params"]) not in wire._ROWS  # not handed to the engine as a pinned row
+
+
+def test_in_place_str_fill_is_probed(monkeypatch):
+    """The encoders write into a fresh str only after an import-time probe of the interpreter;
+    with the probe failing they return base64.b64encode's text (same result)."""
+    import base64
+    import pickle
+
+    from flearn_amd import wire
+
+    assert wire._FILL_IN_PLACE  # CPython 3.10 here
+    obj = {"params": {"w": np.arange(1000, dtype=np.float32)}, "agg_weight": 1.0}
+    want = base64.b64encode(pickle.dumps(obj)).decode()
+    assert wire.pickle_b64(obj) == want
+    monkeypatch.setattr(wire, "_FILL_IN_PLACE", False)
+    assert wire.pickle_b64(obj) == want
+    assert wire.b64encode(b"abcde") == base64.b64encode(b"abcde").decode()

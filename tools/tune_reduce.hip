@@ -311,6 +311,21 @@ int main(int argc, char** argv) {
   vs.push_back(op == FA_OP_AVGM      ? make_rowmajor<V, D, W, KG, FA_OP_AVGM, double, EB>(stack, stride, n, w, ncols, e, bytes, G)   \
                : op == FA_OP_ADAGRAD ? make_rowmajor<V, D, W, KG, FA_OP_ADAGRAD, double, EB>(stack, stride, n, w, ncols, e, bytes, G) \
                                      : make_rowmajor<V, D, W, KG, FA_OP_MEAN, double, EB>(stack, stride, n, w, ncols, e, bytes, G))
+  if (!strcmp(set, "nsgrid")) {  // north-star shape: group size / grid / piece width
+    RM(8, 1, 8, 3, 192);
+    RM(8, 1, 8, 3, 208);
+    RM(8, 1, 8, 3, 240);
+    RM(8, 1, 8, 4, 192);
+    RM(8, 1, 8, 5, 176);
+    RM(8, 1, 8, 2, 192);
+    RM(16, 1, 4, 3, 192);
+    RM(16, 1, 4, 4, 192);
+    RM(16, 1, 4, 2, 192);
+    RM(16, 1, 4, 5, 176);
+    RM(16, 1, 4, 3, 208);
+    RM(16, 1, 4, 4, 224);
+    RM(16, 1, 4, 3, 176);
+  }
   if (!strcmp(set, "epib")) {  // piece epilogue: per-quad guarded loads (0) vs batched buffer loads of B slots
     RME(8, 1, 8, 4, 192, 0);
     RME(8, 1, 8, 4, 192, 2);
