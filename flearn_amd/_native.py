@@ -63,7 +63,7 @@ class Piece(ctypes.Structure):
     """struct fa_piece (include/flearn_amd.h)."""
 
     _fields_ = [("col", ctypes.c_int64), ("seg_off", ctypes.c_int64), ("seg", ctypes.c_int32),
-                ("n_cols", ctypes.c_int32), ("reserved", ctypes.c_int64)]
+                ("n_cols", ctypes.c_int32), ("aux", ctypes.c_int64)]
 
 
 class Epilogue(ctypes.Structure):

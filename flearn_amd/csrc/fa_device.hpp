@@ -822,6 +822,98 @@ __global__ __launch_bounds__(64 * W) void reduce_kernel_splitn(const float* __re
   }
 }
 
+// Row-major form of the row-pointer reduce.  A claim is a GROUP of KG wide pieces (the leading
+// pieces[0].aux entries of the largest-first table) swept together row by row — step (row i,
+// piece j), j fastest, one step (V*W KiB) in flight, like reduce_kernel_rowmajor — so the blocks
+// stay on neighbouring client rows as the stack kernel's do; the row pointer of the step after
+// the next one is fetched while the next is in flight (every index is static: j is unrolled).
+// Claims past the groups are the narrow pieces, one at a time, through the deep one-quad sweep.
+template <class P, typename T, int OP, int V, int W, int KG, int DN, bool NT>
+__global__ __launch_bounds__(64 * W) void reduce_kernel_segrows_rm(const float* const* __restrict__ rows, int n,
+                                                                   const typename P::w_t* __restrict__ w,
+                                                                   const fa_piece* __restrict__ pieces,
+                                                                   int64_t npieces, int* __restrict__ next, Epi<T> e) {
+  typedef typename P::acc_t A;
+  typedef typename vec4<A>::type AV;
+  typedef typename vec4<float>::type XV;
+  __shared__ int s_next;
+  const int64_t nwide = npieces > 0 ? pieces[0].aux : 0;
+  const int64_t groups = (nwide + KG - 1) / KG;
+  const int64_t claims = groups + (npieces - nwide);
+  const int voff = (int)threadIdx.x * 16;
+  int64_t t = blockIdx.x;
+  while (t < claims) {
+    int claimed = 0;
+    if (threadIdx.x == 0) claimed = (int)gridDim.x + atomicAdd(next, 1);
+    if (t < groups) {
+      const float* const* rp[KG];
+      int64_t ob[KG], col[KG];
+      int cols[KG];
+      uint32_t bytes[KG];
+#pragma unroll
+      for (int j = 0; j < KG; ++j) {
+        const int64_t pi = t * KG + j;
+        const fa_piece pc = pi < nwide ? pieces[pi] : fa_piece{0, 0, 0, 0, 0};
+        rp[j] = rows + (int64_t)pc.seg * n;  // a missing piece keeps segment 0's pointers, 0 bytes
+        ob[j] = pc.seg_off * 4;
+        col[j] = pc.col;
+        cols[j] = pc.n_cols;
+        bytes[j] = (uint32_t)pc.n_cols * 4u;
+      }
+      // row pointer of step (i, j); rows clamped (a step past the end is never loaded)
+#define FA_SRM_PTR(i, j) (reinterpret_cast<const char*>(rp[j][(i) < n ? (i) : n - 1]) + ob[j])
+#define FA_SRM_LOAD(p, j)                                                                                    \
+  {                                                                                                          \
+    const __amdgpu_buffer_rsrc_t r_ = row_rsrc((p), bytes[j]);                                               \
+    _Pragma("unroll") for (int v = 0; v < V; ++v) x[v] = buf_load_quad<NT>(r_, voff + v * 64 * W * 16, 0); \
+  }
+      AV acc[KG][V];
+      XV x[V];
+      const char* pn = FA_SRM_PTR(0, 0);
+      FA_SRM_LOAD(pn, 0);
+      pn = KG > 1 ? FA_SRM_PTR(0, 1 % KG) : FA_SRM_PTR(1, 0);
+      int i = 0;
+      for (; i < n; ++i) {
+        const typename P::w_t wi = w[i];
+#pragma unroll
+        for (int j = 0; j < KG; ++j) {
+#pragma unroll
+          for (int v = 0; v < V; ++v) acc[j][v] = i == 0 ? quad_mul<P>(wi, x[v]) : quad_axpy<P>(acc[j][v], wi, x[v]);
+          __builtin_amdgcn_sched_barrier(0);
+          if (j + 1 < KG || i + 1 < n) {  // the next step exists: (i, j+1) or (i+1, 0)
+            FA_SRM_LOAD(pn, (j + 1) % KG);
+            // the step after it: (i, j+2), (i+1, j+2-KG) or (i+2, 0)
+            pn = j + 2 < KG ? FA_SRM_PTR(i, j + 2) : (j + 2 - KG < KG ? FA_SRM_PTR(i + 1, (j + 2) % KG) : FA_SRM_PTR(i + 2, 0));
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+#undef FA_SRM_LOAD
+#undef FA_SRM_PTR
+#pragma unroll
+      for (int j = 0; j < KG; ++j) finish_piece<T, OP, A, V, 64 * W, (V >= 2 ? 2 : V)>(e, col[j] / 4, cols[j], acc[j]);
+    } else {
+      const fa_piece pc = pieces[nwide + (t - groups)];
+      const float* const* rp = rows + (int64_t)pc.seg * n;
+      const uint32_t bytes = (uint32_t)pc.n_cols * 4u;
+      const PtrRows row{rp, pc.seg_off * 4};
+      if (((pc.n_cols + 3) >> 2) > 64 * W) {  // a wide piece the groups did not take
+        AV acc[V];
+        rows_sweep<P, V, 1, W, NT>(row, bytes, n, w, acc);
+        finish_piece<T, OP, A, V, 64 * W, (V >= 2 ? 2 : V)>(e, pc.col / 4, pc.n_cols, acc);
+      } else if (pc.n_cols > 0) {
+        AV acc[1];
+        rows_sweep<P, 1, DN, W, NT>(row, bytes, n, w, acc);
+        finish_piece<T, OP, A, 1, 64 * W, 1>(e, pc.col / 4, pc.n_cols, acc);
+      }
+    }
+    if (threadIdx.x == 0) s_next = claimed;
+    __syncthreads();
+    t = s_next;
+    __syncthreads();
+  }
+}
+
 // fa_gather_rows: block (s, i) copies client i's tensor of segment s into its stack row.
 template <typename E>
 __global__ __launch_bounds__(kThreads) void gather_rows_kernel(E* __restrict__ stack, int64_t stride, int n,

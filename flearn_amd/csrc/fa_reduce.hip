@@ -188,29 +188,26 @@ int launch_reduce(const typename P::x_t* stack, int64_t stride, int n, const voi
   }
 }
 
-// Segmented row-pointer reduce (fa_reduce_f32_rows).  fa_rows_plan cuts every segment into pieces
-// of at most kSegPieceChunks KiB of a row, largest first; blocks claim them dynamically (see
-// reduce_kernel_segrows).  A block keeps one 64-KiB piece row in flight (plain mean: 4 waves x
-// 16 KiB; fused epilogues: 8 waves x 8 KiB) and narrow pieces V rows of one quad per lane.
-// One block per CU (tools/tune_rows.py, profiles/r02/tune_rows: 64-KiB pieces on 256 blocks beat
-// 32-KiB pieces two rows deep and 192 / 384 blocks on 100 x ResNet-18 and 100 x ResNet-50).  Plain mean: 4 waves x 8 KiB, D = 2; fused epilogues: 8 waves
+// Segmented row-pointer reduce (fa_reduce_f32_rows): reduce_kernel_segrows_rm — blocks claim
+// groups of kSegKG wide pieces (at most kSegPieceChunks KiB of a row each) and sweep them row by
+// row, one 64-KiB step (8 waves x 8 KiB) in flight like the stack kernel's row-major groups; then
+// the narrow pieces one by one through a 16-deep one-quad sweep.  192 blocks (tools/tune_rows.py,
+// profiles/r02/tune_rows/: grouped 100 x ResNet-18 85.7% = the stack kernel's, against 81-84% for
+// one claimed piece at a time).  Plain mean: 4 waves x 8 KiB, D = 2; fused epilogues: 8 waves
 // x 4 KiB, D = 2.
 constexpr int kSegPieceChunks = 64;
-constexpr double kSegBlocksPerCU = 1.0;
+constexpr double kSegBlocksPerCU = 0.75;
+constexpr int kSegW = 8, kSegV = 8, kSegKG = 2;                // row-major groups of 2 pieces, 8 x 8 KiB
+constexpr int64_t kSegWideCols = (int64_t)64 * kSegW * 4;      // wider pieces go into groups
 
 template <class P, typename T, int OP>
 int launch_segrows(const float* const* rows, int n, const void* w, const fa_piece* pieces, int64_t npieces,
                    int grid, int32_t* work, const Epi<T>& e, hipStream_t s) {
   const typename P::w_t* wt = static_cast<const typename P::w_t*>(w);
-  if constexpr (OP == FA_OP_MEAN) {
-    constexpr int W = 4, V = kSegPieceChunks / W;  // 16 KiB per wave, one row in flight
-    hipLaunchKernelGGL((reduce_kernel_segrows<P, T, OP, V, kPieceChunks / (V * W), W, kNT>), dim3((unsigned)grid),
-                       dim3(64 * W), 0, s, rows, n, wt, pieces, npieces, work, e);
-  } else {
-    constexpr int W = 8, V = kSegPieceChunks / W;
-    hipLaunchKernelGGL((reduce_kernel_segrows<P, T, OP, V, kPieceChunks / (V * W), W, kNT>), dim3((unsigned)grid),
-                       dim3(64 * W), 0, s, rows, n, wt, pieces, npieces, work, e);
-  }
+  // f64 sums (np.float64 weights) need twice the accumulator registers: one piece per group
+  constexpr int KG = sizeof(typename P::acc_t) == 8 ? 1 : kSegKG;
+  hipLaunchKernelGGL((reduce_kernel_segrows_rm<P, T, OP, kSegV, kSegW, KG, 16, kNT>), dim3((unsigned)grid),
+                     dim3(64 * kSegW), 0, s, rows, n, wt, pieces, npieces, work, e);
   return launch_check();
 }
 
@@ -335,6 +332,18 @@ int check_common(const X* stack, int64_t stride, int n, const void* w, int64_t c
   return FA_OK;
 }
 
+}  // namespace
+
+namespace {
+// Piece cut of one segment: `pc` chunks at most, equal pieces (the last one takes the remainder)
+template <typename F>
+void cut_segment(int64_t len, int64_t pc, F&& emit) {
+  const int64_t chunks = (len + 255) / 256;
+  if (chunks == 0) return;
+  const int64_t np = (chunks + pc - 1) / pc;
+  const int64_t per = (chunks + np - 1) / np * 256;  // columns per piece, whole 1-KiB chunks
+  for (int64_t off = 0; off < len; off += per) emit(off, len - off < per ? len - off : per);
+}
 }  // namespace
 
 extern "C" {
@@ -479,39 +488,65 @@ int fa_opt_apply(int32_t prec, const fa_epilogue* epi, const float* local, const
   return launch_check();
 }
 
+
 int fa_rows_plan(int32_t n_segments, const int64_t* seg_col, const int64_t* seg_len, int32_t op,
                  int32_t grid_hint, fa_piece* pieces, int64_t cap, int64_t* n_pieces, int32_t* grid) {
   if (n_segments < 0 || (n_segments > 0 && (!seg_col || !seg_len)) || !n_pieces || !grid)
     return fail(FA_ERR_ARG, "bad rows plan arguments");
   if (op < FA_OP_MEAN || op > FA_OP_DYN) return fail(FA_ERR_ARG, "unknown epilogue op");
-  constexpr int64_t kMaxCols = (int64_t)kSegPieceChunks * 256;  // columns per piece
-  int64_t count = 0;
-  for (int32_t s = 0; s < n_segments; ++s) {
+  for (int32_t s = 0; s < n_segments; ++s)
     if (seg_len[s] < 0 || seg_col[s] < 0 || seg_col[s] % 4 != 0)
       return fail(FA_ERR_ARG, "segment columns must be >= 0 and 4-aligned");
-    count += (seg_len[s] + kMaxCols - 1) / kMaxCols;
-  }
   int64_t g = grid_hint > 0 ? grid_hint : (int64_t)(device_cus() * kSegBlocksPerCU + 0.5);
-  if (g > count) g = count;
+  // Piece width: the widest (<= kSegPieceChunks) whose wide pieces make whole, or nearly whole,
+  // rounds of KG-piece groups over the grid — a group is the unit a block claims, and a last
+  // round of few groups leaves most blocks idle while it runs (~20% of a 100 x ResNet-50 launch
+  // at 64 KiB: 782 groups on 192 blocks)
+  auto count = [&](int64_t pc, int64_t* nwide) {
+    int64_t all = 0, wide = 0;
+    for (int32_t s = 0; s < n_segments; ++s)
+      cut_segment(seg_len[s], pc, [&](int64_t, int64_t cols) {
+        ++all;
+        wide += cols > kSegWideCols;
+      });
+    *nwide = wide;
+    return all;
+  };
+  int64_t best_pc = kSegPieceChunks, best_fill = -1;
+  for (int64_t pc = kSegPieceChunks; pc >= kSegPieceChunks * 5 / 8; --pc) {
+    int64_t nwide = 0;
+    count(pc, &nwide);
+    const int64_t groups = (nwide + kSegKG - 1) / kSegKG;
+    const int64_t r = groups % g;
+    const int64_t fill = (groups == 0 || r == 0) ? 1000 : r * 1000 / g;  // busy share of the last round
+    if (fill > best_fill) {
+      best_fill = fill;
+      best_pc = pc;
+    }
+    if (fill >= 900) break;
+  }
+  int64_t nwide = 0;
+  const int64_t total = count(best_pc, &nwide);
+  const int64_t claims = (nwide + kSegKG - 1) / kSegKG + (total - nwide);
+  if (g > claims) g = claims;
   *grid = (int32_t)g;
-  *n_pieces = count;
+  *n_pieces = total;
   if (!pieces) return FA_OK;
-  if (cap < count) return fail(FA_ERR_SIZE, "piece array too small");
+  if (cap < total) return fail(FA_ERR_SIZE, "piece array too small");
   int64_t k = 0;
-  for (int32_t s = 0; s < n_segments; ++s) {
-    const int64_t len = seg_len[s];
-    for (int64_t off = 0; off < len; off += kMaxCols) {  // full pieces, then the segment's remainder
+  for (int32_t s = 0; s < n_segments; ++s)
+    cut_segment(seg_len[s], best_pc, [&](int64_t off, int64_t cols) {
       fa_piece& p = pieces[k++];
       p.col = seg_col[s] + off;
       p.seg_off = off;
       p.seg = s;
-      p.n_cols = (int32_t)(len - off < kMaxCols ? len - off : kMaxCols);
-      p.reserved = 0;
-    }
-  }
-  // largest first (stable: equal pieces keep bucket order, so neighbouring blocks start on
-  // neighbouring columns): the dynamically claimed tail is made of the smallest pieces
+      p.n_cols = (int32_t)cols;
+      p.aux = 0;
+    });
+  // largest first (stable: equal pieces keep bucket order): the wide pieces lead and pair into
+  // groups of similar size, the narrow ones are claimed last, one at a time
   std::stable_sort(pieces, pieces + k, [](const fa_piece& a, const fa_piece& b) { return a.n_cols > b.n_cols; });
+  if (k > 0) pieces[0].aux = nwide;
   return FA_OK;
 }
 

@@ -149,12 +149,14 @@ typedef struct fa_piece {
   int64_t seg_off;
   int32_t seg;
   int32_t n_cols;
-  int64_t reserved;
+  int64_t aux; /* set by fa_rows_plan (pieces[0].aux: how many leading pieces are swept in
+                  row-major groups); pass the plan through unchanged                          */
 } fa_piece;
 
-/* HOST function: the work plan of fa_reduce_f32_rows: every segment cut into pieces of at most
- * 64 KiB of a row, largest first, and the grid to launch (grid_hint <= 0: the library's default
- * for the current device, never more than the piece count).  seg_col[s] must be a multiple of 4.
+/* HOST function: the work plan of fa_reduce_f32_rows: every segment cut into equal pieces of at
+ * most 64 KiB of a row (the width chosen so the wide pieces fill whole rounds of the grid),
+ * largest first, and the grid to launch (grid_hint <= 0: the library's default for the current
+ * device, never more than the work items).  seg_col[s] must be a multiple of 4.
  * pieces == NULL or cap too small: *n_pieces / *grid report the sizes (FA_ERR_SIZE when
  * pieces != NULL).                                                                             */
 int fa_rows_plan(int32_t n_segments, const int64_t* seg_col, const int64_t* seg_len, int32_t op,

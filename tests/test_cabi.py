@@ -155,25 +155,43 @@ def _plan(L, cols, lens, op=0, grid=0):
 
 @pytest.mark.parametrize("grid", [192, 7, 0])
 def test_rows_plan_covers_every_segment_once(L, grid):
-    """fa_rows_plan (host): pieces tile each segment exactly, stay inside one segment, start on
-    64-KiB boundaries within it (full pieces, then the remainder), largest first; the grid never
-    exceeds the piece count."""
+    """fa_rows_plan (host): pieces tile each segment exactly in equal 1-KiB-chunk multiples of at
+    most 64 KiB of a row, stay inside one segment, come largest first; pieces[0].aux counts the
+    leading wide pieces (> 2048 columns) the kernel sweeps in groups; the grid never exceeds the
+    work items."""
     lens = [1, 3, 4, 63, 64, 255, 256, 257, 8191, 8192, 8193, 2_359_296, 0, 100_003]
     cols, c = [], 0
     for n in lens:
         cols.append(c)
         c += -(-max(n, 1) // 64) * 64
-    pieces, g = _plan(L, cols, lens, grid=grid)
-    assert 1 <= g <= len(pieces) and (grid == 0 or g == min(grid, len(pieces)))
+    ctypes_pieces = _plan_raw(L, cols, lens, grid)
+    pieces, g = ctypes_pieces[0], ctypes_pieces[1]
     assert [p[3] for p in pieces] == sorted((p[3] for p in pieces), reverse=True)
+    nwide = ctypes_pieces[2]
+    assert nwide == sum(1 for p in pieces if p[3] > 2048)
+    assert all(p[3] > 2048 for p in pieces[:nwide])
+    claims = -(-nwide // 2) + (len(pieces) - nwide)
+    assert 1 <= g <= claims and (grid == 0 or g == min(grid, claims))
     for s, (c0, n) in enumerate(zip(cols, lens)):
         mine = sorted((p for p in pieces if p[2] == s), key=lambda p: p[1])
         assert sum(p[3] for p in mine) == n
         off = 0
         for col, seg_off, _, w in mine:
-            assert seg_off == off and col == c0 + off and 0 < w <= 16384 and seg_off % 16384 == 0
+            assert seg_off == off and col == c0 + off and 0 < w <= 16384 and seg_off % 256 == 0
             off += w
-    assert len([p for p in pieces if p[2] == lens.index(2_359_296)]) == 2_359_296 // 16384
+        if len(mine) > 1:  # equal cut: all but the last piece the same width
+            assert len({p[3] for p in mine[:-1]}) == 1 and mine[-1][3] <= mine[0][3]
+
+
+def _plan_raw(L, cols, lens, grid):
+    S = len(cols)
+    c = (ctypes.c_int64 * max(S, 1))(*cols)
+    n = (ctypes.c_int64 * max(S, 1))(*lens)
+    cnt, g = ctypes.c_int64(), ctypes.c_int32()
+    assert L.fa_rows_plan(S, c, n, 0, grid, None, 0, ctypes.byref(cnt), ctypes.byref(g)) == 0
+    arr = (na.Piece * max(cnt.value, 1))()
+    assert L.fa_rows_plan(S, c, n, 0, grid, arr, cnt.value, ctypes.byref(cnt), ctypes.byref(g)) == 0
+    return [(p.col, p.seg_off, p.seg, p.n_cols) for p in arr[: cnt.value]], g.value, (arr[0].aux if cnt.value else 0)
 
 
 def test_rows_plan_empty(L):

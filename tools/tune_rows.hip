@@ -98,3 +98,31 @@ extern "C" int tune_oob_probe(const float* src, uint32_t bytes, int off, float* 
   hipLaunchKernelGGL(oob_probe_kernel, dim3(1), dim3(64), 0, static_cast<hipStream_t>(stream), src, bytes, off, out);
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }
+
+// row-major grouped row-pointer kernel (fa_device.hpp reduce_kernel_segrows_rm<V, W, KG, DN>)
+namespace {
+template <int V, int W, int KG>
+int launch_rm(const float* const* rows, int n, const float* w, const fa_piece* pieces, int64_t npieces, int grid,
+              int* work, const Epi<double>& e, hipStream_t s) {
+  if (hipMemsetAsync(work, 0, sizeof(int), s) != hipSuccess) return -3;
+  hipLaunchKernelGGL((reduce_kernel_segrows_rm<AccF32, double, 0, V, W, KG, 16, true>), dim3((unsigned)grid),
+                     dim3(64 * W), 0, s, rows, n, w, pieces, npieces, work, e);
+  return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+}  // namespace
+
+extern "C" int tune_rows_rm_launch(int variant, const float* const* rows, int n, const float* w,
+                                   const fa_piece* pieces, int64_t npieces, int grid, int* work, double denom,
+                                   float* out32, void* stream) {
+  Epi<double> e{};
+  e.denom = denom;
+  e.out32 = out32;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  switch (variant) {
+    case 0: return launch_rm<8, 8, 2>(rows, n, w, pieces, npieces, grid, work, e, s);
+    case 1: return launch_rm<8, 8, 3>(rows, n, w, pieces, npieces, grid, work, e, s);
+    case 2: return launch_rm<8, 8, 4>(rows, n, w, pieces, npieces, grid, work, e, s);
+    case 3: return launch_rm<16, 4, 2>(rows, n, w, pieces, npieces, grid, work, e, s);
+    default: return -1;
+  }
+}

@@ -27,7 +27,7 @@ from flearn_amd import aggregator as agg  # noqa: E402
 from flearn_amd import layouts  # noqa: E402
 
 TUNE_LIB = REPO / "tools" / "libtune_rows.so"
-PIECE = np.dtype([("col", "<i8"), ("seg_off", "<i8"), ("seg", "<i4"), ("n_cols", "<i4"), ("reserved", "<i8")])
+PIECE = np.dtype([("col", "<i8"), ("seg_off", "<i8"), ("seg", "<i4"), ("n_cols", "<i4"), ("aux", "<i8")])
 CONFIGS = {"c2": ("resnet18", 100), "ns": ("resnet50", 100), "c4s": ("resnet18", 800)}
 
 
@@ -120,7 +120,20 @@ def main():
     kernels = {"v8d2w4_c32": (0, 32), "v16d1w4_c64": (1, 64), "v8d1w8_c64": (2, 64), "v8d2w8_c64": (3, 64),
                "v8d4w4_c32": (4, 32), "v4d4w4_c16": (5, 16), "v4d2w8_c32": (6, 32), "v16d2w4_c64": (7, 64),
                "v8d2w4_c16": (0, 16), "v16d1w4_c32": (1, 32)}
+    T.tune_rows_rm_launch.argtypes = T.tune_rows_launch.argtypes
     variants = {"stack": None, "lib": (None,) + lib_plan(segs, 0)}
+    # row-major grouped kernel: pieces of 64 KiB, largest first, pieces[0].aux = the wide ones
+    rm_kernels = {"rm_v8w8kg2": (0, 8), "rm_v8w8kg3": (1, 8), "rm_v8w8kg4": (2, 8), "rm_v16w4kg2": (3, 4)}
+    for kname, (kid, wv) in rm_kernels.items():
+        if a.only and not any(o in kname for o in a.only.split(",")):
+            continue
+        pcs = sorted(cut(segs, 64), key=lambda q: -q[3])
+        nwide = sum(1 for q in pcs if (q[3] + 3) // 4 > 64 * wv)
+        for g in (192, 256):
+            arr = np.zeros(len(pcs), PIECE)
+            for i, q in enumerate(pcs):
+                arr[i] = (q[0], q[1], q[2], q[3], nwide if i == 0 else 0)
+            variants[f"{kname}_g{g}"] = (100 + kid, arr, min(g, len(pcs)))
     for kname, (kid, c) in kernels.items():
         if a.only and not any(o in kname for o in a.only.split(",")):
             continue
@@ -144,8 +157,9 @@ def main():
             na.check(L.fa_reduce_f32_rows(ptr_d.data_ptr(), n, na.MODE_W32_DIV64, w.data_ptr(), float(n), t.data_ptr(),
                                           cnt, g, work.data_ptr(), None, out.data_ptr(), None, stream), k)
             return
-        rc = T.tune_rows_launch(kid, ptr_d.data_ptr(), n, w.data_ptr(), t.data_ptr(), cnt, g, work.data_ptr(), float(n),
-                                out.data_ptr(), stream)
+        fn = T.tune_rows_rm_launch if kid >= 100 else T.tune_rows_launch
+        rc = fn(kid % 100, ptr_d.data_ptr(), n, w.data_ptr(), t.data_ptr(), cnt, g, work.data_ptr(), float(n),
+                out.data_ptr(), stream)
         assert rc == 0, (k, rc)
 
     times = {k: [] for k in variants}
