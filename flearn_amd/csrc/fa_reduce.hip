@@ -105,6 +105,19 @@ int launch_rows(const float* stack, int64_t stride, int n, const typename P::w_t
 template <class P, typename T, int OP, int KG>
 int launch_rowmajor(const float* stack, int64_t stride, int n, const typename P::w_t* w, int64_t col0,
                     int64_t ncols, const Epi<T>& e, int64_t grid, hipStream_t s) {
+  // The same 64-KiB pieces either as 8 waves x 8 KiB or as 4 waves x 16 KiB.  With several groups
+  // per block (k >= 6) a plain mean streams ~1% faster on 4 waves (100 x 25.6 M: 86.6 vs 85.8%,
+  // 85.1 vs 83.7% on two boxes; 100 x 86.6 M: 83.2 vs 82.3%), with one group (C2, C4) it does not
+  // (84.2 vs 85.0%, 89.7 vs 89.8%) — profiles/r02/tune_nsgrid.  Fused epilogues keep 8 waves.
+  if constexpr (OP == FA_OP_MEAN && KG <= 4) {  // KG = 5 would not fit 5 x 16 quads of sums
+    const int64_t chunks = ((ncols + 3) / 4 + 63) / 64;
+    const int64_t k = (chunks + grid * kPieceChunks - 1) / (grid * kPieceChunks);
+    if (k >= 6) {
+      hipLaunchKernelGGL((reduce_kernel_rowmajor<P, T, OP, 16, 1, 4, KG, kNT>), dim3((unsigned)grid), dim3(256), 0,
+                         s, stack, stride, n, w, col0, ncols, e);
+      return launch_check();
+    }
+  }
   hipLaunchKernelGGL((reduce_kernel_rowmajor<P, T, OP, 8, 1, 8, KG, kNT>), dim3((unsigned)grid), dim3(512), 0, s,
                      stack, stride, n, w, col0, ncols, e);
   return launch_check();
