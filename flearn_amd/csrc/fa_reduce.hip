@@ -106,10 +106,12 @@ template <class P, typename T, int OP, int KG>
 int launch_rowmajor(const float* stack, int64_t stride, int n, const typename P::w_t* w, int64_t col0,
                     int64_t ncols, const Epi<T>& e, int64_t grid, hipStream_t s) {
   // The same 64-KiB pieces either as 8 waves x 8 KiB or as 4 waves x 16 KiB.  With several groups
-  // per block (k >= 6) a plain mean streams ~1% faster on 4 waves (100 x 25.6 M: 86.6 vs 85.8%,
-  // 85.1 vs 83.7% on two boxes; 100 x 86.6 M: 83.2 vs 82.3%), with one group (C2, C4) it does not
-  // (84.2 vs 85.0%, 89.7 vs 89.8%) — profiles/r02/tune_nsgrid.  Fused epilogues keep 8 waves.
-  if constexpr (OP == FA_OP_MEAN && KG <= 4) {  // KG = 5 would not fit 5 x 16 quads of sums
+  // per block (k >= 6) 4 waves stream ~1% faster — plain mean 100 x 25.6 M: 86.6 vs 85.8% and
+  // 85.1 vs 83.7% on two boxes, 100 x 86.6 M: 83.2 vs 82.3% (profiles/r02/tune_nsgrid); fused
+  // AVGM 100 x 25.6 M: 85.7 vs 84.4%, Adagrad 100 x 86.6 M: 85.1 vs 84.1% (profiles/r02/tune_epiw)
+  // — with one group (C2, C4) they do not (84.2 vs 85.0%, 89.7 vs 89.8%, AVGM 83.2 vs 83.4%).
+  // KG = 5 would not fit 5 x 16 quads of sums, nor Yogi's f64 epilogue 4 x 16 (144 spilled VGPRs)
+  if constexpr (KG <= 3 || (KG == 4 && !(OP == FA_OP_YOGI && sizeof(T) == 8))) {
     const int64_t chunks = ((ncols + 3) / 4 + 63) / 64;
     const int64_t k = (chunks + grid * kPieceChunks - 1) / (grid * kPieceChunks);
     if (k >= 6) {

@@ -326,6 +326,15 @@ int main(int argc, char** argv) {
     RM(16, 1, 4, 4, 224);
     RM(16, 1, 4, 3, 176);
   }
+  if (!strcmp(set, "epiw")) {  // fused epilogues: 8 waves x 8 KiB vs 4 waves x 16 KiB steps
+    RME(8, 1, 8, 4, 192, 2);
+    RME(8, 1, 8, 3, 192, 2);
+    RME(16, 1, 4, 4, 192, 2);
+    RME(16, 1, 4, 3, 192, 2);
+    RME(16, 1, 4, 2, 192, 2);
+    RME(16, 1, 4, 4, 192, 1);
+    RME(16, 1, 4, 3, 192, 1);
+  }
   if (!strcmp(set, "epib")) {  // piece epilogue: per-quad guarded loads (0) vs batched buffer loads of B slots
     RME(8, 1, 8, 4, 192, 0);
     RME(8, 1, 8, 4, 192, 2);
