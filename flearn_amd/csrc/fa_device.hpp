@@ -120,6 +120,7 @@ struct Epi {
   float alpha32;               // FA_OP_DYN: fl32(alpha) — alpha * (fp32 h) stays fp32
   float* out32;
   double* out64;
+  unsigned long long* trace;  // tuning only (reduce_kernel_rowmajor<..., TR = true>): phase timestamps
 };
 
 template <typename T>
@@ -660,28 +661,27 @@ __device__ __forceinline__ void rows_sweep(const R& row, uint32_t bytes, int n,
 //     (s_waitcnt vmcnt((D-1)*V) in the steady state, no drain per batch);
 //   * loads go through per-row buffer descriptors whose range check covers the window's end, so
 //     a partial last piece needs no per-lane branches (the slot offset rides in voffset, which
-//     the range check always covers); the one ragged quad (ncols % 4) goes to reduce_ragged.
+//     the range check always covers) and the window's ragged last quad (ncols % 4) is read in
+//     the same instructions (the range check is per dword).
 // The summation order (client list order, first product initialises the sum) is unchanged.
 template <class P, typename T, int OP, int V, int D, int W, bool NT>
 __device__ __forceinline__ void rows_piece(const float* __restrict__ stack, int64_t stride, int n,
                                            const typename P::w_t* __restrict__ w, int64_t col0,
                                            int64_t ncols, const Epi<T>& e, int64_t qb,
                                            int64_t qend) {
-  // the piece is quads [qb, qend), qend - qb <= 64*W*V
+  // the piece is quads [qb, qend), qend - qb <= 64*W*V; its columns, the window's ragged last
+  // quad (ncols % 4 != 0) included: the raw-buffer range check is per dword on gfx950
+  // (tools/probe_oob.py), so the missing elements of that quad load as 0 and are never stored
   typedef typename P::acc_t A;
   typedef typename vec4<A>::type AV;
-  const int64_t qfull = ncols / 4;
-  const int64_t left = (qend < qfull ? qend : qfull) - qb;
-  const int nq = left <= 0 ? 0 : (int)left;  // full quads of the piece
-  if (nq > 0) {
+  const int64_t cend = qend * 4 < ncols ? qend * 4 : ncols;
+  const int cols = cend > qb * 4 ? (int)(cend - qb * 4) : 0;
+  if (cols > 0) {
     AV acc[V];
     rows_sweep<P, V, D, W, NT>(StackRows{reinterpret_cast<const char*>(stack + col0 + qb * 4), stride * 4},
-                               (uint32_t)nq * 16u, n, w, acc);
-    finish_piece<T, OP, A, V, 64 * W, (V >= 2 ? 2 : V)>(e, qb, nq * 4, acc);
+                               (uint32_t)cols * 4u, n, w, acc);
+    finish_piece<T, OP, A, V, 64 * W, (V >= 2 ? 2 : V)>(e, qb, cols, acc);
   }
-  // the window's ragged last quad (ncols % 4 != 0), in the piece that holds it
-  if (threadIdx.x == 0 && qfull * 4 < ncols && qfull >= qb && qfull < qend)
-    reduce_ragged<P, T, OP>(stack + col0, stride, n, w, qfull, qfull + 1, ncols, e);
 }
 
 // Segmented row-pointer reduce (fa_reduce_f32_rows): uploads that are separate device tensors
@@ -958,6 +958,105 @@ __global__ __launch_bounds__(64 * W) void reduce_kernel_rows(const float* __rest
   }
 }
 
+// One group of a row-major block: KG of the block's pieces (slots g0 .. g0+KG-1, interleaved
+// over the grid as in reduce_kernel_rows), all rows swept once, then the group epilogue.
+template <class P, typename T, int OP, int V, int D, int W, int KG, bool NT, int EPIB, bool TR>
+__device__ __forceinline__ void rowmajor_group(const char* __restrict__ base, int64_t row_bytes, int n,
+                                               const typename P::w_t* __restrict__ w, int64_t g0, int64_t k,
+                                               int64_t pc, int64_t pieces, int64_t nquads, int64_t ncols,
+                                               int gi, const Epi<T>& e) {
+  static_assert(KG % D == 0, "pipeline depth must divide the group size");
+  typedef typename P::acc_t A;
+  typedef typename vec4<float>::type XV;
+  typedef typename vec4<A>::type AV;
+  const int64_t g = gridDim.x;
+  const int voff = (int)threadIdx.x * 16;
+  // piece j: columns [qb*4, qb*4 + cols), the window's ragged last quad included (per-dword
+  // range check: its missing elements load as 0 and are never stored)
+  int64_t qb[KG];
+  uint32_t bytes[KG];  // 4 x the piece's columns; 0: every access of this slot is dropped
+#pragma unroll
+  for (int j = 0; j < KG; ++j) {
+    const int64_t pj = blockIdx.x + (g0 + j) * g;  // interleaved pieces, as reduce_kernel_rows
+    qb[j] = pj * pc * 64;
+    const int64_t qe = qb[j] + pc * 64 < nquads ? qb[j] + pc * 64 : nquads;
+    const int64_t ce = qe * 4 < ncols ? qe * 4 : ncols;
+    const int64_t left = ce - qb[j] * 4;
+    bytes[j] = (pj < pieces && g0 + j < k && left > 0) ? (uint32_t)left * 4u : 0u;
+    if (bytes[j] == 0) qb[j] = 0;
+  }
+  XV x[D][V];
+  AV acc[KG][V];
+  // step s = (i, j), i = s / KG, j = s % KG; slot = j % D
+#define FA_RM_LOAD(slot, row, j)                                                                      \
+  {                                                                                                   \
+    const __amdgpu_buffer_rsrc_t r_ = row_rsrc(base + qb[j] * 16 + (int64_t)(row) * row_bytes, bytes[j]); \
+    _Pragma("unroll") for (int v = 0; v < V; ++v) x[slot][v] = buf_load_quad<NT>(r_, voff + v * 64 * W * 16, 0); \
+  }
+#pragma unroll
+  for (int d = 0; d < D; ++d) FA_RM_LOAD(d, 0, d);
+  // row 0: products initialise the sums
+#pragma unroll
+  for (int j = 0; j < KG; ++j) {
+    const typename P::w_t w0 = w[0];
+#pragma unroll
+    for (int v = 0; v < V; ++v) acc[j][v] = quad_mul<P>(w0, x[j % D][v]);
+    __builtin_amdgcn_sched_barrier(0);
+    if (j + D < KG) {
+      FA_RM_LOAD(j % D, 0, j + D);
+    } else if (n > 1) {
+      FA_RM_LOAD(j % D, 1, j + D - KG);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  int i = 1;
+  for (; i + 1 < n; ++i) {  // rows with a successor: every refill is a real step
+    const typename P::w_t wi = w[i];
+#pragma unroll
+    for (int j = 0; j < KG; ++j) {
+#pragma unroll
+      for (int v = 0; v < V; ++v) acc[j][v] = quad_axpy<P>(acc[j][v], wi, x[j % D][v]);
+      __builtin_amdgcn_sched_barrier(0);
+      if (j + D < KG) {
+        FA_RM_LOAD(j % D, i, j + D);
+      } else {
+        FA_RM_LOAD(j % D, i + 1, j + D - KG);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  if (i < n) {  // last row: refills only inside the row
+    const typename P::w_t wi = w[i];
+#pragma unroll
+    for (int j = 0; j < KG; ++j) {
+#pragma unroll
+      for (int v = 0; v < V; ++v) acc[j][v] = quad_axpy<P>(acc[j][v], wi, x[j % D][v]);
+      if (j + D < KG) FA_RM_LOAD(j % D, i, j + D);
+    }
+  }
+#undef FA_RM_LOAD
+  if constexpr (TR) {
+    if (threadIdx.x == 0 && gi < 7) e.trace[blockIdx.x * 16 + 1 + 2 * gi] = wall_clock64();
+  }
+  if constexpr (EPIB == 0) {  // per-quad epilogue (tuning reference: tools/tune_reduce.hip set "epib")
+#pragma unroll
+    for (int j = 0; j < KG; ++j) {
+#pragma unroll
+      for (int v = 0; v < V; ++v) {
+        const int q = v * 64 * W + (int)threadIdx.x;
+        const int valid = (int)(bytes[j] / 4) - q * 4;
+        if (valid > 0) finish_quad<T, OP, A>(e, (qb[j] + q) * 4, valid < 4 ? valid : 4, acc[j][v]);
+      }
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < KG; ++j) finish_piece<T, OP, A, V, 64 * W, EPIB>(e, qb[j], (int)(bytes[j] / 4), acc[j]);
+  }
+  if constexpr (TR) {
+    if (threadIdx.x == 0 && gi < 7) e.trace[blockIdx.x * 16 + 2 + 2 * gi] = wall_clock64();
+  }
+}
+
 // Row-major variant for blocks that own several pieces (k > 1: C2-C5-sized buckets).  The
 // column-major walk (reduce_kernel_rows: piece after piece, all rows each) starts every round of
 // pieces with the blocks out of step, and rounds after the first measured ~8% slower per row on
@@ -966,109 +1065,31 @@ __global__ __launch_bounds__(64 * W) void reduce_kernel_rows(const float* __rest
 // rolling register pipeline D steps deep (D divides KG, so every slot index is static).  The
 // whole grid then moves through the client rows together.  Per element the sum is still rows
 // 0..N-1 in order.
-template <class P, typename T, int OP, int V, int D, int W, int KG, bool NT, int EPIB = (V >= 2 ? 2 : V)>
+// TR (tools/tune_reduce.hip set "timeline"): wave 0 of every block stamps the 100-MHz wall clock
+// at its start and at each group's sweep end and epilogue end into e.trace[block * 16 + slot].
+template <class P, typename T, int OP, int V, int D, int W, int KG, bool NT, int EPIB = (V >= 2 ? 2 : V),
+          bool TR = false>
 __global__ __launch_bounds__(64 * W) void reduce_kernel_rowmajor(const float* __restrict__ stack,
                                                                  int64_t stride, int n,
                                                                  const typename P::w_t* __restrict__ w,
                                                                  int64_t col0, int64_t ncols, Epi<T> e) {
   static_assert(sizeof(typename P::x_t) == 4, "row pipeline is for 4-byte elements");
-  static_assert(KG % D == 0, "pipeline depth must divide the group size");
-  typedef typename P::acc_t A;
-  typedef typename vec4<float>::type XV;
-  typedef typename vec4<A>::type AV;
   const int64_t nquads = (ncols + 3) / 4;
-  const int64_t qfull = ncols / 4;
   const int64_t chunks = (nquads + 63) / 64;
   const int64_t g = gridDim.x;
   const int64_t k = (chunks + g * W * V - 1) / (g * W * V);  // pieces per block
   const int64_t pc = (chunks + g * k - 1) / (g * k);         // chunks per piece (<= W*V)
   const int64_t pieces = (chunks + pc - 1) / pc;
   const int64_t row_bytes = stride * 4;
-  const int voff = (int)threadIdx.x * 16;
   const char* base = reinterpret_cast<const char*>(stack + col0);
-  for (int64_t g0 = 0; g0 < k; g0 += KG) {  // groups of KG of this block's pieces
-    int64_t qb[KG];
-    uint32_t bytes[KG];
-    int nq[KG];
-#pragma unroll
-    for (int j = 0; j < KG; ++j) {
-      const int64_t pj = blockIdx.x + (g0 + j) * g;  // interleaved pieces, as reduce_kernel_rows
-      qb[j] = pj * pc * 64;
-      const int64_t qe = qb[j] + pc * 64 < nquads ? qb[j] + pc * 64 : nquads;
-      const int64_t left = (qe < qfull ? qe : qfull) - qb[j];
-      nq[j] = (pj < pieces && g0 + j < k && left > 0) ? (int)left : 0;
-      bytes[j] = (uint32_t)nq[j] * 16u;  // 0: every load of this slot is dropped by the range check
-      if (nq[j] == 0) qb[j] = 0;
-    }
-    XV x[D][V];
-    AV acc[KG][V];
-    // step s = (i, j), i = s / KG, j = s % KG; slot = j % D
-#define FA_RM_LOAD(slot, row, j)                                                                      \
-  {                                                                                                   \
-    const __amdgpu_buffer_rsrc_t r_ = row_rsrc(base + qb[j] * 16 + (int64_t)(row) * row_bytes, bytes[j]); \
-    _Pragma("unroll") for (int v = 0; v < V; ++v) x[slot][v] = buf_load_quad<NT>(r_, voff + v * 64 * W * 16, 0); \
+  if constexpr (TR) {
+    if (threadIdx.x == 0) e.trace[blockIdx.x * 16] = wall_clock64();
   }
-#pragma unroll
-    for (int d = 0; d < D; ++d) FA_RM_LOAD(d, 0, d);
-    // row 0: products initialise the sums
-#pragma unroll
-    for (int j = 0; j < KG; ++j) {
-      const typename P::w_t w0 = w[0];
-#pragma unroll
-      for (int v = 0; v < V; ++v) acc[j][v] = quad_mul<P>(w0, x[j % D][v]);
-      __builtin_amdgcn_sched_barrier(0);
-      if (j + D < KG) {
-        FA_RM_LOAD(j % D, 0, j + D);
-      } else if (n > 1) {
-        FA_RM_LOAD(j % D, 1, j + D - KG);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    int i = 1;
-    for (; i + 1 < n; ++i) {  // rows with a successor: every refill is a real step
-      const typename P::w_t wi = w[i];
-#pragma unroll
-      for (int j = 0; j < KG; ++j) {
-#pragma unroll
-        for (int v = 0; v < V; ++v) acc[j][v] = quad_axpy<P>(acc[j][v], wi, x[j % D][v]);
-        __builtin_amdgcn_sched_barrier(0);
-        if (j + D < KG) {
-          FA_RM_LOAD(j % D, i, j + D);
-        } else {
-          FA_RM_LOAD(j % D, i + 1, j + D - KG);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    }
-    if (i < n) {  // last row: refills only inside the row
-      const typename P::w_t wi = w[i];
-#pragma unroll
-      for (int j = 0; j < KG; ++j) {
-#pragma unroll
-        for (int v = 0; v < V; ++v) acc[j][v] = quad_axpy<P>(acc[j][v], wi, x[j % D][v]);
-        if (j + D < KG) FA_RM_LOAD(j % D, i, j + D);
-      }
-    }
-#undef FA_RM_LOAD
-    if constexpr (EPIB == 0) {  // per-quad epilogue (tuning reference: tools/tune_reduce.hip set "epib")
-#pragma unroll
-      for (int j = 0; j < KG; ++j) {
-#pragma unroll
-        for (int v = 0; v < V; ++v) {
-          const int q = v * 64 * W + (int)threadIdx.x;
-          if (q < nq[j]) finish_quad<T, OP, A>(e, (qb[j] + q) * 4, 4, acc[j][v]);
-        }
-      }
-    } else {
-#pragma unroll
-      for (int j = 0; j < KG; ++j) finish_piece<T, OP, A, V, 64 * W, EPIB>(e, qb[j], nq[j] * 4, acc[j]);
-    }
-  }
-  // the window's ragged last quad (ncols % 4 != 0): the block that owns its piece
-  if (threadIdx.x == 0 && qfull * 4 < ncols) {
-    const int64_t pr = qfull / (pc * 64);
-    if (pr % g == blockIdx.x) reduce_ragged<P, T, OP>(stack + col0, stride, n, w, qfull, qfull + 1, ncols, e);
-  }
+#define FA_RM_GROUP(KGX, G0, GI) \
+  rowmajor_group<P, T, OP, V, D, W, KGX, NT, EPIB, TR>(base, row_bytes, n, w, G0, k, pc, pieces, nquads, ncols, GI, e)
+  int gi = 0;
+  for (int64_t g0 = 0; g0 < k; g0 += KG) FA_RM_GROUP(KG, g0, gi++);
+#undef FA_RM_GROUP
 }
 
 // Column-blocked client stack: element (n, c) lives at ((c / B) * N + n) * B + c % B with

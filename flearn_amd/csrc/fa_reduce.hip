@@ -110,7 +110,7 @@ int launch_rowmajor(const float* stack, int64_t stride, int n, const typename P:
   // 85.1 vs 83.7% on two boxes, 100 x 86.6 M: 83.2 vs 82.3% (profiles/r02/tune_nsgrid); fused
   // AVGM 100 x 25.6 M: 85.7 vs 84.4%, Adagrad 100 x 86.6 M: 85.1 vs 84.1% (profiles/r02/tune_epiw)
   // — with one group (C2, C4) they do not (84.2 vs 85.0%, 89.7 vs 89.8%, AVGM 83.2 vs 83.4%).
-  // KG = 5 would not fit 5 x 16 quads of sums, nor Yogi's f64 epilogue 4 x 16 (144 spilled VGPRs)
+  // Yogi's f64 epilogue does not fit 4 x 16 quads of sums (144 spilled VGPRs)
   if constexpr (KG <= 3 || (KG == 4 && !(OP == FA_OP_YOGI && sizeof(T) == 8))) {
     const int64_t chunks = ((ncols + 3) / 4 + 63) / 64;
     const int64_t k = (chunks + grid * kPieceChunks - 1) / (grid * kPieceChunks);
@@ -126,7 +126,7 @@ int launch_rowmajor(const float* stack, int64_t stride, int n, const typename P:
 }
 
 // Row-major geometry for windows of several 64-KiB pieces per block (k >= 2): a grid near 192
-// blocks whose k splits into equal groups of KG in {4, 3, 2, 5} pieces (every step of a group is
+// blocks whose k splits into equal groups of KG in {4, 3, 2} pieces (every step of a group is
 // a real piece).  Returns false when no grid in [160, cus] gives such a k.
 bool rowmajor_geometry(int64_t chunks, int cus, int64_t target, int64_t* grid, int* kg) {
   const int64_t lo = 160 < cus ? 160 : cus, hi = cus;
@@ -136,8 +136,8 @@ bool rowmajor_geometry(int64_t chunks, int cus, int64_t target, int64_t* grid, i
       if (g < lo || g > hi || (d == 0 && sgn)) continue;
       const int64_t k = (chunks + g * kPieceChunks - 1) / (g * kPieceChunks);
       if (k < 2) return false;  // one piece per block: the column-major kernel
-      for (int c : {4, 3, 2, 5}) {
-        if (k % c == 0 && (c != 5 || k == 5)) {
+      for (int c : {4, 3, 2}) {  // (5 x 8 quads of sums + the pipeline do not fit 256 VGPRs)
+        if (k % c == 0) {
           *grid = g;
           *kg = c;
           return true;
@@ -163,8 +163,7 @@ int launch_reduce(const typename P::x_t* stack, int64_t stride, int n, const voi
         switch (kg) {
           case 2: return launch_rowmajor<P, T, OP, 2>(stack, stride, n, wt, col0, ncols, e, g, s);
           case 3: return launch_rowmajor<P, T, OP, 3>(stack, stride, n, wt, col0, ncols, e, g, s);
-          case 4: return launch_rowmajor<P, T, OP, 4>(stack, stride, n, wt, col0, ncols, e, g, s);
-          default: return launch_rowmajor<P, T, OP, 5>(stack, stride, n, wt, col0, ncols, e, g, s);
+          default: return launch_rowmajor<P, T, OP, 4>(stack, stride, n, wt, col0, ncols, e, g, s);
         }
       }
     }
@@ -297,6 +296,7 @@ int make_epi(const fa_epilogue* in, double denom, int n_reduced, float* out32, d
   e->prev = nullptr;
   e->v = nullptr;
   e->h = nullptr;
+  e->trace = nullptr;
   e->beta = e->eta = e->tau = e->beta2 = e->c = e->n = T(0);
   e->alpha32 = 0.f;
   e->out32 = out32;

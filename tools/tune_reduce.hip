@@ -149,6 +149,67 @@ Variant make_rowmajor(const float* stack, int64_t stride, int n, const float* w,
           true, {}};
 }
 
+// one traced launch of reduce_kernel_rowmajor<..., TR = true>: per group, the spread over blocks
+// of the sweep end and the epilogue end (us from the first block's start), and the epilogue length
+template <int V, int D, int W, int KG, int OP, typename T, int EB = 2>
+void timeline(const float* stack, int64_t stride, int n, const float* w, int64_t ncols, Epi<T> e, int64_t grid) {
+  const int64_t chunks = ((ncols + 3) / 4 + 63) / 64;
+  if (grid > chunks) grid = chunks;
+  const int64_t k = (chunks + grid * W * V - 1) / (grid * W * V);
+  const int groups = (int)std::min<int64_t>((k + KG - 1) / KG, 7);
+  unsigned long long* tr;
+  CK(hipMalloc(&tr, grid * 16 * 8));
+  std::vector<unsigned long long> h(grid * 16);
+  for (int rep = 0; rep < 2; ++rep) {
+    CK(hipMemset(tr, 0, grid * 16 * 8));
+    e.trace = tr;
+    hipLaunchKernelGGL((reduce_kernel_rowmajor<AccF32, T, OP, V, D, W, KG, true, EB, true>),
+                       dim3((unsigned)grid), dim3(64 * W), 0, 0, stack, stride, n, w, (int64_t)0, ncols, e);
+    CK(hipDeviceSynchronize());
+    CK(hipMemcpy(h.data(), tr, grid * 16 * 8, hipMemcpyDeviceToHost));
+    unsigned long long t0 = ~0ull;
+    for (int64_t b = 0; b < grid; ++b) t0 = std::min(t0, h[b * 16]);
+    auto stat = [&](int slot, const char* what) {
+      std::vector<double> us;
+      for (int64_t b = 0; b < grid; ++b)
+        if (h[b * 16 + slot]) us.push_back((h[b * 16 + slot] - t0) / 100.0);  // 100 MHz
+      if (us.empty()) return;
+      std::sort(us.begin(), us.end());
+      printf("  %-12s min %8.1f  p10 %8.1f  med %8.1f  p90 %8.1f  max %8.1f us\n", what, us[0],
+             us[us.size() / 10], us[us.size() / 2], us[us.size() * 9 / 10], us.back());
+    };
+    printf("timeline V%d D%d W%d KG%d g%lld k%lld op%d epib%d rep %d\n", V, D, W, KG, (long long)grid, (long long)k,
+           OP, EB, rep);
+    stat(0, "start");
+    {  // the last epilogue end per XCD (blocks are dispatched to the 8 XCDs round-robin)
+      const int last = 2 + 2 * (groups - 1);
+      printf("  end by XCD  ");
+      for (int x = 0; x < 8; ++x) {
+        double s = 0;
+        int c = 0;
+        for (int64_t b = x; b < grid; b += 8)
+          if (h[b * 16 + last]) s += (h[b * 16 + last] - t0) / 100.0, ++c;
+        printf(" %7.1f", c ? s / c : 0.0);
+      }
+      printf(" us (mean)\n");
+    }
+    for (int gi = 0; gi < groups; ++gi) {
+      char a[32], b2[32];
+      snprintf(a, sizeof a, "g%d sweep", gi);
+      snprintf(b2, sizeof b2, "g%d epi", gi);
+      stat(1 + 2 * gi, a);
+      stat(2 + 2 * gi, b2);
+      std::vector<double> d;
+      for (int64_t b = 0; b < grid; ++b)
+        if (h[b * 16 + 2 + 2 * gi]) d.push_back((h[b * 16 + 2 + 2 * gi] - h[b * 16 + 1 + 2 * gi]) / 100.0);
+      if (d.empty()) continue;
+      std::sort(d.begin(), d.end());
+      printf("  g%d epi len   min %8.1f  med %8.1f  max %8.1f us\n", gi, d[0], d[d.size() / 2], d.back());
+    }
+  }
+  CK(hipFree(tr));
+}
+
 template <int V, int U, int OP, typename T>
 Variant make_blocked(const float* stack, int n, const float* w, int64_t ncols, Epi<T> e, double bytes) {
   const int64_t B = 256 * V * 4;
@@ -325,6 +386,10 @@ int main(int argc, char** argv) {
     RM(16, 1, 4, 3, 208);
     RM(16, 1, 4, 4, 224);
     RM(16, 1, 4, 3, 176);
+  }
+  if (!strcmp(set, "timeline")) {  // phase timestamps of the product geometry (printed after the timing)
+    RM(16, 1, 4, 3, 192);
+    RM(16, 1, 4, 4, 192);
   }
   if (!strcmp(set, "epiw")) {  // fused epilogues: 8 waves x 8 KiB vs 4 waves x 16 KiB steps
     RME(8, 1, 8, 4, 192, 2);
@@ -522,6 +587,19 @@ int main(int argc, char** argv) {
     const double med = var.times[var.times.size() / 2], mn = var.times[0];
     const double gbs = var.bytes / 1e9 / (med / 1e3);
     printf("%-28s %10.1f %10.1f %10.1f %8.2f\n", var.name.c_str(), med * 1e3, mn * 1e3, gbs, gbs / 80.0);
+  }
+  if (!strcmp(set, "timeline")) {
+    const int64_t chunks = ((ncols + 3) / 4 + 63) / 64;
+    const int64_t kk = (chunks + 192 * 64 - 1) / (192 * 64);
+    if (op == FA_OP_AVGM) {
+      timeline<16, 1, 4, 3, FA_OP_AVGM, double>(stack, stride, n, w, ncols, e, 192);
+    } else if (op == FA_OP_ADAGRAD) {
+      timeline<16, 1, 4, 4, FA_OP_ADAGRAD, double>(stack, stride, n, w, ncols, e, 192);
+    } else if (kk % 3 == 0) {
+      timeline<16, 1, 4, 3, FA_OP_MEAN, double>(stack, stride, n, w, ncols, e, 192);
+    } else {
+      timeline<16, 1, 4, 4, FA_OP_MEAN, double>(stack, stride, n, w, ncols, e, 192);
+    }
   }
   return 0;
 }
