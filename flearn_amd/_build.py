@@ -44,8 +44,39 @@ def build_pyhost(force: bool = False, verbose: bool = False) -> Path:
     return PYHOST_OUT
 
 
+TORCHMETA_SOURCE = HERE / "csrc" / "fa_torchmeta.cpp"  # tensor-metadata walks (ctypes.PyDLL), not C ABI
+TORCHMETA_OUT = HERE / "lib" / "libfa_torchmeta.so"
+
+
+def build_torchmeta(force: bool = False, verbose: bool = False) -> Path:
+    """libfa_torchmeta.so: g++ against this torch's headers, linked to its libtorch_python /
+    libtorch / libc10 (rpath: the same image on the GPU box)."""
+    import sysconfig
+
+    import torch
+    from torch.utils.cpp_extension import include_paths
+
+    newest = max(TORCHMETA_SOURCE.stat().st_mtime, Path(__file__).stat().st_mtime)
+    if TORCHMETA_OUT.exists() and not force and TORCHMETA_OUT.stat().st_mtime >= newest:
+        return TORCHMETA_OUT
+    TORCHMETA_OUT.parent.mkdir(parents=True, exist_ok=True)
+    tmp = TORCHMETA_OUT.with_suffix(".so.tmp")
+    tlib = Path(torch.__file__).resolve().parent / "lib"
+    cmd = [os.environ.get("CXX", "g++"), "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall",
+           f"-D_GLIBCXX_USE_CXX11_ABI={int(torch._C._GLIBCXX_USE_CXX11_ABI)}",
+           f"-I{sysconfig.get_paths()['include']}"] + [f"-I{p}" for p in include_paths()] + [
+           str(TORCHMETA_SOURCE), f"-L{tlib}", "-ltorch_python", "-ltorch", "-lc10",
+           f"-Wl,-rpath,{tlib}", "-o", str(tmp)]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.run(cmd, check=True)
+    tmp.replace(TORCHMETA_OUT)
+    return TORCHMETA_OUT
+
+
 def build_native(force: bool = False, verbose: bool = False) -> Path:
     build_pyhost(force, verbose)
+    build_torchmeta(force, verbose)
     newest = max(p.stat().st_mtime for p in SOURCES + HOST_SOURCES + DEPS + HEADERS + [Path(__file__)])
     if OUT.exists() and not force and OUT.stat().st_mtime >= newest:
         return OUT

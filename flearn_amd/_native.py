@@ -17,13 +17,14 @@ from pathlib import Path
 import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 
 LIB_PATH = Path(__file__).resolve().parent / "lib" / "libflearn_amd.so"
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 FA_OK = 0
 FA_ERR_ARG, FA_ERR_ALIGN, FA_ERR_LAUNCH = -1, -2, -3
 FA_ERR_SIZE, FA_ERR_UNSUPPORTED, FA_ERR_DATA = -4, -5, -6
 MODE_W32_DIV64, MODE_W32_DIV32, MODE_W64 = 0, 1, 2
 OP_MEAN, OP_AVGM, OP_ADAGRAD, OP_YOGI, OP_ADAM, OP_DYN = 0, 1, 2, 3, 4, 5
+SRC_F64, SRC_I64, SRC_F32 = 0, 1, 2  # fa_gather_rows_f64 source kinds
 PREC_F32, PREC_F64 = 0, 1
 OP_BY_NAME = {"mean": OP_MEAN, "avgm": OP_AVGM, "adagrad": OP_ADAGRAD, "yogi": OP_YOGI, "adam": OP_ADAM, "dyn": OP_DYN}
 
@@ -39,6 +40,7 @@ EXPORTS = (
     "fa_rows_plan",
     "fa_reduce_f32_rows",
     "fa_gather_rows",
+    "fa_gather_rows_f64",
     "fa_fill_uniform_f32",
     "fa_b64_decoded_size",
     "fa_b64_decode",
@@ -91,8 +93,9 @@ PYHOST_PATH = LIB_PATH.parent / "libfa_pyhost.so"
 
 
 def load_pyhost():
-    """The Python-object pack helper (csrc/fa_pyhost.c), loaded with ctypes.PyDLL so it runs with
-    the GIL held (it releases it around its copies).  Raises NativeUnavailable."""
+    """The Python-object pack helper (csrc/fa_pyhost.c fa_py_pack_rows), loaded with
+    ctypes.PyDLL so it runs with the GIL held (it releases it around its copies).  Raises
+    NativeUnavailable."""
     global _pyhost
     with _lock:
         if _pyhost is None:
@@ -101,12 +104,39 @@ def load_pyhost():
                     f"{PYHOST_PATH} not built; run `python -c 'import __graft_entry__ as g; g.build()'`"
                 )
             L = ctypes.PyDLL(str(PYHOST_PATH))
-            P, I64 = ctypes.c_void_p, ctypes.c_int64
-            fn = L.fa_py_pack_rows
-            fn.argtypes = [ctypes.py_object, ctypes.py_object, I64, P, I64, I64]
-            fn.restype = ctypes.c_int
-            _pyhost = fn
+            P, I64, O = ctypes.c_void_p, ctypes.c_int64, ctypes.py_object
+            L.fa_py_pack_rows.argtypes = [O, O, I64, P, I64, I64]
+            L.fa_py_pack_rows.restype = ctypes.c_int
+            _pyhost = L
     return _pyhost
+
+
+_torchmeta = None
+TORCHMETA_PATH = LIB_PATH.parent / "libfa_torchmeta.so"
+
+
+def load_torchmeta():
+    """The tensor-metadata walks (csrc/fa_torchmeta.cpp: fa_tm_same_signature,
+    fa_tm_tensor_ptrs), loaded with ctypes.PyDLL (GIL held), or None when the library is not
+    built — they only speed up checks the callers can also do in Python."""
+    global _torchmeta
+    with _lock:
+        if _torchmeta is None:
+            if not TORCHMETA_PATH.exists():
+                _torchmeta = False
+            else:
+                try:
+                    L = ctypes.PyDLL(str(TORCHMETA_PATH))
+                except OSError:
+                    _torchmeta = False
+                else:
+                    O, P, I64 = ctypes.py_object, ctypes.c_void_p, ctypes.c_int64
+                    L.fa_tm_same_signature.argtypes = [O, O]
+                    L.fa_tm_same_signature.restype = ctypes.c_int
+                    L.fa_tm_tensor_ptrs.argtypes = [O, O, O, I64, P, O]
+                    L.fa_tm_tensor_ptrs.restype = ctypes.c_int
+                    _torchmeta = L
+    return _torchmeta or None
 
 
 def load(require_gpu: bool = False):
@@ -135,6 +165,7 @@ def load(require_gpu: bool = False):
                 "fa_reduce_f32_rows": ([P, I32, I32, P, D, P, I64, I32, P, ctypes.POINTER(Epilogue), P, P, P],
                                        ctypes.c_int),
                 "fa_gather_rows": ([P, I64, I32, I32, P, P, I32, P], ctypes.c_int),
+                "fa_gather_rows_f64": ([P, I64, I32, P, P, I32, P], ctypes.c_int),
                 "fa_fill_uniform_f32": ([P, I64, I32, I64, ctypes.c_uint64, I64, I64, P], ctypes.c_int),
                 "fa_b64_decoded_size": ([P, I64], I64),
                 "fa_b64_decode": ([P, I64, P, I64, I32], ctypes.c_int),

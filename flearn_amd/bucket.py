@@ -35,6 +35,8 @@ SMALL_BYTES = 4 << 20  # below this, host packing / unpacking runs on the callin
 
 _STORE = {KIND_F32: np.float32, KIND_F64: np.float64, KIND_I64: np.int64}
 _TORCH = {np.float32: torch.float32, np.float64: torch.float64, np.int64: torch.int64}
+# device-upload dtypes a group's row table takes, and their fa_gather_rows_f64 source kind
+_ROW_SOURCES = {torch.float64: {torch.float64: na.SRC_F64, torch.int64: na.SRC_I64, torch.float32: na.SRC_F32}}
 _NP = {torch.float32: np.float32, torch.float64: np.float64, torch.int64: np.int64}
 _FMT = {np.dtype(np.float32): ord("f"), np.dtype(np.float64): ord("d"), np.dtype(np.int64): ord("i")}
 
@@ -47,7 +49,7 @@ class _NativeRows:
     layouts...), and the caller then packs those rows from Python."""
 
     def __init__(self, pieces, hosts, w_local_lst, rows, memo=None):
-        self.fn = na.load_pyhost()
+        self.fn = na.load_pyhost().fa_py_pack_rows
         # plain dicts only (dict / OrderedDict, whose item lookup the C side reproduces)
         self.clients = [w if type(w) in (dict, collections.OrderedDict) else None for w in w_local_lst]
         hp = tuple((h.data_ptr(), h.stride(0)) for h in hosts)
@@ -137,6 +139,25 @@ def _raw_signature(w, keys):
         return None
 
 
+def _plain_dicts(w_local_lst) -> bool:
+    """Every upload is a dict / OrderedDict, whose item lookup the native walks reproduce."""
+    return all(type(w) in (dict, collections.OrderedDict) for w in w_local_lst)
+
+
+def _same_signature_native(w_local_lst, keys) -> bool:
+    """True when every client's (type, dtype, shape) per key equals client 0's, read from the
+    tensors' TensorImpl by csrc/fa_torchmeta.cpp (torch uploads; the same comparisons as
+    _raw_signature without torch's per-attribute dispatch); False when it differs or cannot tell
+    (numpy uploads, no library) — the caller then compares in Python."""
+    if len(w_local_lst) < 2 or not _plain_dicts(w_local_lst):
+        return False
+    L = na.load_torchmeta()
+    if L is None:
+        return False
+    lst = w_local_lst if type(w_local_lst) is list else list(w_local_lst)
+    return L.fa_tm_same_signature(lst, tuple(keys)) == 1
+
+
 def select_keys(w_local_lst, key_lst=None):
     """strategy.py:119-121: the keys common to every client when key_lst is None, else key_lst.
     Ordered by the first client's insertion order (the reference's order is set-hash order,
@@ -168,8 +189,11 @@ def make_plan(agg_weight_lst, w_local_lst, key_lst=None) -> BucketPlan:
         raise ValueError("agg_weight_lst and w_local_lst differ in length")
     keys = select_keys(w_local_lst, key_lst)
     sig0 = _raw_signature(w_local_lst[0], keys)
-    slow = [n for n in range(1, len(w_local_lst))
-            if sig0 is None or _raw_signature(w_local_lst[n], keys) != sig0]
+    if sig0 is not None and _same_signature_native(w_local_lst, keys):
+        slow = []
+    else:
+        slow = [n for n in range(1, len(w_local_lst))
+                if sig0 is None or _raw_signature(w_local_lst[n], keys) != sig0]
     ck = None
     if sig0 is not None and not slow:
         ck = (tuple(keys), sig0, len(w_local_lst), tuple(map(type, agg_weight_lst)), repr(list(agg_weight_lst)))
@@ -395,23 +419,38 @@ class Packer:
 
     def row_table(self, plan: BucketPlan, g: Group, w_local_lst, shards):
         """RowTable of device-resident uploads for bucket group g, or None when some value is
-        not a contiguous tensor of its dtype on the bucket's (single, whole-bucket) device."""
+        not a contiguous tensor of an accepted dtype on the bucket's (single, whole-bucket)
+        device.  Accepted: the store dtype; for the float64 group also int64 and float32 values
+        (BN num_batches_tracked), which fa_gather_rows_f64 converts as numpy's promotion does."""
         if len(shards) != 1 or shards[0].c0 != 0 or shards[0].c1 != g.stride:
             return None
         dev = shards[0].device
-        dt = _TORCH[g.store_dtype]
+        store = _TORCH[g.store_dtype]
+        accept = _ROW_SOURCES.get(store, {store: na.SRC_F64})
         segs = [s for s in g.segments if s.numel > 0]
+        w0 = w_local_lst[0]
+        dts = tuple(getattr(w0[s.key], "dtype", None) for s in segs)
+        if any(d not in accept for d in dts):
+            return None
+        src = [accept[d] for d in dts]
         ptrs = np.empty((len(segs), plan.n_clients), dtype=np.int64)
+        L = na.load_torchmeta()
+        if L is not None and _plain_dicts(w_local_lst):  # TensorImpl reads (csrc/fa_torchmeta.cpp)
+            keep = [None] * (len(segs) * plan.n_clients)
+            lst = w_local_lst if type(w_local_lst) is list else list(w_local_lst)
+            index = dev.index if dev.index is not None else torch.cuda.current_device()
+            if L.fa_tm_tensor_ptrs(lst, tuple(s.key for s in segs), dts, index, ptrs.ctypes.data, keep) == 0:
+                return RowTable(self, plan, g, segs, ptrs, keep, dev, src)
         keep = []
         for j, s in enumerate(segs):
             row = ptrs[j]
             for n, w in enumerate(w_local_lst):
                 t = w[s.key]
-                if t.dtype != dt or t.device != dev or not t.is_contiguous():
+                if t.dtype != dts[j] or t.device != dev or not t.is_contiguous():
                     return None
                 row[n] = t.data_ptr()
                 keep.append(t)
-        return RowTable(self, plan, g, segs, ptrs, keep, dev)
+        return RowTable(self, plan, g, segs, ptrs, keep, dev, src)
 
     def _wire_stack(self, g: Group, w_local_lst, device):
         from .wire import wire_device_stack
@@ -553,8 +592,10 @@ class RowTable:
     recorded after them is checked at the next use of the packer), so the caching allocator
     cannot hand their memory to another stream meanwhile."""
 
-    def __init__(self, packer: Packer, plan: BucketPlan, g: Group, segs, ptrs: np.ndarray, keep, device):
+    def __init__(self, packer: Packer, plan: BucketPlan, g: Group, segs, ptrs: np.ndarray, keep, device, src=None):
         self.packer, self.plan, self.group, self.segs = packer, plan, g, segs
+        self.src = tuple(src) if src is not None else (na.SRC_F64,) * len(segs)  # per segment
+        self.converts = any(k != na.SRC_F64 for k in self.src)  # some segment is not the store dtype
         self.device = torch.device(device)
         self.shape = (plan.n_clients, g.stride)
         self.aligned = bool(ptrs.size == 0 or not (ptrs % 16).any())
@@ -599,16 +640,23 @@ class RowTable:
         return hit
 
     def gather_into(self, stack: torch.Tensor) -> None:
-        """One launch: every (key, client) tensor into its segment of the device stack [N, stride]."""
+        """One launch: every (key, client) tensor into its segment of the device stack [N, stride]
+        (converted to float64 per segment when the float64 group holds int64 / float32 values)."""
         L = na.load()
-        mk = ("row_segs", self.group.kind, str(self.device))
+        mk = ("row_segs", self.group.kind, str(self.device), self.src)
         segs = self.plan.memo.get(mk)
         if segs is None:
-            t = np.array([s.offset for s in self.segs] + [s.numel for s in self.segs], dtype=np.int64)
+            cols = [s.offset for s in self.segs] + [s.numel for s in self.segs]
+            t = np.array(cols + (list(self.src) if self.converts else []), dtype=np.int64)
             segs = self.plan.memo[mk] = torch.from_numpy(t).to(self.device)
-        na.check(L.fa_gather_rows(stack.data_ptr(), stack.stride(0), self.shape[0], self.elem_size,
-                                  self.ptrs.data_ptr(), segs.data_ptr(), len(self.segs),
-                                  na.stream_handle(self.device)), "fa_gather_rows")
+        if self.converts:
+            na.check(L.fa_gather_rows_f64(stack.data_ptr(), stack.stride(0), self.shape[0], self.ptrs.data_ptr(),
+                                          segs.data_ptr(), len(self.segs), na.stream_handle(self.device)),
+                     "fa_gather_rows_f64")
+        else:
+            na.check(L.fa_gather_rows(stack.data_ptr(), stack.stride(0), self.shape[0], self.elem_size,
+                                      self.ptrs.data_ptr(), segs.data_ptr(), len(self.segs),
+                                      na.stream_handle(self.device)), "fa_gather_rows")
         self.release()
 
     def release(self) -> None:

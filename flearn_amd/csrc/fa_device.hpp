@@ -926,6 +926,27 @@ __global__ __launch_bounds__(kThreads) void gather_rows_kernel(E* __restrict__ s
   for (int64_t k = threadIdx.x; k < len; k += kThreads) dst[k] = src[k];
 }
 
+// fa_gather_rows_f64: the same into a float64 stack, segment s's source converted by kind
+// (segs[2*nseg + s]: FA_SRC_F64 copy, FA_SRC_I64 int64 -> double rounded to nearest, FA_SRC_F32).
+__global__ __launch_bounds__(kThreads) void gather_rows_f64_kernel(double* __restrict__ stack, int64_t stride, int n,
+                                                                   const void* const* __restrict__ rows,
+                                                                   const int64_t* __restrict__ segs, int nseg) {
+  const int s = blockIdx.x, i = blockIdx.y;
+  const int64_t col = segs[s], len = segs[nseg + s], kind = segs[2 * nseg + s];
+  const void* src = rows[(int64_t)s * n + i];
+  double* dst = stack + (int64_t)i * stride + col;
+  if (kind == FA_SRC_I64) {
+    const int64_t* x = static_cast<const int64_t*>(src);
+    for (int64_t k = threadIdx.x; k < len; k += kThreads) dst[k] = (double)x[k];
+  } else if (kind == FA_SRC_F32) {
+    const float* x = static_cast<const float*>(src);
+    for (int64_t k = threadIdx.x; k < len; k += kThreads) dst[k] = (double)x[k];
+  } else {
+    const double* x = static_cast<const double*>(src);
+    for (int64_t k = threadIdx.x; k < len; k += kThreads) dst[k] = x[k];
+  }
+}
+
 // Work split: the window's 1-KiB chunks are cut into equal pieces of pc <= W*V chunks, as many
 // as make k whole rounds of the grid (pc = ceil(chunks / (k * grid))), so every block sweeps k
 // pieces (the last one or two blocks one fewer) and the launch has no tail round.

@@ -619,6 +619,17 @@ int fa_gather_rows(void* stack, int64_t row_stride, int32_t n_clients, int32_t e
   return launch_check();
 }
 
+int fa_gather_rows_f64(double* stack, int64_t row_stride, int32_t n_clients, const void* const* rows,
+                       const int64_t* segs, int32_t n_segments, void* stream) {
+  if (n_clients < 0 || n_segments < 0 || row_stride < 0) return fail(FA_ERR_ARG, "bad gather sizes");
+  if (n_clients == 0 || n_segments == 0) return FA_OK;
+  if (!stack || !rows || !segs) return fail(FA_ERR_ARG, "null gather pointer");
+  if (n_clients > 65535) return fail(FA_ERR_ARG, "too many clients for one gather");
+  hipLaunchKernelGGL(gather_rows_f64_kernel, dim3((unsigned)n_segments, (unsigned)n_clients), dim3(kThreads), 0,
+                     static_cast<hipStream_t>(stream), stack, row_stride, n_clients, rows, segs, n_segments);
+  return launch_check();
+}
+
 int fa_fill_uniform_f32(float* dst, int64_t row_stride, int32_t n_rows, int64_t n_cols,
                         uint64_t seed, int64_t row_begin, int64_t col_global_begin, void* stream) {
   if (!dst || n_rows < 0 || n_cols < 0 || row_stride < n_cols) return fail(FA_ERR_ARG, "bad fill");

@@ -40,7 +40,7 @@ class _DictPack:
     value is not a C-contiguous array of the expected dtype (the caller then copies in Python)."""
 
     def __init__(self, lay, dtype, dst_ptr):
-        self.fn = na.load_pyhost()
+        self.fn = na.load_pyhost().fa_py_pack_rows
         item, fmt = np.dtype(dtype).itemsize, _FMT[np.dtype(dtype)]
         parts, cur, size = [], [], 0
         for k, _s, o, n in lay:

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define FA_ABI_VERSION 4
+#define FA_ABI_VERSION 5
 
 /* return codes */
 #define FA_OK 0
@@ -181,6 +181,18 @@ int fa_reduce_f32_rows(const float* const* rows, int32_t n_clients, int32_t mode
  * Any alignment (element-wise copies).                                                         */
 int fa_gather_rows(void* stack, int64_t row_stride, int32_t n_clients, int32_t elem_size,
                    const void* const* rows, const int64_t* segs, int32_t n_segments, void* stream);
+
+/* The same gather into a float64 stack, converting each segment's source elements as numpy's
+ * astype(np.float64) does (what np.multiply(w_local[k], agg_weight) does to an int64 or float32
+ * value before the float64 sum, strategy.py:124-126): segs = device int64 [3 * n_segments] =
+ * seg_col..., seg_len..., seg_src... with seg_src[s] one of FA_SRC_F64 (copied), FA_SRC_I64
+ * (rounded to nearest, as a C cast), FA_SRC_F32 (exact).  For BN num_batches_tracked (int64)
+ * of device uploads.                                                                          */
+#define FA_SRC_F64 0
+#define FA_SRC_I64 1
+#define FA_SRC_F32 2
+int fa_gather_rows_f64(double* stack, int64_t row_stride, int32_t n_clients, const void* const* rows,
+                       const int64_t* segs, int32_t n_segments, void* stream);
 
 /* Synthetic client data: dst[r*row_stride + c] = U(-1,1) from splitmix64 of
  * (seed, row_begin + r, col_global_begin + c) — the bench/test generator; the CPU oracle

@@ -45,6 +45,8 @@ def test_abi_version_and_constants(L):
     assert header_define("FA_MODE_W32_DIV64") == na.MODE_W32_DIV64
     assert header_define("FA_MODE_W32_DIV32") == na.MODE_W32_DIV32
     assert header_define("FA_MODE_W64") == na.MODE_W64
+    assert (header_define("FA_SRC_F64"), header_define("FA_SRC_I64"), header_define("FA_SRC_F32")) == (
+        na.SRC_F64, na.SRC_I64, na.SRC_F32)
     for op, v in na.OP_BY_NAME.items():
         assert header_define(f"FA_OP_{op.upper()}") == v
 
@@ -215,3 +217,7 @@ def test_rows_entry_points_validate(L):
     assert L.fa_gather_rows(FAKE, 64, 2, 2, FAKE, FAKE, 1, None) == err  # element size
     assert L.fa_gather_rows(FAKE, 64, 70000, 4, FAKE, FAKE, 1, None) == err
     assert L.fa_gather_rows(FAKE, 64, 0, 4, FAKE, FAKE, 1, None) == 0
+    assert L.fa_gather_rows_f64(FAKE, 64, 70000, FAKE, FAKE, 1, None) == err
+    assert L.fa_gather_rows_f64(FAKE, -1, 2, FAKE, FAKE, 1, None) == err
+    assert L.fa_gather_rows_f64(None, 64, 2, FAKE, FAKE, 1, None) == err
+    assert L.fa_gather_rows_f64(FAKE, 64, 2, FAKE, FAKE, 0, None) == 0

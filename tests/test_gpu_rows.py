@@ -43,8 +43,38 @@ def test_device_uploads_read_in_place(name, cuda):
     got = s.server(_upload(clients, g.weights()), 0)["w_glob"]
     packer = s.engine.packer
     assert packer.last_row_tables.get("f32") == "rows", packer.last_row_tables  # no pack copy
+    # int64 values of the float64 group (BN counters with float weights) take the converting
+    # gather, never per-tensor copy kernels
+    assert "copy" not in packer.last_row_tables.values(), packer.last_row_tables
     for k, w in g.output().items():
         assert bitwise_equal(_host(got[k]), np.asarray(w)), (name, k)
+
+
+def test_gather_rows_f64_converts_like_numpy(cuda):
+    """fa_gather_rows_f64: int64 -> float64 rounded to nearest as numpy's astype (values beyond
+    2**53 included), float32 exact, float64 copied; segments at any column offset."""
+    L = na.load()
+    n, stride = 3, 256
+    rng = np.random.default_rng(5)
+    big = np.array([2**53 + 1, 2**53 + 3, -(2**63), 2**63 - 1, -(2**53) - 1, 0, -1, 7], dtype=np.int64)
+    segs_host = []  # (col, values)
+    vals = [[big, rng.integers(-2**62, 2**62, 37, dtype=np.int64), rng.standard_normal(5).astype(np.float32),
+             rng.standard_normal(11)] for _ in range(n)]
+    cols = [0, 9, 101, 130]
+    srcs = [na.SRC_I64, na.SRC_I64, na.SRC_F32, na.SRC_F64]
+    dev_vals = [[torch.from_numpy(v).to(cuda) for v in row] for row in vals]
+    ptrs = np.array([[dev_vals[i][s].data_ptr() for i in range(n)] for s in range(4)], dtype=np.int64)
+    ptr_d = torch.from_numpy(ptrs.reshape(-1)).to(cuda)
+    segs = torch.tensor(cols + [len(v) for v in vals[0]] + srcs, dtype=torch.int64, device=cuda)
+    stack = torch.full((n, stride), -5.0, dtype=torch.float64, device=cuda)
+    na.check(L.fa_gather_rows_f64(stack.data_ptr(), stride, n, ptr_d.data_ptr(), segs.data_ptr(), 4,
+                                  na.stream_handle(cuda)), "gather")
+    got = stack.cpu().numpy()
+    for i in range(n):
+        want = np.full(stride, -5.0)
+        for c, v in zip(cols, vals[i]):
+            want[c : c + len(v)] = v.astype(np.float64)
+        assert bitwise_equal(got[i], want), i
 
 
 def test_unaligned_device_uploads_take_one_gather(cuda):

@@ -5,7 +5,8 @@
 Times, on the same synthetic data:
   stack    : fa_reduce_f32 over a packed [N, stride] device stack (bench.py's kernel),
   rows     : fa_reduce_f32_rows reading the N*K separate tensors in place (one launch),
-  server   : Strategy.server() on the dict uploads (pointer-table build + H2D + the rows launch),
+  server   : Strategy.server() on the full state_dict uploads, BN num_batches_tracked (int64)
+             included (plan + pointer tables + H2D + the rows launch + the float64 gather),
 and checks rows == stack bit for bit.  Prints one JSON line.
 """
 from __future__ import annotations
@@ -43,6 +44,7 @@ def main():
     p = layouts.fp32_elems(layout)
     x = torch.empty((n, stride), dtype=torch.float32, device=dev)
     agg.fill_uniform(x, seed=7)
+    counters = [(k, shape) for k, shape, dt in layouts.get(name) if dt == "i64"]  # BN num_batches_tracked
     clients = []  # per client one model buffer (generated in place: no copy kernels), keys are views
     for i in range(n):
         buf = torch.empty((1, stride), dtype=torch.float32, device=dev)
@@ -52,6 +54,8 @@ def main():
             m = int(np.prod(shape, dtype=np.int64))
             d[k] = buf[0, off : off + m].view(shape)
             off += -(-max(m, 1) // 64) * 64
+        for k, shape in counters:  # int64 with float weights: the float64 group (converting gather)
+            d[k] = torch.full(shape, i + 1, dtype=torch.int64, device=dev)
         clients.append(d)
     uploads = [{"agg_weight": 1.0, "params": c} for c in clients]
     s = AVG(output="device") if op == "mean" else AVGM(server_side=True, output="device")
@@ -78,6 +82,7 @@ def main():
     s.server(uploads, 0)
     plan = make_plan([1.0] * n, clients)
     table = s.engine.packer.row_table(plan, plan.f32, clients, s.engine.packer.shards(plan, "f32"))
+    path = dict(s.engine.packer.last_row_tables)
     out_rows = torch.empty(stride, dtype=torch.float32, device=dev)
     t_rows = ev_time(lambda: agg.reduce_stack(table, w, na.MODE_W32_DIV64, float(n), out32=out_rows, **epi), a.steps)
     if op == "mean":
@@ -93,13 +98,13 @@ def main():
         walls.append(time.perf_counter() - t0)
     algo = n * p * 4 + p * 4 + (0 if op == "mean" else p * 20)
     print(json.dumps({
-        "config": a.config, "clients": n, "params": p, "tensors_per_client": len(layout), "op": op,
+        "config": a.config, "clients": n, "params": p, "tensors_per_client": len(layout) + len(counters), "op": op,
         "stack_kernel_us": round(t_stack, 1), "rows_kernel_us": round(t_rows, 1),
         "stack_frac_of_8TBs": round(algo / t_stack / 8e6, 4), "rows_frac_of_8TBs": round(algo / t_rows / 8e6, 4),
         "rows_bit_equal_stack": same,
         "server_call_ms_median": round(float(np.median(walls)) * 1e3, 3),
         "server_call_ms_min": round(min(walls) * 1e3, 3),
-        "path": s.engine.packer.last_row_tables,
+        "path": path,
     }), flush=True)
 
 
