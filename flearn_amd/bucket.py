@@ -169,6 +169,9 @@ def select_keys(w_local_lst, key_lst=None):
                 if k not in w:
                     raise KeyError(k)
         return keys
+    k0 = w_local_lst[0].keys()
+    if all(w.keys() == k0 for w in w_local_lst[1:]):  # the usual case: one model, same keys (C-level set compare)
+        return list(k0)
     common = reduce(lambda a, b: a & b, [set(w.keys()) for w in w_local_lst])
     return [k for k in w_local_lst[0].keys() if k in common]
 
