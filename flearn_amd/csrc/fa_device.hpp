@@ -689,10 +689,9 @@ __device__ __forceinline__ void rows_piece(const float* __restrict__ stack, int6
 // is a column range of ONE segment, so every row of a piece is one contiguous range of one
 // tensor and gets one buffer descriptor; client order and epilogue are the row pipeline's.
 //   * scheduling: pieces come largest first; block b starts with piece b and then claims the
-//     next unclaimed one from a device counter (claimed at the START of its current piece, so
-//     the atomic's latency hides behind the sweep).  Blocks finish within about one small piece
-//     of each other whatever the mix of tensor sizes — a static split of 100 ResNet-sized
-//     uploads left a ~10% tail (tools/tune_rows.py);
+//     next unclaimed one from a device counter.  Blocks finish within about one small piece of
+//     each other whatever the mix of tensor sizes — a static split of 100 ResNet-sized uploads
+//     left a ~10% tail (tools/tune_rows.py);
 //   * narrow pieces (<= W KiB of a row: BN vectors, biases) are latency-bound, not
 //     bandwidth-bound: they take a one-quad-per-lane sweep V*D rows deep instead of D, so a
 //     64-element tensor of 100 clients costs ~7 HBM round trips instead of ~50.
@@ -828,7 +827,10 @@ __global__ __launch_bounds__(64 * W) void reduce_kernel_splitn(const float* __re
 // stay on neighbouring client rows as the stack kernel's do; the row pointer of the step after
 // the next one is fetched while the next is in flight (every index is static: j is unrolled).
 // Claims past the groups are the narrow pieces, one at a time, through the deep one-quad sweep.
-template <class P, typename T, int OP, int V, int W, int KG, int DN, bool NT>
+// TR (tools/tune_rows.hip): wave 0 of every block stamps the 100-MHz wall clock at each claim it
+// starts (e.trace[block * 32 + 1 + c], c < 30) and at its exit (slot 0), claim count in slot 31.
+// DS: steps in flight (1, or any divisor of KG: step s = (i, j) lives in slot j % DS).
+template <class P, typename T, int OP, int V, int W, int KG, int DN, bool NT, bool TR = false, int DS = 1>
 __global__ __launch_bounds__(64 * W) void reduce_kernel_segrows_rm(const float* const* __restrict__ rows, int n,
                                                                    const typename P::w_t* __restrict__ w,
                                                                    const fa_piece* __restrict__ pieces,
@@ -842,9 +844,18 @@ __global__ __launch_bounds__(64 * W) void reduce_kernel_segrows_rm(const float* 
   const int64_t claims = groups + (npieces - nwide);
   const int voff = (int)threadIdx.x * 16;
   int64_t t = blockIdx.x;
+  int nclaim = 0;
   while (t < claims) {
+    // the next claim: a group (hundreds of us) claims during its last row, so an idle block can
+    // take what is left meanwhile (claiming at the start reserved work behind a long group while
+    // blocks that had drawn short pieces ran dry: tools/tune_rows.py --trace); a narrow piece
+    // claims at its start, which hides the atomic behind its short sweep
     int claimed = 0;
-    if (threadIdx.x == 0) claimed = (int)gridDim.x + atomicAdd(next, 1);
+    if (t >= groups && threadIdx.x == 0) claimed = (int)gridDim.x + atomicAdd(next, 1);
+    if constexpr (TR) {
+      if (threadIdx.x == 0 && nclaim < 30) e.trace[blockIdx.x * 32 + 1 + nclaim] = wall_clock64();
+      ++nclaim;
+    }
     if (t < groups) {
       const float* const* rp[KG];
       int64_t ob[KG], col[KG];
@@ -862,32 +873,48 @@ __global__ __launch_bounds__(64 * W) void reduce_kernel_segrows_rm(const float* 
       }
       // row pointer of step (i, j); rows clamped (a step past the end is never loaded)
 #define FA_SRM_PTR(i, j) (reinterpret_cast<const char*>(rp[j][(i) < n ? (i) : n - 1]) + ob[j])
-#define FA_SRM_LOAD(p, j)                                                                                    \
+#define FA_SRM_LOAD(p, j, slot)                                                                              \
   {                                                                                                          \
     const __amdgpu_buffer_rsrc_t r_ = row_rsrc((p), bytes[j]);                                               \
-    _Pragma("unroll") for (int v = 0; v < V; ++v) x[v] = buf_load_quad<NT>(r_, voff + v * 64 * W * 16, 0); \
+    _Pragma("unroll") for (int v = 0; v < V; ++v) x[slot][v] = buf_load_quad<NT>(r_, voff + v * 64 * W * 16, 0); \
   }
+      static_assert(KG % DS == 0, "steps in flight must divide the group");
       AV acc[KG][V];
-      XV x[V];
-      const char* pn = FA_SRM_PTR(0, 0);
-      FA_SRM_LOAD(pn, 0);
-      pn = KG > 1 ? FA_SRM_PTR(0, 1 % KG) : FA_SRM_PTR(1, 0);
-      int i = 0;
-      for (; i < n; ++i) {
+      XV x[DS][V];
+#pragma unroll
+      for (int d = 0; d < DS; ++d) FA_SRM_LOAD(FA_SRM_PTR(d / KG, d % KG), d % KG, d);
+      const char* pn = FA_SRM_PTR(DS / KG, DS % KG);  // the pointer of the next step to load
+      // after consuming step (i, j): refill its slot with step (i, j) + DS, then fetch the pointer
+      // of the step after that one
+#define FA_SRM_REFILL(i, j)                                           \
+  __builtin_amdgcn_sched_barrier(0);                                  \
+  if ((i) + ((j) + DS) / KG < n) {                                    \
+    FA_SRM_LOAD(pn, ((j) + DS) % KG, (j) % DS);                       \
+    pn = FA_SRM_PTR((i) + ((j) + DS + 1) / KG, ((j) + DS + 1) % KG); \
+  }                                                                   \
+  __builtin_amdgcn_sched_barrier(0);
+      {  // row 0: the products initialise the sums (peeled: a select between the first product
+         // and the running sum kept both alive for every slot and spilled KG >= 3)
+        const typename P::w_t w0 = w[0];
+        if (n == 1 && threadIdx.x == 0) claimed = (int)gridDim.x + atomicAdd(next, 1);
+#pragma unroll
+        for (int j = 0; j < KG; ++j) {
+#pragma unroll
+          for (int v = 0; v < V; ++v) acc[j][v] = quad_mul<P>(w0, x[j % DS][v]);
+          FA_SRM_REFILL(0, j)
+        }
+      }
+      for (int i = 1; i < n; ++i) {
+        if (i == n - 1 && threadIdx.x == 0) claimed = (int)gridDim.x + atomicAdd(next, 1);
         const typename P::w_t wi = w[i];
 #pragma unroll
         for (int j = 0; j < KG; ++j) {
 #pragma unroll
-          for (int v = 0; v < V; ++v) acc[j][v] = i == 0 ? quad_mul<P>(wi, x[v]) : quad_axpy<P>(acc[j][v], wi, x[v]);
-          __builtin_amdgcn_sched_barrier(0);
-          if (j + 1 < KG || i + 1 < n) {  // the next step exists: (i, j+1) or (i+1, 0)
-            FA_SRM_LOAD(pn, (j + 1) % KG);
-            // the step after it: (i, j+2), (i+1, j+2-KG) or (i+2, 0)
-            pn = j + 2 < KG ? FA_SRM_PTR(i, j + 2) : (j + 2 - KG < KG ? FA_SRM_PTR(i + 1, (j + 2) % KG) : FA_SRM_PTR(i + 2, 0));
-          }
-          __builtin_amdgcn_sched_barrier(0);
+          for (int v = 0; v < V; ++v) acc[j][v] = quad_axpy<P>(acc[j][v], wi, x[j % DS][v]);
+          FA_SRM_REFILL(i, j)
         }
       }
+#undef FA_SRM_REFILL
 #undef FA_SRM_LOAD
 #undef FA_SRM_PTR
 #pragma unroll
@@ -911,6 +938,12 @@ __global__ __launch_bounds__(64 * W) void reduce_kernel_segrows_rm(const float* 
     __syncthreads();
     t = s_next;
     __syncthreads();
+  }
+  if constexpr (TR) {
+    if (threadIdx.x == 0) {
+      e.trace[blockIdx.x * 32] = wall_clock64();
+      e.trace[blockIdx.x * 32 + 31] = (unsigned long long)nclaim;
+    }
   }
 }
 

@@ -512,11 +512,12 @@ int fa_rows_plan(int32_t n_segments, const int64_t* seg_col, const int64_t* seg_
   for (int32_t s = 0; s < n_segments; ++s)
     if (seg_len[s] < 0 || seg_col[s] < 0 || seg_col[s] % 4 != 0)
       return fail(FA_ERR_ARG, "segment columns must be >= 0 and 4-aligned");
-  int64_t g = grid_hint > 0 ? grid_hint : (int64_t)(device_cus() * kSegBlocksPerCU + 0.5);
-  // Piece width: the widest (<= kSegPieceChunks) whose wide pieces make whole, or nearly whole,
-  // rounds of KG-piece groups over the grid — a group is the unit a block claims, and a last
-  // round of few groups leaves most blocks idle while it runs (~20% of a 100 x ResNet-50 launch
-  // at 64 KiB: 782 groups on 192 blocks)
+  const int64_t target = grid_hint > 0 ? grid_hint : (int64_t)(device_cus() * kSegBlocksPerCU + 0.5);
+  // Piece width and grid: the widest pieces (<= kSegPieceChunks) and a grid near the target
+  // whose KG-piece groups fill whole rounds — a group is the unit a block claims, and every slot
+  // of the last round left empty is a block idling through a whole group sweep (92% fill left
+  // 15 of 192 blocks idle for half of a 100 x ResNet-18 launch: tools/tune_rows.py --trace).
+  // A grid hint is taken as given.
   auto count = [&](int64_t pc, int64_t* nwide) {
     int64_t all = 0, wide = 0;
     for (int32_t s = 0; s < n_segments; ++s)
@@ -527,18 +528,22 @@ int fa_rows_plan(int32_t n_segments, const int64_t* seg_col, const int64_t* seg_
     *nwide = wide;
     return all;
   };
-  int64_t best_pc = kSegPieceChunks, best_fill = -1;
-  for (int64_t pc = kSegPieceChunks; pc >= kSegPieceChunks * 5 / 8; --pc) {
+  const int64_t glo = grid_hint > 0 ? target : target - target / 8, ghi = target;
+  int64_t best_pc = kSegPieceChunks, g = target, best_fill = -1;
+  for (int64_t pc = kSegPieceChunks; pc >= kSegPieceChunks * 5 / 8 && best_fill < 1000; --pc) {
     int64_t nwide = 0;
     count(pc, &nwide);
     const int64_t groups = (nwide + kSegKG - 1) / kSegKG;
-    const int64_t r = groups % g;
-    const int64_t fill = (groups == 0 || r == 0) ? 1000 : r * 1000 / g;  // busy share of the last round
-    if (fill > best_fill) {
-      best_fill = fill;
-      best_pc = pc;
+    for (int64_t gg = ghi; gg >= glo && gg >= 1; --gg) {
+      const int64_t rounds = (groups + gg - 1) / gg;
+      const int64_t fill = groups == 0 ? 1000 : groups * 1000 / (rounds * gg);  // busy share of the slots
+      if (fill > best_fill) {
+        best_fill = fill;
+        best_pc = pc;
+        g = gg;
+      }
+      if (fill >= 1000) break;
     }
-    if (fill >= 900) break;
   }
   int64_t nwide = 0;
   const int64_t total = count(best_pc, &nwide);

@@ -28,7 +28,8 @@ from flearn_amd import layouts  # noqa: E402
 
 TUNE_LIB = REPO / "tools" / "libtune_rows.so"
 PIECE = np.dtype([("col", "<i8"), ("seg_off", "<i8"), ("seg", "<i4"), ("n_cols", "<i4"), ("aux", "<i8")])
-CONFIGS = {"c2": ("resnet18", 100), "ns": ("resnet50", 100), "c4s": ("resnet18", 800)}
+CONFIGS = {"c2": ("resnet18", 100), "ns": ("resnet50", 100), "c4s": ("resnet18", 800),
+           "c2flat": ("flat:11699136", 100), "c2wide": ("flat:2359296x5", 100)}  # synthetic: big tensors only
 
 
 def cut(segs, max_chunks):
@@ -40,6 +41,50 @@ def cut(segs, max_chunks):
             out.append((col + off, off, s, w))
             off += w
     return out
+
+
+def product_plan(segs, pc, kg=2, wide_cols=64 * 8 * 4):
+    """fa_rows_plan's table for a given piece width pc (chunks): pieces cut as its cut_segment,
+    largest first (stable), pieces[0].aux = the wide ones."""
+    out = []
+    for s, (col, n) in enumerate(segs):
+        chunks = -(-n // 256)
+        if chunks == 0:
+            continue
+        npc = -(-chunks // pc)
+        per = -(-chunks // npc) * 256
+        off = 0
+        while off < n:
+            w = min(per, n - off)
+            out.append((col + off, off, s, w))
+            off += per
+    out.sort(key=lambda q: -q[3])
+    arr = np.zeros(len(out), PIECE)
+    for i, q in enumerate(out):
+        arr[i] = (q[0], q[1], q[2], q[3], 0)
+    if len(out):
+        arr[0]["aux"] = sum(1 for q in out if q[3] > wide_cols)
+    return arr
+
+
+def filled_plan(segs, kg, pmax=64, wv=8, target=192):
+    """The product planner's search (fa_rows_plan) for group size kg and pieces of at most pmax
+    chunks: the widest pieces and a grid in [target - target/8, target] whose groups fill whole
+    rounds.  Returns (table, grid)."""
+    best = None
+    for pc in range(pmax, pmax * 5 // 8 - 1, -1):
+        arr = product_plan(segs, pc, kg, wide_cols=64 * wv * 4)
+        groups = -(-int(arr[0]["aux"]) // kg) if len(arr) else 0
+        for g in range(target, target - target // 8 - 1, -1):
+            rounds = -(-groups // g)
+            fill = groups / (rounds * g) if groups else 1.0
+            if best is None or fill > best[0] + 1e-9:
+                best = (fill, arr, g)
+            if fill >= 1.0:
+                break
+        if best[0] >= 1.0:
+            break
+    return best[1], best[2]
 
 
 def block_major(per_block, kg=1):
@@ -79,11 +124,18 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--only", default="", help="comma list of kernel-name substrings ('lib' adds the library plan)")
+    ap.add_argument("--trace", action="store_true", help="per-block claim timeline of the product plan, then exit")
+    ap.add_argument("--plans", default="", help="comma list of PC:GRID piece-width/grid plans run through the "
+                    "product kernel (fa_reduce_f32_rows) beside its own plan")
     a = ap.parse_args()
     L = na.lib()
     name, n = CONFIGS[a.config]
     dev = torch.device("cuda", 0)
-    layout = [x for x in layouts.get(name) if x[2] == "f32"]
+    if name.startswith("flat:"):  # one (or k) equal fp32 tensors per client: every piece full width
+        m, _, k = name[5:].partition("x")
+        layout = [(f"t{i}", (int(m),), "f32") for i in range(int(k or 1))]
+    else:
+        layout = [x for x in layouts.get(name) if x[2] == "f32"]
     stride = layouts.padded_f32_stride(layout)
     p = layouts.fp32_elems(layout)
     x = torch.empty((n, stride), dtype=torch.float32, device=dev)
@@ -122,18 +174,20 @@ def main():
                "v8d2w4_c16": (0, 16), "v16d1w4_c32": (1, 32)}
     T.tune_rows_rm_launch.argtypes = T.tune_rows_launch.argtypes
     variants = {"stack": None, "lib": (None,) + lib_plan(segs, 0)}
+    for spec in filter(None, a.plans.split(",")):
+        pc, g = (int(x) for x in spec.split(":"))
+        variants[f"plan_pc{pc}_g{g}"] = (None, product_plan(segs, pc), g)
     # row-major grouped kernel: pieces of 64 KiB, largest first, pieces[0].aux = the wide ones
-    rm_kernels = {"rm_v8w8kg2": (0, 8), "rm_v8w8kg3": (1, 8), "rm_v8w8kg4": (2, 8), "rm_v16w4kg2": (3, 4)}
-    for kname, (kid, wv) in rm_kernels.items():
+    # name -> (kernel variant, waves, piece chunks = V * W KiB per row)
+    rm_kernels = {"rm_v8w8kg2": (0, 8, 64), "rm_v8w8kg3": (1, 8, 64), "rm_v8w8kg4": (2, 8, 64),
+                  "rm_v16w4kg2": (3, 4, 64), "rm_v8w8kg2ds2": (4, 8, 64), "rm_v8w8kg4ds2": (5, 8, 64),
+                  "rm_v16w4kg2ds2": (6, 4, 64), "rm_v4w8kg4ds2": (7, 8, 32), "rm_v4w8kg4ds4": (8, 8, 32)}
+    for kname, (kid, wv, pchunks) in rm_kernels.items():
         if a.only and not any(o in kname for o in a.only.split(",")):
             continue
-        pcs = sorted(cut(segs, 64), key=lambda q: -q[3])
-        nwide = sum(1 for q in pcs if (q[3] + 3) // 4 > 64 * wv)
-        for g in (192, 256):
-            arr = np.zeros(len(pcs), PIECE)
-            for i, q in enumerate(pcs):
-                arr[i] = (q[0], q[1], q[2], q[3], nwide if i == 0 else 0)
-            variants[f"{kname}_g{g}"] = (100 + kid, arr, min(g, len(pcs)))
+        kg = int(kname.split("kg")[1][0])
+        arr, g = filled_plan(segs, kg, pchunks, wv)
+        variants[f"{kname}_filled_g{g}"] = (100 + kid, arr, min(g, len(arr)))
     for kname, (kid, c) in kernels.items():
         if a.only and not any(o in kname for o in a.only.split(",")):
             continue
@@ -145,6 +199,10 @@ def main():
             variants[f"{kname}_g{g}"] = (kid, arr, min(g, len(pcs)))
     dev_tabs = {k: (v[0], torch.from_numpy(v[1].view(np.uint8)).to(dev), len(v[1]), v[2])
                 for k, v in variants.items() if v}
+    if a.trace:
+        out = torch.empty(stride, dtype=torch.float32, device=dev)
+        _trace(T, dev_tabs["lib"], ptr_d, n, w, work, out, dev, na.stream_handle(dev), segs, variants["lib"][1])
+        return
     out = torch.empty(stride, dtype=torch.float32, device=dev)
     stream = na.stream_handle(dev)
 
@@ -183,6 +241,36 @@ def main():
     for k, ts in times.items():
         print(json.dumps({"config": a.config, "alloc": a.alloc, "variant": k, "us_min": round(min(ts), 1),
                           "us_med": round(float(np.median(ts)), 1), "frac": round(algo / min(ts) / 8e6, 4)}), flush=True)
+
+
+def _trace(T, tab, ptr_d, n, w, work, out, dev, stream, segs, plan):
+    """Claim timeline of the product kernel on the product plan: when each block starts each of
+    its claims, how many it made, when it exits (us from the first block's first claim)."""
+    T.tune_rows_rm_trace.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+                                     ctypes.c_int, ctypes.c_void_p, ctypes.c_double, ctypes.c_void_p, ctypes.c_void_p,
+                                     ctypes.c_void_p]
+    _, t, cnt, g = tab
+    nwide = int(plan[0]["aux"]) if len(plan) else 0
+    print(json.dumps({"pieces": int(cnt), "wide": nwide, "groups": (nwide + 1) // 2, "narrow": int(cnt) - nwide,
+                      "grid": g, "wide_cols": [int(x) for x in np.unique(plan["n_cols"][:nwide])][:8]}), flush=True)
+    for rep in range(3):
+        tr = torch.zeros(g * 32, dtype=torch.int64, device=dev)
+        rc = T.tune_rows_rm_trace(ptr_d.data_ptr(), n, w.data_ptr(), t.data_ptr(), cnt, g, work.data_ptr(), float(n),
+                                  out.data_ptr(), tr.data_ptr(), stream)
+        assert rc == 0
+        torch.cuda.synchronize()
+        h = tr.view(g, 32).cpu().numpy().astype(np.float64)
+        t0 = h[:, 1][h[:, 1] > 0].min()
+        nclaim = h[:, 31].astype(int)
+        end = (h[:, 0] - t0) / 100.0
+        starts = [(h[b, 1 : 1 + min(nclaim[b], 30)] - t0) / 100.0 for b in range(g)]
+        first_narrow = []
+        q = lambda x: [round(float(np.percentile(x, p)), 1) for p in (0, 10, 50, 90, 100)]
+        print(json.dumps({"rep": rep, "claims_per_block": np.bincount(nclaim).tolist(),
+                          "end_us_p0_10_50_90_100": q(end),
+                          "claim2_start_us": q([s[1] for s in starts if len(s) > 1]),
+                          "claim3_start_us": q([s[2] for s in starts if len(s) > 2]),
+                          "last_claim_start_us": q([s[-1] for s in starts if len(s)])}), flush=True)
 
 
 def _segments_equal(out, want, segs):
