@@ -22,11 +22,20 @@ from flearn_amd import layouts  # noqa: E402
 from _refavg import ReferenceClientUpdate  # noqa: E402
 
 
-def model(lay, seed, dtype):
+def model(lay, seed, dtype, counters=True):
+    """One state_dict of the layout: float keys in `dtype`; with `counters` the BN
+    num_batches_tracked keys too — int64 arrays in a client's w_local, numpy float64 scalars in
+    the server's w_glob (what the reference's server mean makes of a 0-d int64 value)."""
     p = layouts.fp32_elems(lay)
     flat = np.random.default_rng(seed).standard_normal(p).astype(dtype)
     sd = layouts.synthetic_state_dict(lay, flat.astype(np.float32), counter=1)
-    return {k: v.astype(dtype) for k, v in sd.items() if isinstance(v, np.ndarray) and v.dtype == np.float32}
+    out = {}
+    for k, v in sd.items():
+        if v.dtype == np.float32:
+            out[k] = v.astype(dtype)
+        elif counters:
+            out[k] = v.copy() if dtype == np.float32 else np.float64(seed)
+    return out
 
 
 def main():
@@ -34,12 +43,14 @@ def main():
     ap.add_argument("--layout", default="resnet50")
     ap.add_argument("--rounds", type=int, default=4)
     ap.add_argument("--ref-rounds", type=int, default=2)
+    ap.add_argument("--no-counters", action="store_true", help="drop the BN num_batches_tracked keys")
     a = ap.parse_args()
     lay = layouts.get(a.layout)
-    w_local0 = model(lay, 1, np.float32)
-    globs = [model(lay, 10 + r, np.float64) for r in range(a.rounds)]
-    p = sum(v.size for v in w_local0.values())
-    res = {"layout": a.layout, "params": p}
+    w_local0 = model(lay, 1, np.float32, not a.no_counters)
+    globs = [model(lay, 10 + r, np.float64, not a.no_counters) for r in range(a.rounds)]
+    p = sum(v.size for v in w_local0.values() if v.dtype == np.float32)
+    res = {"layout": a.layout, "params": p, "keys": len(w_local0),
+           "int64_counters": sum(1 for v in w_local0.values() if v.dtype == np.int64)}
     for method in ("avgm", "adagrad"):
         s = flearn_amd.AVGM() if method == "avgm" else flearn_amd.OPT()
         fn = ((lambda wl, wg: s.mean_momentum(wl, wg, 0.9)) if method == "avgm"

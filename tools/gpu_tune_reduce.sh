@@ -10,6 +10,7 @@ T=$R/tools/tune_reduce
 case $SET in
   narrow) SHAPES="200:5849600:mean 200:1462400:mean 400:2924800:mean 400:731200:mean 800:1462400:mean 800:365632:mean 100:1462400:mean 100:365632:mean 100:3201280:mean" ;;
   nsgrid) SHAPES="100:25610176:mean 100:11699136:mean 100:86567680:mean 1000:11699136:mean" ;;
+  kgrid) SHAPES="100:25610176:avgm 100:25610176:mean 100:25610176:adagrad" ;;
   timeline) SHAPES="100:25610176:avgm 100:86567680:adagrad" ;;
   epiw) SHAPES="100:25610176:avgm 100:86567680:adagrad 100:11699136:avgm" ;;
   epib) SHAPES="100:25610176:avgm 100:86567680:adagrad 100:11699136:adagrad" ;;

@@ -391,6 +391,14 @@ int main(int argc, char** argv) {
     RM(16, 1, 4, 3, 192);
     RM(16, 1, 4, 4, 192);
   }
+  if (!strcmp(set, "kgrid")) {  // fewer, larger groups from a grid a few blocks off 192 (k = 8 / KG 4 at 196)
+    RM(16, 1, 4, 3, 192);
+    RM(16, 1, 4, 4, 196);
+    RM(16, 1, 4, 4, 200);
+    RM(16, 1, 4, 4, 208);
+    RM(16, 1, 4, 2, 192);
+    RM(8, 1, 8, 4, 196);
+  }
   if (!strcmp(set, "epiw")) {  // fused epilogues: 8 waves x 8 KiB vs 4 waves x 16 KiB steps
     RME(8, 1, 8, 4, 192, 2);
     RME(8, 1, 8, 3, 192, 2);
