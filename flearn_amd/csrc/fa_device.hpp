@@ -297,14 +297,24 @@ __device__ __forceinline__ vec4<float>::type buf_load_quad(__amdgpu_buffer_rsrc_
 // the previous quad's stores, before the next: 24 serial HBM round trips at every piece-group end
 // of the fused FedAVGM kernel.
 // ---------------------------------------------------------------------------------------------
+// Cache policy bits of the epilogue's state loads and result / state stores (2 = non-temporal).
+// Non-temporal stores: +1.6% on 100 x 25.6 M mean, +1.2% AVGM, +-0.1% Adagrad 100 x 86.6 M (5
+// interleaved passes each, tools/gpu_epi_aux2.sh, profiles/r02/tune_epiaux/); non-temporal state
+// loads were mixed (-1..-5% Adagrad) and stay cached.
+#ifndef FA_EPI_LOAD_AUX
+#define FA_EPI_LOAD_AUX 0
+#endif
+#ifndef FA_EPI_STORE_AUX
+#define FA_EPI_STORE_AUX 2
+#endif
 template <typename T>
 __device__ __forceinline__ typename vec4<T>::type buf_load_tquad(__amdgpu_buffer_rsrc_t r, int q) {
   if constexpr (sizeof(T) == 4) {
-    return __builtin_bit_cast(typename vec4<T>::type, __builtin_amdgcn_raw_buffer_load_b128(r, q * 16, 0, 0));
+    return __builtin_bit_cast(typename vec4<T>::type, __builtin_amdgcn_raw_buffer_load_b128(r, q * 16, 0, FA_EPI_LOAD_AUX));
   } else {
     typedef double d2 __attribute__((ext_vector_type(2)));
-    const d2 lo = __builtin_bit_cast(d2, __builtin_amdgcn_raw_buffer_load_b128(r, q * 32, 0, 0));
-    const d2 hi = __builtin_bit_cast(d2, __builtin_amdgcn_raw_buffer_load_b128(r, q * 32 + 16, 0, 0));
+    const d2 lo = __builtin_bit_cast(d2, __builtin_amdgcn_raw_buffer_load_b128(r, q * 32, 0, FA_EPI_LOAD_AUX));
+    const d2 hi = __builtin_bit_cast(d2, __builtin_amdgcn_raw_buffer_load_b128(r, q * 32 + 16, 0, FA_EPI_LOAD_AUX));
     return typename vec4<T>::type{lo[0], lo[1], hi[0], hi[1]};
   }
 }
@@ -312,12 +322,12 @@ __device__ __forceinline__ typename vec4<T>::type buf_load_tquad(__amdgpu_buffer
 template <typename T>
 __device__ __forceinline__ void buf_store_tquad(__amdgpu_buffer_rsrc_t r, int q, typename vec4<T>::type v) {
   if constexpr (sizeof(T) == 4) {
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, q * 16, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, q * 16, 0, FA_EPI_STORE_AUX);
   } else {
     typedef double d2 __attribute__((ext_vector_type(2)));
     const d2 lo = {v[0], v[1]}, hi = {v[2], v[3]};
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, lo), r, q * 32, 0, 0);
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, hi), r, q * 32 + 16, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, lo), r, q * 32, 0, FA_EPI_STORE_AUX);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, hi), r, q * 32 + 16, 0, FA_EPI_STORE_AUX);
   }
 }
 

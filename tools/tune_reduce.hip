@@ -391,6 +391,11 @@ int main(int argc, char** argv) {
     RM(16, 1, 4, 3, 192);
     RM(16, 1, 4, 4, 192);
   }
+  if (!strcmp(set, "epinT")) {  // product geometry; built twice (-DFA_EPI_STORE_AUX / LOAD_AUX) for the A/B
+    RM(16, 1, 4, 3, 192);
+    RM(16, 1, 4, 4, 192);
+    RM(8, 1, 8, 4, 192);
+  }
   if (!strcmp(set, "kgrid")) {  // fewer, larger groups from a grid a few blocks off 192 (k = 8 / KG 4 at 196)
     RM(16, 1, 4, 3, 192);
     RM(16, 1, 4, 4, 196);
