@@ -345,60 +345,95 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t col_rsrc(E* base, int64_t qbas
   return row_rsrc(reinterpret_cast<const void*>((uintptr_t)(((uint64_t)hi << 32) | lo)), n);
 }
 
+// The four descriptors of one piece's epilogue (state operands, results); a null array or, for
+// the plain mean, the state gets an empty range.
+template <typename T, int OP>
+struct EpiRsrc {
+  __amdgpu_buffer_rsrc_t rl, rv, r32, r64;
+  __device__ __forceinline__ EpiRsrc(const Epi<T>& e, int64_t qbase, int cols)
+      : rl(col_rsrc<const float>(OP == FA_OP_DYN ? e.h : e.prev, qbase, OP == FA_OP_MEAN ? 0 : cols)),
+        rv(col_rsrc<T>(e.v, qbase, OP == FA_OP_MEAN ? 0 : cols)),
+        r32(col_rsrc<float>(e.out32, qbase, cols)),
+        r64(col_rsrc<double>(e.out64, qbase, cols)) {}
+};
+
+// state operands of quad q (zeros for the plain mean, which has none)
+template <typename T, int OP>
+__device__ __forceinline__ void epi_load(const EpiRsrc<T, OP>& r, int q, typename vec4<float>::type& l,
+                                         typename vec4<T>::type& vv) {
+  if constexpr (OP != FA_OP_MEAN) {
+    l = buf_load_tquad<float>(r.rl, q);
+    vv = buf_load_tquad<T>(r.rv, q);
+  } else {
+    l = typename vec4<float>::type{0.f, 0.f, 0.f, 0.f};
+    vv = typename vec4<T>::type{T(0), T(0), T(0), T(0)};
+  }
+}
+
+// divide and update one quad: a = its sums, l / vv = its loaded state in, updated state out (l:
+// FedDyn's h), w = the new global values
+template <typename T, int OP, typename A>
+__device__ __forceinline__ void epi_compute(const Epi<T>& e, const typename vec4<A>::type a,
+                                            typename vec4<float>::type& l, typename vec4<T>::type& vv,
+                                            typename vec4<T>::type& w) {
+  if constexpr (OP == FA_OP_DYN) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const T g = (T)a[j] / e.denom;
+      const T d = g * e.n - vv[j];                  // delta_theta = w_glob*N - theta   dyn.py:20-21
+      const float hn = (float)((T)l[j] - e.c * d);  // h -= alpha/N * delta (fp32 h)    dyn.py:26
+      const float ah = e.alpha32 * hn;              // alpha * h stays fp32              dyn.py:33
+      w[j] = g - (T)ah;                             // w_glob - alpha*h                  dyn.py:33
+      l[j] = hn;
+      vv[j] = w[j];                                 // theta = w_glob                    dyn.py:34
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const T g = (T)a[j] / e.denom;  // np.divide(w_glob, np.sum(a))  strategy.py:127-129
+      T vj = vv[j];
+      w[j] = update<T, OP>(e, g, (T)l[j], vj);
+      vv[j] = vj;
+    }
+  }
+}
+
+// store quad q's updated state and results.  GUARD = false: the result stores are issued
+// unconditionally (a null out32 / out64 has an empty descriptor range, so they are dropped) and
+// the quad is one basic block.
+template <typename T, int OP, bool GUARD = true>
+__device__ __forceinline__ void epi_store(const Epi<T>& e, const EpiRsrc<T, OP>& r, int q,
+                                          const typename vec4<float>::type l, const typename vec4<T>::type vv,
+                                          const typename vec4<T>::type w) {
+  if constexpr (OP == FA_OP_DYN) buf_store_tquad<float>(r.rl, q, l);
+  if constexpr (OP != FA_OP_MEAN) buf_store_tquad<T>(r.rv, q, vv);
+  if (!GUARD || e.out32) buf_store_tquad<float>(r.r32, q, typename vec4<float>::type{(float)w[0], (float)w[1], (float)w[2], (float)w[3]});
+  if (!GUARD || e.out64) buf_store_tquad<double>(r.r64, q, typename vec4<double>::type{(double)w[0], (double)w[1], (double)w[2], (double)w[3]});
+}
+
+template <typename T, int OP, typename A, bool GUARD = true>
+__device__ __forceinline__ void epi_quad(const Epi<T>& e, const EpiRsrc<T, OP>& r, int q,
+                                         const typename vec4<A>::type a, typename vec4<float>::type l,
+                                         typename vec4<T>::type vv) {
+  typename vec4<T>::type w;
+  epi_compute<T, OP, A>(e, a, l, vv, w);
+  epi_store<T, OP, GUARD>(e, r, q, l, vv, w);
+}
+
 template <typename T, int OP, typename A, int V, int STEP, int B>
 __device__ __forceinline__ void finish_piece(const Epi<T>& e, int64_t qbase, int cols,
                                              const typename vec4<A>::type (&acc)[V]) {
   static_assert(V % B == 0, "batch must divide the slots");
   if (cols <= 0) return;
-  const __amdgpu_buffer_rsrc_t rl = col_rsrc<const float>(OP == FA_OP_DYN ? e.h : e.prev, qbase, OP == FA_OP_MEAN ? 0 : cols);
-  const __amdgpu_buffer_rsrc_t rv = col_rsrc<T>(e.v, qbase, OP == FA_OP_MEAN ? 0 : cols);
-  const __amdgpu_buffer_rsrc_t r32 = col_rsrc<float>(e.out32, qbase, cols);
-  const __amdgpu_buffer_rsrc_t r64 = col_rsrc<double>(e.out64, qbase, cols);
+  const EpiRsrc<T, OP> r(e, qbase, cols);
 #pragma unroll
   for (int b0 = 0; b0 < V; b0 += B) {
     typename vec4<float>::type l[B];
     typename vec4<T>::type vv[B];
 #pragma unroll
-    for (int b = 0; b < B; ++b) {
-      const int q = (int)threadIdx.x + (b0 + b) * STEP;
-      if constexpr (OP != FA_OP_MEAN) {
-        l[b] = buf_load_tquad<float>(rl, q);
-        vv[b] = buf_load_tquad<T>(rv, q);
-      } else {
-        l[b] = typename vec4<float>::type{0.f, 0.f, 0.f, 0.f};
-        vv[b] = typename vec4<T>::type{T(0), T(0), T(0), T(0)};
-      }
-    }
+    for (int b = 0; b < B; ++b) epi_load<T, OP>(r, (int)threadIdx.x + (b0 + b) * STEP, l[b], vv[b]);
 #pragma unroll
-    for (int b = 0; b < B; ++b) {
-      const int q = (int)threadIdx.x + (b0 + b) * STEP;
-      const typename vec4<A>::type a = acc[b0 + b];
-      typename vec4<T>::type w;
-      if constexpr (OP == FA_OP_DYN) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const T g = (T)a[j] / e.denom;
-          const T d = g * e.n - vv[b][j];                // delta_theta = w_glob*N - theta   dyn.py:20-21
-          const float hn = (float)((T)l[b][j] - e.c * d);  // h -= alpha/N * delta (fp32 h)    dyn.py:26
-          const float ah = e.alpha32 * hn;               // alpha * h stays fp32              dyn.py:33
-          w[j] = g - (T)ah;                              // w_glob - alpha*h                  dyn.py:33
-          l[b][j] = hn;
-          vv[b][j] = w[j];                               // theta = w_glob                    dyn.py:34
-        }
-        buf_store_tquad<float>(rl, q, l[b]);
-      } else {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const T g = (T)a[j] / e.denom;  // np.divide(w_glob, np.sum(a))  strategy.py:127-129
-          T vj = vv[b][j];
-          w[j] = update<T, OP>(e, g, (T)l[b][j], vj);
-          vv[b][j] = vj;
-        }
-      }
-      if constexpr (OP != FA_OP_MEAN) buf_store_tquad<T>(rv, q, vv[b]);
-      if (e.out32) buf_store_tquad<float>(r32, q, typename vec4<float>::type{(float)w[0], (float)w[1], (float)w[2], (float)w[3]});
-      if (e.out64) buf_store_tquad<double>(r64, q, typename vec4<double>::type{(double)w[0], (double)w[1], (double)w[2], (double)w[3]});
-    }
+    for (int b = 0; b < B; ++b) epi_quad<T, OP, A>(e, r, (int)threadIdx.x + (b0 + b) * STEP, acc[b0 + b], l[b], vv[b]);
   }
 }
 

@@ -73,6 +73,215 @@ __global__ __launch_bounds__(256) void roof_burst(const float* __restrict__ x, i
   }
 }
 
+namespace fa {
+// ---------------------------------------------------------------------------------------------
+// Tuning-only kernel (set "dfr", profiles/r02/tune_dfr/, DESIGN.md §4 finding 14 — measured slower
+// than the product's group-end epilogue, so it stays here and not in fa_device.hpp).
+// Row-major groups with DEFERRED epilogues (reduce_kernel_rowmajor_dfr).  In reduce_kernel_rowmajor
+// every block reaches its group end at the same moment (the grid moves through the client rows
+// together), so each group epilogue is a chip-wide burst of mixed state reads and result writes
+// at the copy rate (~5 TB/s, DESIGN.md §4 finding 11) with no client reads left to overlap.
+// Here a group's sums go to LDS instead (KG x 64 KiB per block: KG <= 2 within the CU's 160 KiB)
+// and its epilogue is spread over the NEXT group's sweep: in each of its first rows a lane finishes one quad
+// (state loads issued one unit ahead, then divide / update / store), so the state traffic rides
+// inside the client stream.  Only the last group's epilogue runs at the end.  Each lane reads
+// back only the LDS slots it wrote: no barrier.  Sums and epilogue arithmetic are those of
+// reduce_kernel_rowmajor, element for element.
+// ---------------------------------------------------------------------------------------------
+struct RmGeom {  // the interleaved piece plan of reduce_kernel_rowmajor
+  int64_t g, k, pc, pieces, nquads, ncols;
+  // slot s of this block: piece blockIdx.x + s*g, columns [qb*4, qb*4 + bytes/4)
+  __device__ __forceinline__ void piece(int64_t s, int64_t& qb, uint32_t& bytes) const {
+    const int64_t pj = blockIdx.x + s * g;
+    qb = pj * pc * 64;
+    const int64_t qe = qb + pc * 64 < nquads ? qb + pc * 64 : nquads;
+    const int64_t ce = qe * 4 < ncols ? qe * 4 : ncols;
+    const int64_t left = ce - qb * 4;
+    bytes = (s >= 0 && pj < pieces && s < k && left > 0) ? (uint32_t)left * 4u : 0u;
+    if (bytes == 0) qb = 0;
+  }
+};
+
+template <class P, typename T, int OP, int V, int W, int KGX, bool NT, int EPIB, int TM>
+__device__ __forceinline__ void dfr_group(const char* __restrict__ base, int64_t row_bytes, int n,
+                                          const typename P::w_t* __restrict__ w, const RmGeom& G,
+                                          int64_t g0, int64_t pg0, int pkg, bool last, const Epi<T>& e,
+                                          typename vec4<float>::type* stash) {
+  typedef typename P::acc_t A;
+  typedef typename vec4<float>::type XV;
+  typedef typename vec4<T>::type TV;
+  typedef typename vec4<A>::type AV;
+  constexpr int STEP = 64 * W;
+  const int voff = (int)threadIdx.x * 16;
+  int64_t qb[KGX];
+  uint32_t bytes[KGX];
+#pragma unroll
+  for (int j = 0; j < KGX; ++j) G.piece(g0 + j, qb[j], bytes[j]);
+  // the pending group (pkg pieces from slot pg0; pkg = 0: none): unit u = its piece u / V, slot u % V
+  int64_t pq0, pq1;
+  uint32_t pb0, pb1;
+  G.piece(pkg > 0 ? pg0 : -1, pq0, pb0);
+  G.piece(pkg > 1 ? pg0 + 1 : -1, pq1, pb1);
+  const int U = TM == 0 ? 0 : pkg * V;  // TM 0 (timing probe only): deferred epilogues dropped
+  XV tl, ta, rl;
+  TV tv, rv, rw;
+#define FA_DFR_ISSUE(uu)                                                          \
+  {                                                                               \
+    const int j_ = (uu) >= V;                                                     \
+    const int q_ = (int)threadIdx.x + ((uu) - j_ * V) * STEP;                     \
+    const EpiRsrc<T, OP> r_(e, j_ ? pq1 : pq0, (int)((j_ ? pb1 : pb0) / 4));      \
+    epi_load<T, OP>(r_, q_, tl, tv);                                              \
+    ta = stash[(uu) * STEP + (int)threadIdx.x];                                   \
+  }
+#define FA_DFR_FINISH(uu)                                                         \
+  {                                                                               \
+    const int j_ = (uu) >= V;                                                     \
+    const int q_ = (int)threadIdx.x + ((uu) - j_ * V) * STEP;                     \
+    const EpiRsrc<T, OP> r_(e, j_ ? pq1 : pq0, (int)((j_ ? pb1 : pb0) / 4));      \
+    epi_quad<T, OP, A, false>(e, r_, q_, ta, tl, tv);                             \
+  }
+#define FA_DFR_STORE(uu)  /* TM 2: the results of unit uu, computed a row earlier (uu < 0: none) */ \
+  {                                                                                         \
+    const int us_ = (uu) > 0 ? (uu) : 0;                                                    \
+    const int j_ = us_ >= V;                                                                \
+    const int q_ = (int)threadIdx.x + (us_ - j_ * V) * STEP;                                \
+    const EpiRsrc<T, OP> r_(e, j_ ? pq1 : pq0, (uu) < 0 ? 0 : (int)((j_ ? pb1 : pb0) / 4)); \
+    epi_store<T, OP, false>(e, r_, q_, rl, rv, rw);                                         \
+  }
+#define FA_DFR_LOAD(row, j)                                                                           \
+  {                                                                                                   \
+    const __amdgpu_buffer_rsrc_t r_ = row_rsrc(base + qb[j] * 16 + (int64_t)(row) * row_bytes, bytes[j]); \
+    _Pragma("unroll") for (int v = 0; v < V; ++v) x[v] = buf_load_quad<NT>(r_, voff + v * STEP * 16, 0); \
+  }
+  XV x[V];
+  AV acc[KGX][V];
+  int u = 0;
+  FA_DFR_LOAD(0, 0);
+  if (U > 0) FA_DFR_ISSUE(0);
+  // row 0: products initialise the sums
+#pragma unroll
+  for (int j = 0; j < KGX; ++j) {
+    const typename P::w_t w0 = w[0];
+#pragma unroll
+    for (int v = 0; v < V; ++v) acc[j][v] = quad_mul<P>(w0, x[v]);
+    __builtin_amdgcn_sched_barrier(0);
+    if (j + 1 < KGX) {
+      FA_DFR_LOAD(0, j + 1);
+    } else if (n > 1) {
+      FA_DFR_LOAD(1, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  // rows 1 .. U finish one pending unit each, between the row's last step and the next row's
+  // first refill (one basic block: the scheduling barriers keep that order; a unit's state loads
+  // were issued a row earlier and its stores go out before the refill, so no wait for the next
+  // step covers them); the remaining rows are the plain sweep
+#define FA_DFR_ROW(TRICKLE)                                                                    \
+  {                                                                                            \
+    const typename P::w_t wi = w[i];                                                           \
+    _Pragma("unroll") for (int j = 0; j < KGX; ++j) {                                          \
+      _Pragma("unroll") for (int v = 0; v < V; ++v) acc[j][v] = quad_axpy<P>(acc[j][v], wi, x[v]); \
+      __builtin_amdgcn_sched_barrier(0);                                                       \
+      if (j + 1 < KGX) {                                                                       \
+        FA_DFR_LOAD(i, j + 1);                                                                 \
+      } else {                                                                                 \
+        if (TRICKLE && TM == 1) {                                                              \
+          FA_DFR_FINISH(u);                                                                    \
+          ++u;                                                                                 \
+          FA_DFR_ISSUE(u < U ? u : U - 1);                                                     \
+          __builtin_amdgcn_sched_barrier(0);                                                   \
+        }                                                                                      \
+        if (TRICKLE && TM == 2) {                                                              \
+          FA_DFR_STORE(u - 1);                                                                 \
+          __builtin_amdgcn_sched_barrier(0);                                                   \
+        }                                                                                      \
+        FA_DFR_LOAD(i + 1, 0);                                                                 \
+        if (TRICKLE && TM == 2) {                                                              \
+          __builtin_amdgcn_sched_barrier(0);                                                   \
+          rl = tl;                                                                             \
+          rv = tv;                                                                             \
+          epi_compute<T, OP, A>(e, ta, rl, rv, rw);                                            \
+          ++u;                                                                                 \
+          FA_DFR_ISSUE(u < U ? u : U - 1);                                                     \
+        }                                                                                      \
+      }                                                                                        \
+      __builtin_amdgcn_sched_barrier(0);                                                       \
+    }                                                                                          \
+  }
+  int i = 1;
+  if (U > 0) {
+    for (; i + 1 < n && u < U; ++i) FA_DFR_ROW(true);
+  }
+  for (; i + 1 < n; ++i) FA_DFR_ROW(false);
+#undef FA_DFR_ROW
+  if (i < n) {  // last row: refills only inside the row
+    const typename P::w_t wi = w[i];
+#pragma unroll
+    for (int j = 0; j < KGX; ++j) {
+#pragma unroll
+      for (int v = 0; v < V; ++v) acc[j][v] = quad_axpy<P>(acc[j][v], wi, x[v]);
+      if (j + 1 < KGX) FA_DFR_LOAD(i, j + 1);
+    }
+  }
+  if (TM == 2 && u > 0) FA_DFR_STORE(u - 1);
+  // units the sweep had no rows left for (few clients)
+  while (u < U) {
+    FA_DFR_FINISH(u);
+    ++u;
+    if (u < U) FA_DFR_ISSUE(u);
+  }
+#undef FA_DFR_ISSUE
+#undef FA_DFR_FINISH
+#undef FA_DFR_STORE
+#undef FA_DFR_LOAD
+  if (last) {
+#pragma unroll
+    for (int j = 0; j < KGX; ++j) finish_piece<T, OP, A, V, STEP, EPIB>(e, qb[j], (int)(bytes[j] / 4), acc[j]);
+  } else {
+#pragma unroll
+    for (int j = 0; j < KGX; ++j) {
+#pragma unroll
+      for (int v = 0; v < V; ++v) stash[(j * V + v) * STEP + (int)threadIdx.x] = acc[j][v];
+    }
+  }
+}
+
+template <class P, typename T, int OP, int V, int W, int KG, bool NT, int TM = 2, int EPIB = 2>
+__global__ __launch_bounds__(64 * W) void reduce_kernel_rowmajor_dfr(const float* __restrict__ stack,
+                                                                     int64_t stride, int n,
+                                                                     const typename P::w_t* __restrict__ w,
+                                                                     int64_t col0, int64_t ncols, Epi<T> e) {
+  static_assert(sizeof(typename P::x_t) == 4 && sizeof(typename P::acc_t) == 4, "fp32 sums only");
+  static_assert(KG == 1 || KG == 2, "KG x 64 KiB of sums must fit the CU's LDS");
+  static_assert(V * W == 64, "64-KiB pieces");
+  __shared__ typename vec4<float>::type stash[KG * V * 64 * W];
+  RmGeom G;
+  G.nquads = (ncols + 3) / 4;
+  const int64_t chunks = (G.nquads + 63) / 64;
+  G.g = gridDim.x;
+  G.k = (chunks + G.g * W * V - 1) / (G.g * W * V);
+  G.pc = (chunks + G.g * G.k - 1) / (G.g * G.k);
+  G.pieces = (chunks + G.pc - 1) / G.pc;
+  G.ncols = ncols;
+  const char* base = reinterpret_cast<const char*>(stack + col0);
+  const int64_t row_bytes = stride * 4;
+  int64_t pg0 = 0;
+  int pkg = 0;
+  for (int64_t g0 = 0; g0 < G.k; g0 += KG) {
+    const bool last = g0 + KG >= G.k;
+    if (G.k - g0 >= KG) {
+      dfr_group<P, T, OP, V, W, KG, NT, EPIB, TM>(base, row_bytes, n, w, G, g0, pg0, pkg, last, e, stash);
+      pkg = KG;
+    } else {
+      dfr_group<P, T, OP, V, W, 1, NT, EPIB, TM>(base, row_bytes, n, w, G, g0, pg0, pkg, last, e, stash);
+      pkg = 1;
+    }
+    pg0 = g0;
+  }
+}
+
+}  // namespace fa
+
 struct Variant {
   std::string name;
   double bytes;
@@ -147,6 +356,21 @@ Variant make_rowmajor(const float* stack, int64_t stride, int n, const float* w,
                                dim3(64 * W), 0, 0, stack, stride, n, w, (int64_t)0, ncols, e);
           },
           true, {}};
+}
+
+template <int V, int W, int KG, int OP, typename T, int TM>
+Variant make_dfr(const float* stack, int64_t stride, int n, const float* w, int64_t ncols, Epi<T> e,
+                 double bytes, int64_t grid) {
+  const int64_t chunks = ((ncols + 3) / 4 + 63) / 64;
+  if (grid > chunks) grid = chunks;
+  char name[96];
+  snprintf(name, sizeof name, "rm-dfr V%d W%d KG%d g%lld tm%d", V, W, KG, (long long)grid, TM);
+  return {name, bytes,
+          [=] {
+            hipLaunchKernelGGL((reduce_kernel_rowmajor_dfr<AccF32, T, OP, V, W, KG, true, TM>), dim3((unsigned)grid),
+                               dim3(64 * W), 0, 0, stack, stride, n, w, (int64_t)0, ncols, e);
+          },
+          TM != 0, {}};
 }
 
 // one traced launch of reduce_kernel_rowmajor<..., TR = true>: per group, the spread over blocks
@@ -372,6 +596,24 @@ int main(int argc, char** argv) {
   vs.push_back(op == FA_OP_AVGM      ? make_rowmajor<V, D, W, KG, FA_OP_AVGM, double, EB>(stack, stride, n, w, ncols, e, bytes, G)   \
                : op == FA_OP_ADAGRAD ? make_rowmajor<V, D, W, KG, FA_OP_ADAGRAD, double, EB>(stack, stride, n, w, ncols, e, bytes, G) \
                                      : make_rowmajor<V, D, W, KG, FA_OP_MEAN, double, EB>(stack, stride, n, w, ncols, e, bytes, G))
+#define DFR(V, W, KG, G, TM)                                                                               \
+  vs.push_back(op == FA_OP_AVGM      ? make_dfr<V, W, KG, FA_OP_AVGM, double, TM>(stack, stride, n, w, ncols, e, bytes, G)   \
+               : op == FA_OP_ADAGRAD ? make_dfr<V, W, KG, FA_OP_ADAGRAD, double, TM>(stack, stride, n, w, ncols, e, bytes, G) \
+                                     : make_dfr<V, W, KG, FA_OP_MEAN, double, TM>(stack, stride, n, w, ncols, e, bytes, G))
+  if (!strcmp(set, "dfr")) {  // deferred group epilogues (LDS-stashed sums) vs the product geometries
+    RM(16, 1, 4, 3, 192);
+    RM(16, 1, 4, 4, 192);
+    RM(8, 1, 8, 4, 192);
+    RM(16, 1, 4, 4, 196);
+    RM(16, 1, 4, 2, 196);
+    RM(8, 1, 8, 2, 196);
+    DFR(16, 4, 2, 196, 2);
+    DFR(16, 4, 2, 196, 0);
+    DFR(8, 8, 2, 196, 2);
+    DFR(8, 8, 2, 196, 0);
+    DFR(8, 8, 1, 192, 2);
+    DFR(8, 8, 1, 192, 0);
+  }
   if (!strcmp(set, "nsgrid")) {  // north-star shape: group size / grid / piece width
     RM(8, 1, 8, 3, 192);
     RM(8, 1, 8, 3, 208);
