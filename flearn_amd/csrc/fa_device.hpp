@@ -875,7 +875,8 @@ __global__ __launch_bounds__(64 * W) void reduce_kernel_splitn(const float* __re
 // TR (tools/tune_rows.hip): wave 0 of every block stamps the 100-MHz wall clock at each claim it
 // starts (e.trace[block * 32 + 1 + c], c < 30) and at its exit (slot 0), claim count in slot 31.
 // DS: steps in flight (1, or any divisor of KG: step s = (i, j) lives in slot j % DS).
-template <class P, typename T, int OP, int V, int W, int KG, int DN, bool NT, bool TR = false, int DS = 1>
+template <class P, typename T, int OP, int V, int W, int KG, int DN, bool NT, bool TR = false, int DS = 1,
+          bool SG = false>
 __global__ __launch_bounds__(64 * W) void reduce_kernel_segrows_rm(const float* const* __restrict__ rows, int n,
                                                                    const typename P::w_t* __restrict__ w,
                                                                    const fa_piece* __restrict__ pieces,
@@ -890,13 +891,18 @@ __global__ __launch_bounds__(64 * W) void reduce_kernel_segrows_rm(const float* 
   const int voff = (int)threadIdx.x * 16;
   int64_t t = blockIdx.x;
   int nclaim = 0;
+  // SG (static groups, tuning): block b takes groups b, b + grid, ... in lockstep and claims only
+  // the narrow pieces, numbered from max(groups, grid)
+  const int64_t nbase = SG && groups > (int64_t)gridDim.x ? groups : (int64_t)gridDim.x;
+#define FA_SRM_CLAIM() \
+  ((SG && t < groups && t + (int64_t)gridDim.x < groups) ? (int)(t + gridDim.x) : (int)nbase + atomicAdd(next, 1))
   while (t < claims) {
     // the next claim: a group (hundreds of us) claims during its last row, so an idle block can
     // take what is left meanwhile (claiming at the start reserved work behind a long group while
     // blocks that had drawn short pieces ran dry: tools/tune_rows.py --trace); a narrow piece
     // claims at its start, which hides the atomic behind its short sweep
     int claimed = 0;
-    if (t >= groups && threadIdx.x == 0) claimed = (int)gridDim.x + atomicAdd(next, 1);
+    if (t >= groups && threadIdx.x == 0) claimed = FA_SRM_CLAIM();
     if constexpr (TR) {
       if (threadIdx.x == 0 && nclaim < 30) e.trace[blockIdx.x * 32 + 1 + nclaim] = wall_clock64();
       ++nclaim;
@@ -941,7 +947,7 @@ __global__ __launch_bounds__(64 * W) void reduce_kernel_segrows_rm(const float* 
       {  // row 0: the products initialise the sums (peeled: a select between the first product
          // and the running sum kept both alive for every slot and spilled KG >= 3)
         const typename P::w_t w0 = w[0];
-        if (n == 1 && threadIdx.x == 0) claimed = (int)gridDim.x + atomicAdd(next, 1);
+        if (n == 1 && threadIdx.x == 0) claimed = FA_SRM_CLAIM();
 #pragma unroll
         for (int j = 0; j < KG; ++j) {
 #pragma unroll
@@ -950,7 +956,7 @@ __global__ __launch_bounds__(64 * W) void reduce_kernel_segrows_rm(const float* 
         }
       }
       for (int i = 1; i < n; ++i) {
-        if (i == n - 1 && threadIdx.x == 0) claimed = (int)gridDim.x + atomicAdd(next, 1);
+        if (i == n - 1 && threadIdx.x == 0) claimed = FA_SRM_CLAIM();
         const typename P::w_t wi = w[i];
 #pragma unroll
         for (int j = 0; j < KG; ++j) {
@@ -984,6 +990,7 @@ __global__ __launch_bounds__(64 * W) void reduce_kernel_segrows_rm(const float* 
     t = s_next;
     __syncthreads();
   }
+#undef FA_SRM_CLAIM
   if constexpr (TR) {
     if (threadIdx.x == 0) {
       e.trace[blockIdx.x * 32] = wall_clock64();

@@ -120,7 +120,7 @@ def lib_plan(segs, g):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
-    ap.add_argument("--alloc", default="views", choices=("views", "clones"))
+    ap.add_argument("--alloc", default="views", choices=("views", "clones", "stack"))
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--only", default="", help="comma list of kernel-name substrings ('lib' adds the library plan)")
@@ -148,7 +148,10 @@ def main():
     ptrs = np.empty((len(segs), n), np.int64)
     keep = []
     for i in range(n):
-        if a.alloc == "views":
+        if a.alloc == "stack":  # the row pointers point into the client stack itself
+            for j, (c0, m) in enumerate(segs):
+                ptrs[j, i] = x[i, c0:].data_ptr()
+        elif a.alloc == "views":
             buf = torch.empty((1, stride), dtype=torch.float32, device=dev)
             agg.fill_uniform(buf, seed=7, row_begin=i)
             for j, (c0, m) in enumerate(segs):
@@ -181,7 +184,8 @@ def main():
     # name -> (kernel variant, waves, piece chunks = V * W KiB per row)
     rm_kernels = {"rm_v8w8kg2": (0, 8, 64), "rm_v8w8kg3": (1, 8, 64), "rm_v8w8kg4": (2, 8, 64),
                   "rm_v16w4kg2": (3, 4, 64), "rm_v8w8kg2ds2": (4, 8, 64), "rm_v8w8kg4ds2": (5, 8, 64),
-                  "rm_v16w4kg2ds2": (6, 4, 64), "rm_v4w8kg4ds2": (7, 8, 32), "rm_v4w8kg4ds4": (8, 8, 32)}
+                  "rm_v16w4kg2ds2": (6, 4, 64), "rm_v4w8kg4ds2": (7, 8, 32), "rm_v4w8kg4ds4": (8, 8, 32),
+                  "rm_v8w8kg2sg": (9, 8, 64), "rm_v16w4kg2sg": (10, 4, 64), "rm_v8w8kg3sg": (11, 8, 64)}
     for kname, (kid, wv, pchunks) in rm_kernels.items():
         if a.only and not any(o in kname for o in a.only.split(",")):
             continue
