@@ -183,7 +183,8 @@ def test_reduce_kernel_big_tiles_ragged(n, ncols, cuda):
 # ends; deep stacks are the per-rank shapes of the multi-GPU runs
 ROW_SHAPES = [(800, 150001), (300, 390001), (200, 700003), (64, 1500007), (40, 3300001), (17, 33), (2, 5000003),
               (12, 3500001),  # widens the grid to one full piece per block
-              (3, 14000003), (2, 9000001)]  # row-major groups of 5 and 3 pieces
+              (3, 14000003), (2, 9000001),  # row-major groups of 5 and 3 pieces
+              (1000, 44426), (150, 44426), (300, 70001), (199, 70001), (256, 1), (2000, 5)]  # narrow: 1-2 waves, D 16/32
 
 
 @pytest.mark.parametrize("mode", [na.MODE_W32_DIV32, na.MODE_W64])
@@ -223,7 +224,8 @@ def test_row_pipeline_geometries(n, ncols, cuda):
 
 @pytest.mark.parametrize("n,ncols,op", [(300, 390001, "avgm"), (64, 1500007, "adagrad"), (800, 150001, "adam"),
                                          (50, 700003, "yogi"), (20, 3000001, "avgm"), (10, 3500001, "adagrad"),
-                                         (6, 9000003, "avgm")])
+                                         (6, 9000003, "avgm"), (1000, 44426, "avgm"), (400, 70001, "adagrad"),
+                                         (120, 44426, "yogi")])
 def test_row_pipeline_fused_epilogues(n, ncols, op, cuda):
     stride = -(-ncols // 64) * 64
     x = _device_stack(n, stride, seed=ncols)

@@ -600,6 +600,17 @@ int main(int argc, char** argv) {
   vs.push_back(op == FA_OP_AVGM      ? make_dfr<V, W, KG, FA_OP_AVGM, double, TM>(stack, stride, n, w, ncols, e, bytes, G)   \
                : op == FA_OP_ADAGRAD ? make_dfr<V, W, KG, FA_OP_ADAGRAD, double, TM>(stack, stride, n, w, ncols, e, bytes, G) \
                                      : make_dfr<V, W, KG, FA_OP_MEAN, double, TM>(stack, stride, n, w, ncols, e, bytes, G))
+  if (!strcmp(set, "deep")) {  // windows of ~1 chunk per block (small P, deep N): pipeline depth per wave
+    ROWSG(1, 16, 4, 192);
+    ROWSG(1, 16, 1, 192);
+    ROWSG(1, 32, 1, 192);
+    ROWSG(1, 48, 1, 192);
+    ROWSG(1, 60, 1, 192);
+    ROWSG(2, 24, 1, 192);
+    ROWSG(1, 32, 2, 192);
+    ROWSG(1, 16, 1, 256);
+    ROWSG(1, 48, 1, 256);
+  }
   if (!strcmp(set, "dfr")) {  // deferred group epilogues (LDS-stashed sums) vs the product geometries
     RM(16, 1, 4, 3, 192);
     RM(16, 1, 4, 4, 192);
