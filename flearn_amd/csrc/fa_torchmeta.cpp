@@ -35,7 +35,7 @@ extern "C" {
 // 1: every client's value for every key has client 0's Python type, dtype and shape (what
 // bucket.py _raw_signature compares); 0: some value differs; -1: cannot tell (a value is not a
 // torch tensor, a key is missing, an upload is not a dict) — the caller compares in Python.
-int fa_tm_same_signature(PyObject* clients, PyObject* keys) {
+static int same_signature(PyObject* clients, PyObject* keys) {
   if (!PyList_Check(clients) || !PyTuple_Check(keys)) return kUnknown;
   const Py_ssize_t n = PyList_GET_SIZE(clients), nk = PyTuple_GET_SIZE(keys);
   if (n == 0) return kUnknown;
@@ -71,8 +71,8 @@ int fa_tm_same_signature(PyObject* clients, PyObject* keys) {
 // `device`; each value is also stored in keep[k * n + c] (a list of that length made by the
 // caller) so the tensors outlive the kernel that reads them.  Returns 0, or 1 (nothing reliable
 // written) at the first value that does not qualify.
-int fa_tm_tensor_ptrs(PyObject* clients, PyObject* keys, PyObject* dtypes, int64_t device, int64_t* out,
-                      PyObject* keep) {
+static int tensor_ptrs(PyObject* clients, PyObject* keys, PyObject* dtypes, int64_t device, int64_t* out,
+                       PyObject* keep) {
   if (!PyList_Check(clients) || !PyTuple_Check(keys) || !PyList_Check(keep) || !PyTuple_Check(dtypes))
     return kFallback;
   const Py_ssize_t n = PyList_GET_SIZE(clients), nk = PyTuple_GET_SIZE(keys);
@@ -92,13 +92,37 @@ int fa_tm_tensor_ptrs(PyObject* clients, PyObject* keys, PyObject* dtypes, int64
         return kFallback;
       }
       const c10::Device dv = t->device();
-      if (t->scalar_type() != want || !dv.is_cuda() || dv.index() != device || !t->is_contiguous()) return kFallback;
+      // strided layout with storage first: is_contiguous / data_ptr throw on sparse or
+      // storage-less tensors
+      if (t->scalar_type() != want || !dv.is_cuda() || dv.index() != device || t->layout() != c10::kStrided ||
+          !t->has_storage() || !t->is_contiguous())
+        return kFallback;
       out[k * n + c] = reinterpret_cast<int64_t>(t->data_ptr());
       Py_INCREF(v);
       PyList_SetItem(keep, k * n + c, v);  // steals the new reference, drops the old item
     }
   }
   return kOk;
+}
+
+// C++ exceptions must not cross the ctypes boundary: any one answers "cannot tell" / "fallback"
+int fa_tm_same_signature(PyObject* clients, PyObject* keys) {
+  try {
+    return same_signature(clients, keys);
+  } catch (...) {
+    PyErr_Clear();
+    return kUnknown;
+  }
+}
+
+int fa_tm_tensor_ptrs(PyObject* clients, PyObject* keys, PyObject* dtypes, int64_t device, int64_t* out,
+                      PyObject* keep) {
+  try {
+    return tensor_ptrs(clients, keys, dtypes, device, out, keep);
+  } catch (...) {
+    PyErr_Clear();
+    return kFallback;
+  }
 }
 
 }  // extern "C"

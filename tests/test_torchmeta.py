@@ -73,3 +73,31 @@ def test_make_plan_uses_native_signature(L):
     assert bucket._same_signature_native(cs, list(cs[0]))
     plan = bucket.make_plan([1.0] * len(cs), cs)
     assert plan.n_clients == len(cs)
+
+
+def test_sparse_and_storage_less_values_fall_back(L):
+    """Sparse values answer "fallback" / a signature instead of a C++ exception crossing ctypes."""
+    cs = _clients()
+    keys = ("a.weight", "a.bias")
+    cs2 = [dict(c) for c in cs]
+    cs2[1]["a.bias"] = torch.zeros(3).to_sparse()
+    py = all(bucket._raw_signature(c, list(keys)) == bucket._raw_signature(cs2[0], list(keys)) for c in cs2)
+    assert L.fa_tm_same_signature(cs2, keys) == int(py)  # what the Python comparison says
+    ptrs = np.zeros((2, len(cs)), np.int64)
+    keep = [None] * (2 * len(cs))
+    assert L.fa_tm_tensor_ptrs(cs2, keys, (torch.float32, torch.float32), 0, ptrs.ctypes.data, keep) == 1
+
+
+@pytest.mark.gpu
+def test_sparse_device_value_falls_back(L):
+    """A sparse CUDA tensor passes the dtype and device checks: the layout check must refuse it
+    before is_contiguous() (which throws for sparse tensors) is reached."""
+    dev = torch.device("cuda", 0)
+    cs = [{k: v.to(dev) for k, v in c.items()} for c in _clients()]
+    keys = ("a.weight", "a.bias")
+    ptrs = np.zeros((2, len(cs)), np.int64)
+    keep = [None] * (2 * len(cs))
+    dts = (torch.float32, torch.float32)
+    assert L.fa_tm_tensor_ptrs(cs, keys, dts, 0, ptrs.ctypes.data, keep) == 0
+    cs[3]["a.bias"] = torch.zeros(3, device=dev).to_sparse()
+    assert L.fa_tm_tensor_ptrs(cs, keys, dts, 0, ptrs.ctypes.data, keep) == 1
