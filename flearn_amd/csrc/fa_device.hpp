@@ -1064,6 +1064,100 @@ __global__ __launch_bounds__(64 * W) void reduce_kernel_rows(const float* __rest
   }
 }
 
+// Narrow windows, deep pipeline (at most two 1-KiB row chunks per block: LeNet-sized models, deep
+// client stacks).  Block b owns chunks [b*W, b*W + W), one per wave, lane l one quad.  Only D rows
+// per wave bound the bytes in flight here (a wave's vmcnt counts at most 63 loads), so D goes up
+// to 60 and the pipeline has no drain code: the sweep runs whole D-row rounds; in the last two a
+// refill past the last row re-loads row n-1 (an L2 hit) and a product past it is dropped by a
+// select.  The row address
+// advances by the stride through one running scalar pointer (opaque to the compiler: written as
+// row(i + d) in the unrolled loop, every d * stride was kept in a scalar register pair and
+// spilled).  Same sums, same order as reduce_kernel_rows.
+template <class P, typename T, int OP, int D, int W, bool NT>
+__global__ __launch_bounds__(64 * W) void reduce_kernel_narrow(const float* __restrict__ stack, int64_t stride,
+                                                               int n, const typename P::w_t* __restrict__ w,
+                                                               int64_t col0, int64_t ncols, Epi<T> e) {
+  static_assert(sizeof(typename P::x_t) == 4 && D <= 63, "4-byte rows; vmcnt counts 63 loads");
+  typedef typename P::acc_t A;
+  typedef typename vec4<A>::type AV;
+  typedef typename vec4<float>::type XV;
+  const int64_t nquads = (ncols + 3) / 4;
+  const int64_t qb = (int64_t)blockIdx.x * 64 * W;
+  const int64_t qe = qb + 64 * W < nquads ? qb + 64 * W : nquads;
+  const int64_t cend = qe * 4 < ncols ? qe * 4 : ncols;
+  if (cend <= qb * 4) return;
+  const int cols = (int)(cend - qb * 4);
+  const uint32_t bytes = (uint32_t)cols * 4u;
+  const int voff = (int)threadIdx.x * 16;
+  const int64_t rb = stride * 4;
+  const char* base = reinterpret_cast<const char*>(stack + col0 + qb * 4);
+  const char* lastp = base + (int64_t)(n - 1) * rb;
+  const char* p = base + rb;  // the next row to load (row 1)
+#define FA_NW_LOAD(dst, CLAMP)                                                         \
+  {                                                                                      \
+    const char* q_ = p;                                                                  \
+    if (CLAMP) q_ = p <= lastp ? p : lastp;                                              \
+    dst = buf_load_quad<NT>(row_rsrc(q_, bytes), voff, 0);                               \
+    p += rb;                                                                             \
+    asm volatile("" : "+s"(p));                                                          \
+  }
+  // the weights of a round ride in one VGPR (lane l: row i + l), loaded a round ahead through a
+  // range-checked descriptor and broadcast with readlane: a scalar load per row, waited for right
+  // before its product, put a scalar-cache round trip on every row of the serial chain
+  typedef typename P::w_t WT;
+  const __amdgpu_buffer_rsrc_t wr = row_rsrc(w, (uint32_t)n * (uint32_t)sizeof(WT));
+  const int lane = (int)threadIdx.x & 63;
+  auto wload = [&](int first) {  // lane l of every wave: w[first + l] (0 past the end)
+    if constexpr (sizeof(WT) == 4)
+      return __builtin_bit_cast(WT, __builtin_amdgcn_raw_buffer_load_b32(wr, (lane + first) * 4, 0, 0));
+    else
+      return __builtin_bit_cast(WT, __builtin_amdgcn_raw_buffer_load_b64(wr, (lane + first) * 8, 0, 0));
+  };
+  auto wlane = [](WT v, int l) {
+    if constexpr (sizeof(WT) == 4) {
+      return __builtin_bit_cast(WT, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
+    } else {
+      const long long b = __builtin_bit_cast(long long, v);
+      const int lo = __builtin_amdgcn_readlane((int)b, l), hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+      return __builtin_bit_cast(WT, (long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+    }
+  };
+  WT wcur = wload(1);
+  XV x[D];
+#pragma unroll
+  for (int d = 0; d < D; ++d) FA_NW_LOAD(x[d], true);
+  AV acc = quad_mul<P>(w[0], buf_load_quad<NT>(row_rsrc(base, bytes), voff, 0));
+  int i = 1;
+  // steady rounds: every consumed row and every refill row is real
+  for (; i + 2 * D <= n; i += D) {
+    const WT wnext = wload(i + D);
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      acc = quad_axpy<P>(acc, wlane(wcur, d), x[d]);
+      __builtin_amdgcn_sched_barrier(0);
+      FA_NW_LOAD(x[d], false);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    wcur = wnext;
+  }
+  // the last (at most two) rounds: refills clamped to row n-1, products past it dropped
+  for (; i < n; i += D) {
+    const WT wnext = wload(i + D);
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      const AV t = quad_axpy<P>(acc, wlane(wcur, d), x[d]);
+      acc = i + d < n ? t : acc;
+      __builtin_amdgcn_sched_barrier(0);
+      FA_NW_LOAD(x[d], true);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    wcur = wnext;
+  }
+#undef FA_NW_LOAD
+  const AV accs[1] = {acc};
+  finish_piece<T, OP, A, 1, 64 * W, 1>(e, qb, cols, accs);
+}
+
 // One group of a row-major block: KG of the block's pieces (slots g0 .. g0+KG-1, interleaved
 // over the grid as in reduce_kernel_rows), all rows swept once, then the group epilogue.
 template <class P, typename T, int OP, int V, int D, int W, int KG, bool NT, int EPIB, bool TR>

@@ -102,11 +102,11 @@ int launch_rows(const float* stack, int64_t stride, int n, const typename P::w_t
   return launch_check();
 }
 
-template <class P, typename T, int OP, int V, int D, int W>
-int launch_rows_d(const float* stack, int64_t stride, int n, const typename P::w_t* w, int64_t col0,
+template <class P, typename T, int OP, int D>
+int launch_narrow(const float* stack, int64_t stride, int n, const typename P::w_t* w, int64_t col0,
                   int64_t ncols, const Epi<T>& e, int64_t grid, hipStream_t s) {
-  hipLaunchKernelGGL((reduce_kernel_rows<P, T, OP, V, D, W, kNT>), dim3((unsigned)grid), dim3(64 * W), 0, s, stack,
-                     stride, n, w, col0, ncols, e);
+  hipLaunchKernelGGL((reduce_kernel_narrow<P, T, OP, D, 1, kNT>), dim3((unsigned)grid), dim3(64), 0, s, stack, stride,
+                     n, w, col0, ncols, e);
   return launch_check();
 }
 
@@ -184,17 +184,19 @@ int launch_reduce(const typename P::x_t* stack, int64_t stride, int n, const voi
     if (grid > chunks) grid = chunks;
     const int64_t share = (chunks + grid - 1) / grid;  // chunks per block
     if (share <= 2) {
-      // narrow windows (one or two 1-KiB chunks of every row per block: LeNet-sized models, deep
-      // client stacks): a block of `share` waves, each one chunk D rows deep.  4- or 8-wave blocks
-      // left all but one wave idle with 8-16 KiB in flight per block; 1000 x LeNet5 (one chunk
-      // per block) 51.1 -> 34.3 us, 2000 clients 98.3 -> 62.0 us, 400 clients 27.5 -> 22.1 us,
-      // 100 clients 9.8 -> 8.8 us (D = 16: too few rows for a 32-deep pipeline) — same sums,
-      // same order (tools/tune_reduce.hip set "deep", profiles/r02/tune_deep/)
-      if (share == 1)
-        return n >= 200 ? launch_rows_d<P, T, OP, 1, 32, 1>(stack, stride, n, wt, col0, ncols, e, grid, s)
-                        : launch_rows_d<P, T, OP, 1, 16, 1>(stack, stride, n, wt, col0, ncols, e, grid, s);
-      return n >= 200 ? launch_rows_d<P, T, OP, 1, 32, 2>(stack, stride, n, wt, col0, ncols, e, grid, s)
-                      : launch_rows_d<P, T, OP, 1, 16, 2>(stack, stride, n, wt, col0, ncols, e, grid, s);
+      // narrow windows (at most two 1-KiB chunks of every row per block: LeNet-sized models, deep
+      // client stacks): reduce_kernel_narrow, one single-wave block per chunk, a D-deep pipeline
+      // with no drain code and the round's weights broadcast from one VGPR.  A 4- or 8-wave
+      // block had work for one or two waves (8-16 KiB in flight per block).  1000 x LeNet5 51.1
+      // -> 31.8 us, 2000 clients 98.3 -> 55.6 us, 400 clients 27.5 -> 15.7 us, 100 clients
+      // 9.8 -> 7.4 us, 300 x 70,001 -> 17.2 us (tools/tune_reduce.hip sets "deep", "deep2";
+      // profiles/r02/tune_deep/).  D: 16 rows below 350 clients (the ramp of a deeper pipeline
+      // does not pay off), 32 below 700, else 40 (48-60 lose: fewer waves' worth of latency
+      // hiding per row than the issue cost of the extra slots).  Same sums, same order.
+      const int64_t g1 = chunks;
+      if (n < 350) return launch_narrow<P, T, OP, 16>(stack, stride, n, wt, col0, ncols, e, g1, s);
+      if (n < 700) return launch_narrow<P, T, OP, 32>(stack, stride, n, wt, col0, ncols, e, g1, s);
+      return launch_narrow<P, T, OP, 40>(stack, stride, n, wt, col0, ncols, e, g1, s);
     }
     if constexpr (OP == FA_OP_MEAN) {
       constexpr int W = 4;

@@ -184,14 +184,16 @@ def test_reduce_kernel_big_tiles_ragged(n, ncols, cuda):
 ROW_SHAPES = [(800, 150001), (300, 390001), (200, 700003), (64, 1500007), (40, 3300001), (17, 33), (2, 5000003),
               (12, 3500001),  # widens the grid to one full piece per block
               (3, 14000003), (2, 9000001),  # row-major groups of 5 and 3 pieces
-              (1000, 44426), (150, 44426), (300, 70001), (199, 70001), (256, 1), (2000, 5)]  # narrow: 1-2 waves, D 16/32
+              (1000, 44426), (150, 44426), (300, 70001), (349, 70001), (600, 44426), (700, 3), (256, 1),
+              (2000, 5)]  # narrow windows: one-wave blocks, D 16/32/40, tail rounds
 
 
 @pytest.mark.parametrize("mode", [na.MODE_W32_DIV32, na.MODE_W64])
-def test_big_window_modes_bit_exact(mode, cuda):
-    """Multi-piece windows (row-major geometry for fp32 sums, column-major for f64 sums) in the
-    np.float32 / np.float64 weight modes."""
-    n, ncols = 5, 9_000_001
+@pytest.mark.parametrize("n,ncols", [(5, 9_000_001), (1000, 44426), (400, 70001)])
+def test_big_window_modes_bit_exact(mode, n, ncols, cuda):
+    """Multi-piece windows (row-major geometry for fp32 sums, column-major for f64 sums) and narrow
+    windows (one-wave blocks; f64 weights broadcast in two halves) in the np.float32 / np.float64
+    weight modes."""
     stride = -(-ncols // 64) * 64
     x = _device_stack(n, stride, seed=ncols + mode)
     if mode == na.MODE_W64:

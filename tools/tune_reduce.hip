@@ -343,6 +343,21 @@ Variant make_rows(const float* stack, int64_t stride, int n, const float* w, int
           true, {}};
 }
 
+template <int D, int W, int OP, typename T>
+Variant make_narrow(const float* stack, int64_t stride, int n, const float* w, int64_t ncols, Epi<T> e,
+                    double bytes) {
+  const int64_t chunks = ((ncols + 3) / 4 + 63) / 64;
+  const int64_t grid = (chunks + W - 1) / W;
+  char name[96];
+  snprintf(name, sizeof name, "narrow D%d W%d g%lld", D, W, (long long)grid);
+  return {name, bytes,
+          [=] {
+            hipLaunchKernelGGL((reduce_kernel_narrow<AccF32, T, OP, D, W, true>), dim3((unsigned)grid),
+                               dim3(64 * W), 0, 0, stack, stride, n, w, (int64_t)0, ncols, e);
+          },
+          true, {}};
+}
+
 template <int V, int D, int W, int KG, int OP, typename T, int EPIB = (V >= 2 ? 2 : V)>
 Variant make_rowmajor(const float* stack, int64_t stride, int n, const float* w, int64_t ncols, Epi<T> e,
                       double bytes, int64_t grid) {
@@ -600,6 +615,21 @@ int main(int argc, char** argv) {
   vs.push_back(op == FA_OP_AVGM      ? make_dfr<V, W, KG, FA_OP_AVGM, double, TM>(stack, stride, n, w, ncols, e, bytes, G)   \
                : op == FA_OP_ADAGRAD ? make_dfr<V, W, KG, FA_OP_ADAGRAD, double, TM>(stack, stride, n, w, ncols, e, bytes, G) \
                                      : make_dfr<V, W, KG, FA_OP_MEAN, double, TM>(stack, stride, n, w, ncols, e, bytes, G))
+#define NARROW(D, W)                                                                                      \
+  vs.push_back(op == FA_OP_AVGM      ? make_narrow<D, W, FA_OP_AVGM, double>(stack, stride, n, w, ncols, e, bytes)   \
+               : op == FA_OP_ADAGRAD ? make_narrow<D, W, FA_OP_ADAGRAD, double>(stack, stride, n, w, ncols, e, bytes) \
+                                     : make_narrow<D, W, FA_OP_MEAN, double>(stack, stride, n, w, ncols, e, bytes))
+  if (!strcmp(set, "deep2")) {  // the narrow-window kernel: depth, waves per block
+    ROWSG(1, 32, 1, 192);
+    NARROW(16, 1);
+    NARROW(32, 1);
+    NARROW(40, 1);
+    NARROW(48, 1);
+    NARROW(56, 1);
+    NARROW(60, 1);
+    NARROW(32, 2);
+    NARROW(60, 2);
+  }
   if (!strcmp(set, "deep")) {  // windows of ~1 chunk per block (small P, deep N): pipeline depth per wave
     ROWSG(1, 16, 4, 192);
     ROWSG(1, 16, 1, 192);
