@@ -104,6 +104,7 @@ def main():
         "rows_bit_equal_stack": same,
         "server_call_ms_median": round(float(np.median(walls)) * 1e3, 3),
         "server_call_ms_min": round(min(walls) * 1e3, 3),
+        "server_call_ms_all": [round(x * 1e3, 2) for x in walls],
         "path": path,
     }), flush=True)
 
