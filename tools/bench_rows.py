@@ -36,6 +36,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--no-gc", action="store_true", help="diagnosis: time the server() calls with gc disabled")
     a = ap.parse_args()
     name, n, op = CONFIGS[a.config]
     dev = torch.device("cuda", 0)
@@ -91,6 +92,11 @@ def main():
         same = None  # the fused state advanced differently often; parity is in tests/test_gpu_rows.py
     torch.cuda.synchronize()
     walls = []
+    if a.no_gc:
+        import gc
+
+        gc.collect()
+        gc.disable()
     for r in range(a.steps):
         t0 = time.perf_counter()
         s.server(uploads, r + 1)
