@@ -619,6 +619,15 @@ int main(int argc, char** argv) {
   vs.push_back(op == FA_OP_AVGM      ? make_narrow<D, W, FA_OP_AVGM, double>(stack, stride, n, w, ncols, e, bytes)   \
                : op == FA_OP_ADAGRAD ? make_narrow<D, W, FA_OP_ADAGRAD, double>(stack, stride, n, w, ncols, e, bytes) \
                                      : make_narrow<D, W, FA_OP_MEAN, double>(stack, stride, n, w, ncols, e, bytes))
+  if (!strcmp(set, "deep3")) {  // wider windows (3..30 chunks per block): row kernel vs one-wave narrow blocks
+    ROWSG(1, 16, 4, 192);
+    ROWSG(2, 8, 4, 192);
+    ROWSG(4, 4, 4, 192);
+    ROWSG(8, 2, 4, 192);
+    NARROW(16, 1);
+    NARROW(32, 1);
+    NARROW(40, 1);
+  }
   if (!strcmp(set, "deep2")) {  // the narrow-window kernel: depth, waves per block
     ROWSG(1, 32, 1, 192);
     NARROW(16, 1);
