@@ -227,7 +227,7 @@ def test_row_pipeline_geometries(n, ncols, cuda):
 @pytest.mark.parametrize("n,ncols,op", [(300, 390001, "avgm"), (64, 1500007, "adagrad"), (800, 150001, "adam"),
                                          (50, 700003, "yogi"), (20, 3000001, "avgm"), (10, 3500001, "adagrad"),
                                          (6, 9000003, "avgm"), (1000, 44426, "avgm"), (400, 70001, "adagrad"),
-                                         (120, 44426, "yogi")])
+                                         (120, 44426, "yogi"), (1000, 44426, "adam")])
 def test_row_pipeline_fused_epilogues(n, ncols, op, cuda):
     stride = -(-ncols // 64) * 64
     x = _device_stack(n, stride, seed=ncols)
