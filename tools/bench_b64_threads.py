@@ -35,6 +35,26 @@ def main():
             best = min(best, time.perf_counter() - t)
             assert rc == 0
         res["decode_GB_s_text"][th] = round(len(txt) / best / 1e9, 2)
+    # the same decode into pinned host memory (what HTTP-mode uploads land in) and one upload's size
+    import torch
+
+    pinned = torch.empty(len(out), dtype=torch.uint8).pin_memory()
+    res["pinned_decode_GB_s_text"] = {}
+    for th in (1, 16):
+        best = 1e9
+        for _ in range(4):
+            t = time.perf_counter()
+            assert fn(txt, len(txt), pinned.data_ptr(), len(out), th) == 0
+            best = min(best, time.perf_counter() - t)
+        res["pinned_decode_GB_s_text"][th] = round(len(txt) / best / 1e9, 2)
+    small = txt[: 62 * 2**20 // 4 * 4]
+    for dst_name, ptr in (("pageable", out.ctypes.data), ("pinned", pinned.data_ptr())):
+        best = 1e9
+        for _ in range(10):
+            t = time.perf_counter()
+            assert fn(small, len(small), ptr, len(out), 16) == 0
+            best = min(best, time.perf_counter() - t)
+        res[f"one_upload_62MB_16threads_{dst_name}_ms"] = round(best * 1e3, 3)
     print(json.dumps(res))
 
 
