@@ -522,6 +522,59 @@ def _pinned_row(stride: int) -> torch.Tensor:
     return torch.empty(stride, dtype=torch.float32)
 
 
+class _Template:
+    """Everything decode_fast derives from a scanner manifest alone: the parsed tree (read-only
+    from here on), the row plan, the aux-buffer layout and the payload ranges.  Uploads of one
+    model with the same weight produce the same manifest text (pickle lays the same dict out
+    the same way), so a round of N uploads plans once instead of N times."""
+
+    __slots__ = ("tree", "row_plan", "row_nodes", "aux_size", "planned", "offs", "lens", "rel", "in_row")
+
+    def __init__(self, L, p, n, tree):
+        dec = _Decoder(L, p, n)
+        self.planned = dec.plan_row(tree)
+        dec.assign(tree)
+        self.tree, self.row_plan, self.row_nodes, self.aux_size = tree, dec.row_plan, dec.row_nodes, dec.aux_size
+        offs, lens, rel, in_row = [], [], [], []
+        for node in _payload_nodes_list(tree):
+            if "__nd" in node:
+                o, ln = node["__nd"][3], node["__nd"][4]
+                row = "_aux" not in node
+                r = 4 * dec.row_plan[id(node)] if row else node["_aux"]
+            elif "__sc" in node:
+                o, ln, row, r = node["__sc"][1], node["__sc"][2], False, node["_aux"]
+            else:
+                (o, ln), row, r = node["__b"], False, node["_aux"]
+            if ln:
+                offs.append(o)
+                lens.append(ln)
+                rel.append(r)
+                in_row.append(row)
+        self.offs = np.array(offs, np.int64)
+        self.lens = np.array(lens, np.int64)
+        self.rel = np.array(rel, np.int64)
+        self.in_row = np.array(in_row, bool)
+
+
+_TEMPLATES: collections.OrderedDict = collections.OrderedDict()  # manifest text -> _Template
+_TEMPLATES_MAX = 8
+_TEMPLATES_LOCK = threading.Lock()
+
+
+def _template(L, p, n, manifest: bytes) -> _Template:
+    with _TEMPLATES_LOCK:
+        t = _TEMPLATES.get(manifest)
+        if t is not None:
+            _TEMPLATES.move_to_end(manifest)
+            return t
+    t = _Template(L, p, n, json.loads(manifest.decode("utf-8")))
+    with _TEMPLATES_LOCK:
+        _TEMPLATES[manifest] = t
+        while len(_TEMPLATES) > _TEMPLATES_MAX:
+            _TEMPLATES.popitem(last=False)
+    return t
+
+
 def decode_fast(s: str, stage_to_device: bool = False):
     """Decode base64(pickle) text through the scanner; raises _WireError(FA_ERR_UNSUPPORTED /
     FA_ERR_DATA) when the content or the encoding is outside the fast path.  stage_to_device:
@@ -538,10 +591,10 @@ def decode_fast(s: str, stage_to_device: bool = False):
             continue
         _check(L, rc, "pickle scan")
         break
-    tree = json.loads(buf.raw[: need.value].decode("utf-8"))
+    tmpl = _template(L, p, n, buf.raw[: need.value])
+    tree, planned = tmpl.tree, tmpl.planned
     dec = _Decoder(L, p, n)
-    planned = dec.plan_row(tree)
-    dec.assign(tree)
+    dec.row_plan, dec.row_nodes, dec.aux_size = tmpl.row_plan, tmpl.row_nodes, tmpl.aux_size
     aux_np = np.empty(max(dec.aux_size, 1), dtype=np.uint8)
     row, row_np = None, None
     if planned is not None:
@@ -551,27 +604,11 @@ def decode_fast(s: str, stage_to_device: bool = False):
         row_np._fa_tensor = row
         # zero the alignment gaps (reduced but never returned: keep them finite and deterministic)
         row_np[_gap_index(planned[1])] = 0
-    row_base = row_np.ctypes.data if row_np is not None else 0
-    aux_base = aux_np.ctypes.data
-    offs, lens, dsts = [], [], []
-    for node in _payload_nodes_list(tree):
-        if "__nd" in node:
-            o, ln = node["__nd"][3], node["__nd"][4]
-            dst = row_base + 4 * dec.row_plan[id(node)] if "_aux" not in node else aux_base + node["_aux"]
-        elif "__sc" in node:
-            o, ln = node["__sc"][1], node["__sc"][2]
-            dst = aux_base + node["_aux"]
-        else:
-            o, ln = node["__b"]
-            dst = aux_base + node["_aux"]
-        if ln:
-            offs.append(o)
-            lens.append(ln)
-            dsts.append(dst)
-    if offs:
-        k = len(offs)
-        rc = L.fa_b64_decode_ranges(p, n, k, (ctypes.c_int64 * k)(*offs), (ctypes.c_int64 * k)(*lens),
-                                    (ctypes.c_void_p * k)(*dsts), _threads(sum(lens)))
+    if len(tmpl.offs):
+        row_base = row_np.ctypes.data if row_np is not None else 0
+        dsts = tmpl.rel + np.where(tmpl.in_row, row_base, aux_np.ctypes.data)
+        rc = L.fa_b64_decode_ranges(p, n, len(tmpl.offs), tmpl.offs.ctypes.data, tmpl.lens.ctypes.data,
+                                    dsts.ctypes.data, _threads(int(tmpl.lens.sum())))
         _check(L, rc, "payload decode")
     obj = dec.build(tree, row_np, aux_np)
     if planned is not None:
