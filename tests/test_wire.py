@@ -162,6 +162,26 @@ def test_decode_fast_path_taken_for_uploads():
         same(wire.decode_fast(s), pickle.loads(pickle.dumps(obj)))
 
 
+def test_decode_plan_cache_shares_plans_not_data():
+    """Uploads of one model pickle to the same manifest: the second decode reuses the first's
+    plan (_TEMPLATES) but gets its own arrays with its own values; a different weight or layout
+    is a different manifest."""
+    rng = np.random.default_rng(3)
+    ups = [{"agg_weight": 1.0, "params": {"a.w": rng.standard_normal((40, 30)).astype(np.float32),
+                                          "a.b": rng.standard_normal(30).astype(np.float32),
+                                          "bn.n": np.array(7, np.int64)}} for _ in range(3)]
+    texts = [base64.b64encode(pickle.dumps(u)).decode() for u in ups]
+    wire._TEMPLATES.clear()
+    outs = [wire.decode_fast(t) for t in texts]
+    assert len(wire._TEMPLATES) == 1
+    for u, o in zip(ups, outs):
+        same(o, u)
+    assert not np.shares_memory(outs[0]["params"]["a.w"], outs[1]["params"]["a.w"])
+    other = dict(ups[0], agg_weight=2.5)
+    same(wire.decode_fast(base64.b64encode(pickle.dumps(other)).decode()), other)
+    assert len(wire._TEMPLATES) == 2
+
+
 def test_lenient_base64_like_reference():
     """Text base64.b64decode accepts (here: embedded newlines) is decoded like the reference."""
     obj = {"agg_weight": 1.0, "params": {"w": np.arange(10, dtype=np.float32)}}
