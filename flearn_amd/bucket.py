@@ -239,7 +239,10 @@ def _build_plan(agg_weight_lst, w_local_lst, keys, slow) -> BucketPlan:
         g = groups.get(nm.kind)
         if g is None:
             g = groups[nm.kind] = Group(nm.kind, nm)
-        elif g.numerics != nm and not _same_numerics(g.numerics, nm):
+        elif g.numerics is not nm and not _same_numerics(g.numerics, nm):
+            # (identity first: the dataclass __eq__ would compare the weight arrays elementwise
+            # and raise for more than one client — a float64 model with int64 BN counters put
+            # two dtypes' numerics into the f64 bucket and failed here)
             raise TypeError(f"key {k!r} needs different arithmetic than the rest of its bucket")
         numel = int(math.prod(shape))
         seg = Segment(k, shape, numel, g.stride, dt)

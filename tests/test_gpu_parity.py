@@ -965,3 +965,19 @@ def test_strategy_group_mode_one_rank(name, cuda, tmp_path):
     finally:
         if created:
             dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("weights", [[1.0, 2.5, 0.5, 3.0], [1, 2, 3, 4]])
+def test_float64_model_with_int64_counters(weights, cuda):
+    """A float64 model with BatchNorm counters: with float weights the f64 tensors and the int64
+    counters share the f64 bucket (numpy promotes both to float64, strategy.py:123-129); with
+    int weights the counters keep int64 arithmetic.  Bit-exact vs the oracle (a plan-building
+    bug once raised here: tests/test_plan_props.py found it)."""
+    rng = np.random.default_rng(5)
+    clients = [{"conv.weight": rng.standard_normal((8, 3, 3, 3)),
+                "bn.running_mean": rng.standard_normal(8),
+                "bn.num_batches_tracked": np.array(100 + i, np.int64),
+                "fc.weight": rng.standard_normal((10, 72))} for i in range(len(weights))]
+    want = oracle.server_ensemble(weights, [{k: v.copy() for k, v in c.items()} for c in clients])
+    got = AVG().server(upload(clients, weights), 0)["w_glob"]
+    assert_dict_bitwise(got, want, f"f64 model, weights {type(weights[0]).__name__}")

@@ -1,0 +1,51 @@
+"""Host (no GPU): properties of the bucket plan (flearn_amd/bucket.py make_plan) over random
+model layouts — the invariants the kernels rely on (16-B aligned, disjoint segments inside the
+row stride, one kind per key as numpy's promotion of strategy.py:123-129 decides, the first
+client's key order), checked with hypothesis instead of hand-picked layouts."""
+import numpy as np
+from hypothesis import given, settings
+from hypothesis import strategies as st
+
+from flearn_amd.bucket import ALIGN, make_plan
+from flearn_amd.semantics import KIND_F32, KIND_F64, KIND_I64
+
+DTYPES = [np.float32, np.float32, np.float32, np.float64, np.int64]
+
+shapes = st.lists(st.integers(0, 70), min_size=0, max_size=3).map(tuple)
+layout = st.lists(st.tuples(shapes, st.sampled_from(DTYPES)), min_size=1, max_size=12)
+
+
+@settings(max_examples=150, deadline=None)
+@given(layout, st.integers(1, 5), st.sampled_from(["pyfloat", "pyint", "np32", "np64"]))
+def test_plan_invariants(lay, n, wkind):
+    keys = [f"layer{i}.{'weight' if i % 2 else 'bias'}" for i in range(len(lay))]
+    clients = [{k: np.zeros(s, dt) for k, (s, dt) in zip(keys, lay)} for _ in range(n)]
+    weights = {"pyfloat": [1.0] * n, "pyint": [1] * n, "np32": [np.float32(1)] * n,
+               "np64": [np.float64(1)] * n}[wkind]
+    try:
+        plan = make_plan(weights, clients)
+    except TypeError:
+        # a weight / dtype pair whose per-client precisions would differ is refused, not guessed
+        # (np.float32 weights on int64 buffers promote to float64 — still one precision, so only
+        # dtypes outside fp32/f64/int64 reach here; none are generated)
+        raise
+    assert plan.keys == keys  # the first client's insertion order
+    assert plan.n_clients == n
+    seen = set()
+    for kind, g in plan.groups.items():
+        assert g.stride % ALIGN == 0
+        end = 0
+        for s in g.segments:
+            assert s.offset % ALIGN == 0 and s.offset >= end  # aligned, disjoint, in order
+            assert s.numel == int(np.prod(s.shape, dtype=np.int64))
+            end = s.offset + s.numel
+            assert plan.key_group[s.key] == kind and plan.key_segment[s.key] is s
+            seen.add(s.key)
+        assert end <= g.stride
+    assert seen == set(keys)
+    for k, (s, dt) in zip(keys, lay):
+        prod = np.result_type(weights[0], dt)
+        want = KIND_F32 if dt == np.float32 and prod == np.float32 else (KIND_I64 if prod == np.int64 else KIND_F64)
+        if dt == np.float32:
+            want = KIND_F32  # fp32 tensors stay in the fp32 bucket whatever the sum precision (mode)
+        assert plan.key_group[k] == want, (k, dt, wkind)
