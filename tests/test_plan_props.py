@@ -49,3 +49,38 @@ def test_plan_invariants(lay, n, wkind):
         if dt == np.float32:
             want = KIND_F32  # fp32 tensors stay in the fp32 bucket whatever the sum precision (mode)
         assert plan.key_group[k] == want, (k, dt, wkind)
+
+
+weight = st.one_of(
+    st.floats(0.01, 1e3, allow_nan=False), st.integers(1, 10**6), st.booleans().filter(bool),
+    st.floats(0.01, 1e3).map(np.float32), st.floats(0.01, 1e3).map(np.float64),
+    st.integers(1, 10**6).map(np.int64))
+
+
+@settings(max_examples=300, deadline=None)
+@given(st.lists(weight, min_size=1, max_size=6), st.sampled_from([np.float32, np.float64, np.int64]))
+def test_resolve_matches_numpy_or_refuses(ws, xdtype):
+    """semantics.resolve on arbitrary weight lists: either it refuses (the clients' products
+    would have different precisions — numpy would silently mix them) or it predicts exactly the
+    dtypes numpy gives strategy.py:123-129, the weights as numpy casts them, and W = np.sum."""
+    from flearn_amd.semantics import resolve
+
+    xs = [np.array([1, 2, 3], dtype=xdtype) for _ in ws]
+    prods = {np.result_type(w, xdtype) for w in ws}
+    if len(prods) > 1:
+        try:
+            resolve(ws, xdtype)
+        except TypeError:
+            return
+        raise AssertionError("mixed per-client precisions must be refused")
+    acc = ws[0] * xs[0]
+    for a, x in zip(ws[1:], xs[1:]):
+        acc = acc + a * x
+    with np.errstate(all="ignore"):
+        out = np.divide(acc, np.sum(ws))
+    nm = resolve(ws, xdtype)
+    assert nm.acc_dtype == acc.dtype and nm.out_dtype == out.dtype
+    assert nm.denom == float(np.sum(ws))
+    for w, c in zip(ws, nm.weights):
+        one = (w * np.ones(1, xdtype))[0]  # numpy's cast of the weight in its product (x 1: exact)
+        assert one.dtype == acc.dtype and (one == c or (np.isnan(one) and np.isnan(c)))
