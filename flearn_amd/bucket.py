@@ -53,7 +53,11 @@ class _NativeRows:
         # plain dicts only (dict / OrderedDict, whose item lookup the C side reproduces)
         self.clients = [w if type(w) in (dict, collections.OrderedDict) else None for w in w_local_lst]
         hp = tuple((h.data_ptr(), h.stride(0)) for h in hosts)
-        key = ("native_rows", hp)
+        # keyed by the pieces list (memoized on the plan: one object per kind and shard layout)
+        # AND the staging addresses: two kinds' stagings of different packers can occupy the same
+        # pinned block in turn (the host caching allocator hands a freed block out again), and a
+        # table keyed by addresses alone then packed one kind's keys into the other's stack
+        key = ("native_rows", id(pieces), hp)
         cached = memo.get(key) if memo is not None else None
         if cached is None:
             # per piece: itemsize, numel, src lo, src hi, format, dst base, dst row stride

@@ -1,0 +1,103 @@
+"""GPU: property test of the whole server path — random model layouts (fp32 / float64 / int64
+tensors, 0-d and empty included, sizes that land on every kernel geometry from one chunk to
+several pieces per block), random client counts and every weight kind numpy distinguishes —
+AVG().server (plan, pack, HIP reduce, unpack) against the oracle's restatement of
+strategy.py:102-130, bit for bit."""
+import os
+
+import numpy as np
+import pytest
+from hypothesis import HealthCheck, given, settings
+from hypothesis import strategies as st
+
+import oracle
+from flearn_amd import AVG
+from golden_io import assert_dict_bitwise
+
+pytestmark = pytest.mark.gpu
+
+SIZES = [0, 1, 3, 4, 63, 64, 65, 257, 1000, 4099, 44426, 70001, 262147]
+
+
+@st.composite
+def case(draw):
+    nkeys = draw(st.integers(1, 6))
+    lay = []
+    for i in range(nkeys):
+        dt = draw(st.sampled_from([np.float32, np.float32, np.float32, np.float64, np.int64]))
+        numel = draw(st.sampled_from(SIZES))
+        shape = () if (numel == 1 and draw(st.booleans())) else (numel,)
+        lay.append((f"k{i}", shape, dt))
+    n = draw(st.sampled_from([1, 2, 3, 7, 17, 64, 130]))
+    wkind = draw(st.sampled_from(["pyfloat", "pyint", "np32", "np64", "ones"]))
+    seed = draw(st.integers(0, 2**31 - 1))
+    return lay, n, wkind, seed
+
+
+@settings(max_examples=int(os.environ.get("FA_PROP_EXAMPLES", "40")), deadline=None,
+          suppress_health_check=list(HealthCheck))
+@given(c=case())
+def test_server_matches_oracle_on_random_layouts(c, cuda):
+    lay, n, wkind, seed = c
+    rng = np.random.default_rng(seed)
+    clients = []
+    for _ in range(n):
+        d = {}
+        for k, shape, dt in lay:
+            if dt == np.int64:
+                d[k] = rng.integers(-1000, 1000, size=shape).astype(np.int64)
+            else:
+                d[k] = rng.standard_normal(shape).astype(dt)
+        clients.append(d)
+    weights = {"pyfloat": [float(x) for x in rng.uniform(0.1, 3.0, n)],
+               "pyint": [int(x) for x in rng.integers(1, 600, n)],
+               "np32": [np.float32(x) for x in rng.uniform(0.1, 3.0, n)],
+               "np64": [np.float64(x) for x in rng.uniform(0.1, 3.0, n)],
+               "ones": [1.0] * n}[wkind]
+    want = oracle.server_ensemble(weights, [{k: v.copy() for k, v in cl.items()} for cl in clients])
+    got = AVG().server([{"agg_weight": w, "params": cl} for w, cl in zip(weights, clients)], 0)["w_glob"]
+    assert_dict_bitwise(got, want, f"{lay} n={n} {wkind}")
+
+
+@settings(max_examples=int(os.environ.get("FA_PROP_EXAMPLES", "40")) // 2, deadline=None,
+          suppress_health_check=list(HealthCheck))
+@given(c=case())
+def test_device_uploads_match_host_uploads(c, cuda):
+    """The same random rounds with the uploads as CUDA tensors (flearn's run2 path: the
+    row-pointer kernel and the one-launch gathers read them in place) give the values the host
+    path gives (itself bit-exact against the oracle above)."""
+    import torch
+
+    lay, n, wkind, seed = c
+    if wkind not in ("pyfloat", "ones"):
+        return  # torch uploads follow torch's promotion; the run2 simulator sends 1.0 / len(loader)
+    rng = np.random.default_rng(seed)
+    clients = [{k: (rng.integers(-1000, 1000, size=shape).astype(np.int64) if dt == np.int64
+                    else rng.standard_normal(shape).astype(dt)) for k, shape, dt in lay} for _ in range(n)]
+    weights = [float(x) for x in rng.uniform(0.1, 3.0, n)] if wkind == "pyfloat" else [1.0] * n
+    host = AVG().server([{"agg_weight": w, "params": cl} for w, cl in zip(weights, clients)], 0)["w_glob"]
+    dev_clients = [{k: torch.from_numpy(np.array(v)).to(cuda) for k, v in cl.items()} for cl in clients]  # 0-d stays 0-d
+    dev = AVG().server([{"agg_weight": w, "params": cl} for w, cl in zip(weights, dev_clients)], 0)["w_glob"]
+    assert list(dev) == list(host)
+    for k in host:
+        h = np.asarray(host[k])
+        d = dev[k].cpu().numpy() if isinstance(dev[k], torch.Tensor) else np.asarray(dev[k])
+        assert d.shape == h.shape, k
+        assert np.array_equal(d.astype(np.float64).view(np.int64), h.astype(np.float64).view(np.int64)), k
+
+
+def test_fresh_servers_reusing_a_cached_plan(cuda):
+    """Regression (found by the property test above): servers created one after another reuse
+    the module's plan cache while their pinned stagings recycle each other's blocks; the native
+    pack table must follow the pieces, not just the staging addresses.  A float64 key, an int64
+    key (int weights: its own bucket) and fp32 keys, the same round on four fresh servers."""
+    lay = [("k0", (65,), np.float64), ("k1", (262147,), np.float32), ("k2", (1000,), np.float32),
+           ("k3", (257,), np.float32), ("k4", (65,), np.int64), ("k5", (63,), np.float32)]
+    rng = np.random.default_rng(354)
+    clients = [{k: (rng.integers(-1000, 1000, size=s).astype(np.int64) if dt == np.int64
+                    else rng.standard_normal(s).astype(dt)) for k, s, dt in lay} for _ in range(2)]
+    weights = [int(x) for x in rng.integers(1, 600, 2)]
+    want = oracle.server_ensemble(weights, [{k: v.copy() for k, v in c.items()} for c in clients])
+    for rep in range(4):
+        got = AVG().server([{"agg_weight": w, "params": c} for w, c in zip(weights, clients)], rep)["w_glob"]
+        assert_dict_bitwise(got, want, f"fresh server {rep}")
