@@ -101,3 +101,55 @@ def test_fresh_servers_reusing_a_cached_plan(cuda):
     for rep in range(4):
         got = AVG().server([{"agg_weight": w, "params": c} for w, c in zip(weights, clients)], rep)["w_glob"]
         assert_dict_bitwise(got, want, f"fresh server {rep}")
+
+
+@settings(max_examples=int(os.environ.get("FA_PROP_EXAMPLES", "40")) // 2, deadline=None,
+          suppress_health_check=list(HealthCheck))
+@given(c=case(), strat=st.sampled_from(["AVG", "BN", "LG"]), shards=st.integers(1, 3),
+       out=st.sampled_from(["reference", "float32"]), http=st.booleans())
+def test_strategies_shards_outputs_and_codec(c, strat, shards, out, http, cuda):
+    """Key filters (BN: keys without "bn", bn.py:23-33; LG: the shared keys, lg.py:27-35), column
+    shards over several devices (the same GPU here), output="float32" (= fl32 of the reference's
+    float64 result for fp32 keys) and HTTP-mode uploads (the reference's base64(pickle) text
+    through flearn_amd.Encrypt) on random layouts, against the oracle."""
+    import base64
+    import pickle
+
+    from flearn_amd import BN, LG, Encrypt
+
+    lay, n, wkind, seed = c
+    lay = [(("bn." if i % 3 == 1 else "conv.") + k, s, dt) for i, (k, s, dt) in enumerate(lay)]
+    rng = np.random.default_rng(seed)
+    clients = [{k: (rng.integers(-1000, 1000, size=s).astype(np.int64) if dt == np.int64
+                    else rng.standard_normal(s).astype(dt)) for k, s, dt in lay} for _ in range(n)]
+    weights = {"pyfloat": [float(x) for x in rng.uniform(0.1, 3.0, n)],
+               "pyint": [int(x) for x in rng.integers(1, 600, n)],
+               "np32": [np.float32(x) for x in rng.uniform(0.1, 3.0, n)],
+               "np64": [np.float64(x) for x in rng.uniform(0.1, 3.0, n)],
+               "ones": [1.0] * n}[wkind]
+    keys = [k for k, _, _ in lay]
+    if strat == "BN":
+        s, key_lst = BN(), [k for k in keys if "bn" not in k]
+    elif strat == "LG":
+        shared = keys[::2]
+        s, key_lst = LG(shared), shared
+    else:
+        s, key_lst = AVG(), keys
+    if not key_lst:
+        return
+    s.output = out
+    s.devices = [cuda] * shards
+    want = oracle.server_ensemble(weights, [{k: v.copy() for k, v in cl.items()} for cl in clients], key_lst)
+    ups = [{"agg_weight": w, "params": cl} for w, cl in zip(weights, clients)]
+    if http:  # what a flearn HTTP server hands Strategy.server after receive_processing
+        enc = Encrypt(fast_min_chars=0)
+        ups = [enc.decode(base64.b64encode(pickle.dumps(u)).decode()) for u in ups]
+    got = s.server(ups, 0)["w_glob"]
+    assert set(got) == set(want)
+    for k, w in want.items():
+        g, w = np.asarray(got[k]), np.asarray(w)
+        src = dict((kk, dt) for kk, _, dt in lay)[k]
+        if out == "float32" and src == np.float32 and w.dtype == np.float64:
+            w = w.astype(np.float32)
+        assert g.shape == w.shape and g.dtype == w.dtype, (k, g.dtype, w.dtype)
+        assert np.array_equal(g.reshape(-1).view(np.uint8), w.reshape(-1).view(np.uint8)), (k, strat, shards, out, http)
