@@ -103,8 +103,6 @@ def test_fresh_servers_reusing_a_cached_plan(cuda):
         assert_dict_bitwise(got, want, f"fresh server {rep}")
 
 
-@pytest.mark.skipif(not os.environ.get("FA_PROP_STRATEGIES"),
-                    reason="not yet run on a GPU box (set FA_PROP_STRATEGIES=1)")
 @settings(max_examples=int(os.environ.get("FA_PROP_EXAMPLES", "40")) // 2, deadline=None,
           suppress_health_check=list(HealthCheck))
 @given(c=case(), strat=st.sampled_from(["AVG", "BN", "LG"]), shards=st.integers(1, 3),
