@@ -20,10 +20,16 @@ Configs (BASELINE.json):  ns  FedAVG    100 x ResNet-50 (25,610,152 fp32)      [
                           c4  FedAVG   1000 x ResNet-18
                           c5  FedOPT-Adagrad 100 x ViT-B/16 (86,567,656 fp32)
 Multi-GPU (element-range column shards + RCCL all-gather, flearn_amd/dist.py):
-  --scaling weak   (default) the job aggregates clients x G uploads on G GPUs, so every GPU
-                   streams the same bytes as the 1-GPU run (G=8 from c2: 800 clients x
-                   ResNet-18, the shape of BASELINE config 4)
-  --scaling strong the config's clients on G GPUs (each GPU reduces P/G columns)
+  --scaling strong (default) `value` is the config's fixed problem (its clients) on G GPUs, so the
+                   N-GPU values divide directly by the 1-GPU line (the north star's speedup);
+                   the weak job (clients x G uploads, every GPU streaming the 1-GPU bytes) runs
+                   after it and is reported in the "weak" field (--no-weak skips it)
+  --scaling weak   the other way round
+  stripes          by default the reduce/gather pipeline is planned per job from a two-stage
+                   model whose coefficients are fitted on the running job (reduce of the whole
+                   and 1/8 of the local width, RCCL all-gather of both; max over ranks): the
+                   "multi_gpu" field reports the widths, the model, its prediction, the measured
+                   per-rank reduce time and the exposed gather time; --stripes K fixes K stripes
   --emulate-world G  one GPU runs rank 0's share of a G-GPU job (no collective): the per-rank
                    reduce of the multi-GPU runs, measurable on a single-GPU box
 Prints ONE JSON line on rank 0 (stdout); progress goes to stderr.
@@ -48,13 +54,12 @@ sys.path.insert(0, str(REPO))
 from flearn_amd import _native as na  # noqa: E402
 from flearn_amd import aggregator as agg  # noqa: E402
 from flearn_amd import launch, layouts  # noqa: E402
-from flearn_amd.dist import ShardedReducer, ShardPlan, hip_reduce_fn  # noqa: E402
+from flearn_amd.dist import (ALIGN, ShardedReducer, ShardPlan, StripeModel, all_gather_into,  # noqa: E402
+                             hip_reduce_fn, plan_stripes)
 
 METRIC = "device-resident GiB/s, FedAVG N-client weighted tensor reduce; %HBM peak"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
 GIB = 1024.0**3
-DEFAULT_STRIPES = 2  # N>1: stripe 0's all-gather overlaps stripe 1's reduce ...
-DEFAULT_STRIPE_WEIGHTS = (3, 1)  # ... and the small last stripe leaves little of the gather exposed
 
 CONFIGS = {
     "ns": dict(layout="resnet50", clients=100, op="mean",
@@ -134,16 +139,164 @@ def load_traffic(config: str):
     return d.get("hbm_bytes_per_launch"), d.get("source")
 
 
+class Job:
+    """One aggregation job on this rank: n clients x the config's layout, this rank's block-cyclic
+    columns (plan) resident in HBM, the fused HIP reduce per stripe and (world > 1) the RCCL
+    all-gather of every stripe."""
+
+    def __init__(self, cfg, layout, n, plan, dev, world, reorder):
+        self.cfg, self.n, self.plan, self.dev = cfg, n, plan, dev
+        cols = plan.local_cols
+        log(f"[rank {plan.rank}] alloc {n} x {cols} fp32 = {n * cols * 4 / 1e9:.2f} GB, stripes {plan.widths}")
+        self.stack = torch.empty((n, cols), dtype=torch.float32, device=dev)
+        for c in range(plan.stripes):
+            lo = plan.local_begin(c)
+            agg.fill_uniform(self.stack[:, lo:], seed=2024, row_begin=0, col_begin=plan.global_begin(c),
+                             n_cols=plan.shard_of(c))
+        self.weights = torch.ones(n, dtype=torch.float32, device=dev)  # Python 1.0 -> fl32(1.0)
+        denom = float(np.sum([1.0] * n))  # np.sum(agg_weight_lst), strategy.py:127
+        epi, local_out = {}, None
+        if cfg["op"] != "mean":
+            prev = torch.empty((1, cols), dtype=torch.float32, device=dev)
+            for c in range(plan.stripes):
+                lo = plan.local_begin(c)
+                agg.fill_uniform(prev[:, lo:], seed=1, col_begin=plan.global_begin(c), n_cols=plan.shard_of(c))
+            prev = prev[0]
+            v = torch.zeros(cols, dtype=torch.float64, device=dev)
+            epi = dict(op=na.OP_BY_NAME[cfg["op"]], prev=prev, v=v)
+            local_out = prev  # the fused step advances the global model in place
+        self.fn = hip_reduce_fn(self.stack, self.weights, na.MODE_W32_DIV64, denom, reorder=reorder, **epi)
+        self.red = ShardedReducer(plan, self.fn, dev, local_out=local_out, gather=world > 1)
+
+    def release(self):
+        self.stack = self.red = self.fn = None
+        torch.cuda.empty_cache()
+
+    def reduce_only(self):
+        """The reduce launches of one step (every stripe), no collective."""
+        p = self.plan
+        for c in range(p.stripes):
+            lo, sc = p.local_begin(c), p.shard_of(c)
+            self.fn(lo, sc, self.red.local_out[lo : lo + sc])
+
+
+def _event_time(fn, reps: int) -> float:
+    """Seconds per call of fn, HIP events on torch's current stream (what the launches use)."""
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / 1e3 / reps
+
+
+def _max_over_ranks(vals, world, dev):
+    if world == 1:
+        return list(vals)
+    t = torch.tensor(list(vals), dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return t.tolist()
+
+
+def calibrate(job: Job, world: int, dev, reps: int = 5):
+    """Fit the stripe model on the running job: the reduce of the whole local width and of 1/8 of
+    it, and an all-gather of each width (real RCCL over xGMI), max over ranks.  Returns
+    (StripeModel, the raw measurements).  On one GPU (--emulate-world) the gather terms are the
+    model's a priori ones (StripeModel.assumed)."""
+    p = job.plan
+    big = p.local_cols
+    small = max(ALIGN, (big // 8) // ALIGN * ALIGN)
+    out = job.red.local_out
+    r_big = _event_time(lambda: job.fn(0, big, out[:big]), reps)
+    r_small = _event_time(lambda: job.fn(0, small, out[:small]), reps)
+    if world > 1:
+        full = torch.empty(world * big, dtype=torch.float32, device=dev)
+        for _ in range(2):  # RCCL's first calls set up channels / buffers
+            all_gather_into(full, out[:big])
+            all_gather_into(full[: world * small], out[:small])
+        torch.cuda.synchronize()
+        dist.barrier()
+        g_big = _event_time(lambda: all_gather_into(full, out[:big]), reps)
+        g_small = _event_time(lambda: all_gather_into(full[: world * small], out[:small]), reps)
+        del full
+    else:
+        m = StripeModel.assumed(job.n, p.world)
+        g_big, g_small = m.a_g + m.b_g * big, m.a_g + m.b_g * small
+    r_big, r_small, g_big, g_small = _max_over_ranks((r_big, r_small, g_big, g_small), world, dev)
+    return StripeModel.fit(big, small, r_big, r_small, g_big, g_small), dict(
+        width_cols=[big, small], reduce_us=[round(r_big * 1e6, 2), round(r_small * 1e6, 2)],
+        gather_us=[round(g_big * 1e6, 2), round(g_small * 1e6, 2)], measured_gather=world > 1)
+
+
+def run_job(cfg, layout, n, args, world, rank, dev, g_eff):
+    """Plan (calibrated stripes unless --stripes is given), warm up, time args.steps steps.
+    Returns (job, step_s, wall_s, info)."""
+    p_real = layouts.fp32_elems(layout)
+    info = {}
+    if g_eff == 1:
+        plan = ShardPlan.make(p_real, 1, 0, args.stripes or 1)
+    elif args.stripes:
+        sw = (None if args.stripe_weights in (None, "equal") or args.stripes == 1 else
+              tuple(float(x) for x in args.stripe_weights.split(",")))
+        plan = ShardPlan.make(p_real, g_eff, rank, args.stripes, weights=sw)
+        info["stripe_choice"] = "fixed by --stripes"
+    else:
+        probe = Job(cfg, layout, n, ShardPlan.make(p_real, g_eff, rank, 1), dev, world, args.reorder)
+        for _ in range(2):
+            probe.reduce_only()
+        model, cal = calibrate(probe, world, dev)
+        probe.release()
+        widths = plan_stripes(-(-p_real // g_eff), model)
+        plan = ShardPlan.from_widths(p_real, g_eff, rank, widths)
+        pred, red_s, exposed = model.makespan(plan.widths)
+        info.update(stripe_choice="model (flearn_amd.dist.plan_stripes), coefficients fitted on this job",
+                    model={"a_r_us": round(model.a_r * 1e6, 3), "b_r_ns_per_col": round(model.b_r * 1e9, 5),
+                           "a_g_us": round(model.a_g * 1e6, 3), "b_g_ns_per_col": round(model.b_g * 1e9, 5)},
+                    calibration=cal, predicted_ms=round(pred * 1e3, 4),
+                    predicted_exposed_gather_ms=round(exposed * 1e3, 4))
+    info["stripe_widths"] = list(plan.widths)
+    job = Job(cfg, layout, n, plan, dev, world, args.reorder)
+    for _ in range(args.warmup):
+        job.red.step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record()
+    for _ in range(args.steps):
+        job.red.step()
+    ev1.record()
+    torch.cuda.synchronize(dev)
+    wall = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = max(ev0.elapsed_time(ev1) / 1e3, 0.0)  # s, on the stream the kernels run on
+    elapsed, wall = _max_over_ranks((elapsed, wall), world, dev)
+    step_s = elapsed / args.steps
+    if g_eff > 1:  # this rank's reduce launches of one step alone (no collective), max over ranks
+        red_s = _max_over_ranks((_event_time(job.reduce_only, max(3, min(args.steps, 20))),), world, dev)[0]
+        info["per_rank_reduce_ms"] = round(red_s * 1e3, 4)
+        info["exposed_gather_ms"] = round(max(step_s - red_s, 0.0) * 1e3, 4)
+    return job, step_s, wall, info
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="ns", choices=sorted(CONFIGS))
-    ap.add_argument("--stripes", type=int, default=None, help="reduce/gather pipeline depth (N>1)")
+    ap.add_argument("--stripes", type=int, default=None,
+                    help="fix the reduce/gather pipeline depth (N>1); default: the calibrated model's plan")
     ap.add_argument("--stripe-weights", default=None,
-                    help="relative stripe widths, e.g. 3,1 (default for 2 stripes); 'equal' for equal")
-    ap.add_argument("--scaling", choices=("weak", "strong"), default="weak")
+                    help="relative stripe widths with --stripes, e.g. 3,1; 'equal' (default) for equal")
+    ap.add_argument("--scaling", choices=("strong", "weak"), default="strong",
+                    help="N>1: which job is `value` (the other one is reported beside it)")
+    ap.add_argument("--no-weak", action="store_true", help="N>1: skip the weak-scaling job")
     ap.add_argument("--emulate-world", type=int, default=None,
                     help="single process: time rank 0's reduce of a G-GPU job (no gather)")
     ap.add_argument("--cpu-sample", type=int, default=None, help="clients in the CPU-baseline sample")
@@ -171,88 +324,25 @@ def main():
     cfg = CONFIGS[args.config]
     layout = layouts.get(cfg["layout"])
     emu = args.emulate_world
-    if emu is not None and world != 1:
-        raise SystemExit("--emulate-world is a single-process mode")
     g_eff = emu or world  # GPUs of the (possibly emulated) job
-    n = cfg["clients"] * (g_eff if args.scaling == "weak" else 1)
     p_real = layouts.fp32_elems(layout)
-    stripes = args.stripes or (1 if g_eff == 1 else DEFAULT_STRIPES)
-    if args.stripe_weights == "equal" or stripes == 1:
-        sw = None
-    elif args.stripe_weights:
-        sw = tuple(float(x) for x in args.stripe_weights.split(","))
-    else:
-        sw = DEFAULT_STRIPE_WEIGHTS if stripes == len(DEFAULT_STRIPE_WEIGHTS) else None
-    plan = ShardPlan.make(p_real, g_eff, rank, stripes, weights=sw)
-    cols = plan.local_cols
+    strong_n, weak_n = cfg["clients"], cfg["clients"] * g_eff
+    main_n = strong_n if args.scaling == "strong" else weak_n
 
-    # ---- device-resident synthetic uploads: this rank's columns of all N clients ----
-    log(f"[rank {rank}] alloc {n} x {cols} fp32 = {n * cols * 4 / 1e9:.2f} GB")
-    stack = torch.empty((n, cols), dtype=torch.float32, device=dev)
-    for c in range(stripes):
-        lo = plan.local_begin(c)
-        agg.fill_uniform(stack[:, lo:], seed=2024, row_begin=0, col_begin=plan.global_begin(c),
-                         n_cols=plan.shard_of(c))
-    weights = torch.ones(n, dtype=torch.float32, device=dev)  # Python 1.0 -> fl32(1.0)
-    denom = float(np.sum([1.0] * n))  # np.sum(agg_weight_lst), strategy.py:127
-    epi = {}
-    local_out = None
-    if cfg["op"] != "mean":
-        prev = torch.empty((1, cols), dtype=torch.float32, device=dev)
-        for c in range(stripes):
-            lo = plan.local_begin(c)
-            agg.fill_uniform(prev[:, lo:], seed=1, col_begin=plan.global_begin(c), n_cols=plan.shard_of(c))
-        prev = prev[0]
-        v = torch.zeros(cols, dtype=torch.float64, device=dev)
-        epi = dict(op=na.OP_BY_NAME[cfg["op"]], prev=prev, v=v)
-        local_out = prev  # the fused step advances the global model in place
-    fn = hip_reduce_fn(stack, weights, na.MODE_W32_DIV64, denom, reorder=args.reorder, **epi)
-    red = ShardedReducer(plan, fn, dev, local_out=local_out, gather=world > 1)
-
-    # ---- warmup + timed steps ----
-    for _ in range(args.warmup):
-        red.step()
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    t0 = time.perf_counter()
-    ev0.record()
-    for _ in range(args.steps):
-        red.step()
-    ev1.record()
-    torch.cuda.synchronize(dev)
-    wall = time.perf_counter() - t0
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    elapsed = ev0.elapsed_time(ev1) / 1e3  # s, on the stream the kernels run on
-    elapsed = max(elapsed, 0.0)
-    if world > 1:
-        t = torch.tensor([elapsed, wall], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, wall = t.tolist()
-    step_s = elapsed / args.steps
-    job_bytes = algorithmic_bytes(n, p_real, cfg["op"])
+    job, step_s, wall, info = run_job(cfg, layout, main_n, args, world, rank, dev, g_eff)
+    cols = job.plan.local_cols
+    job_bytes = algorithmic_bytes(main_n, p_real, cfg["op"])
     if emu:  # rank 0's columns only
-        job_bytes = algorithmic_bytes(n, plan.local_cols, cfg["op"])
+        job_bytes = algorithmic_bytes(main_n, cols, cfg["op"])
     value = job_bytes / GIB / step_s
 
     # ---- roofline of the dominant kernel: per-launch algorithmic bytes / launch time ----
-    if g_eff == 1 and stripes == 1:
+    if g_eff == 1 and job.plan.stripes == 1:
         launch_s = step_s  # the step IS one kernel launch
-        launch_cols = p_real
-    else:  # time the reduce launches alone (no gather) on this rank
-        k0, k1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        k0.record()
-        for _ in range(args.steps):
-            fn(0, cols, red.local_out)
-        k1.record()
-        torch.cuda.synchronize(dev)
-        launch_s = k0.elapsed_time(k1) / 1e3 / args.steps
-        launch_cols = cols
-    launch_bytes = algorithmic_bytes(n, launch_cols, cfg["op"])
+    else:  # the reduce of this rank's whole local width as one launch (no gather)
+        launch_s = _max_over_ranks((_event_time(lambda: job.fn(0, cols, job.red.local_out), args.steps),),
+                                   world, dev)[0]
+    launch_bytes = algorithmic_bytes(main_n, cols, cfg["op"])
     achieved = launch_bytes / 1e9 / launch_s
     traffic, traffic_src = load_traffic(args.config) if g_eff == 1 else (None, None)
     roofline = {
@@ -270,11 +360,27 @@ def main():
 
     cpu = None
     if rank == 0 and g_eff == 1 and not args.no_cpu_baseline:
-        sample = args.cpu_sample or min(n, 100)
+        sample = args.cpu_sample or min(main_n, 100)
         log(f"[rank 0] CPU baseline over {sample} clients ...")
-        cpu = cpu_baseline(stack, layout, sample)
+        cpu = cpu_baseline(job.stack, layout, sample)
+
+    other = None
+    if g_eff > 1 and not args.no_weak and emu is None:
+        job.release()
+        other_n = weak_n if args.scaling == "strong" else strong_n
+        ojob, ostep, _, oinfo = run_job(cfg, layout, other_n, args, world, rank, dev, g_eff)
+        other = {
+            "scaling": "weak" if args.scaling == "strong" else "strong",
+            "clients": other_n,
+            "value": round(algorithmic_bytes(other_n, p_real, cfg["op"]) / GIB / ostep, 2),
+            "unit": "GiB/s",
+            "ms_per_step": round(ostep * 1e3, 4),
+            **oinfo,
+        }
+        ojob.release()
 
     if rank == 0:
+        weak_main = args.scaling == "weak" and g_eff > 1
         line = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -284,23 +390,24 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(step_s * 1e3, 4),
             "higher_is_better": True,
-            "scaling": args.scaling,
+            "scaling": "weak" if weak_main else "strong",
             "vs_baseline": None,
             "dtype": "fp32",
             "data": "synthetic: device-generated splitmix64 U(-1,1) client uploads, agg_weight 1.0 (flearn default)",
             "config": {
-                "workload": (cfg["workload"] if g_eff == 1 or args.scaling == "strong" else
-                             f"{cfg['workload']}, weak-scaled: {n} clients on {g_eff} GPUs"),
+                "workload": (f"{cfg['workload']}, weak-scaled: {main_n} clients on {g_eff} GPUs" if weak_main
+                             else cfg["workload"] + (f" on {g_eff} GPUs (fixed problem)" if g_eff > 1 else "")),
                 "config": args.config,
-                "clients": n,
+                "clients": main_n,
                 "params": p_real,
                 "layout": cfg["layout"],
                 "epilogue": cfg["op"],
                 "order": ("split-N allowed (fixed-order tree of client splits, <= 1e-6 normwise)" if args.reorder
                           else "reference client order (bit-exact)"),
                 "parallelism": ("single GPU" if g_eff == 1 else
-                                f"element-range shards x{g_eff} + RCCL all-gather ({stripes} stripes"
-                                + (f", widths {'/'.join(str(x) for x in plan.widths)}" if stripes > 1 else "") + ")"
+                                f"element-range shards x{g_eff} + RCCL all-gather ({job.plan.stripes} stripes"
+                                + (f", widths {'/'.join(str(x) for x in job.plan.widths)}" if job.plan.stripes > 1
+                                   else "") + ")"
                                 + (f"; EMULATED: rank 0's reduce of a {emu}-GPU job on one GPU, no gather"
                                    if emu else "")),
                 "hbm_peak_frac_of_value": round(value * GIB / 1e9 / HBM_PEAK_GBS, 4),
@@ -309,6 +416,10 @@ def main():
             "roofline": roofline,
             "cpu_baseline": cpu,
         }
+        if g_eff > 1:
+            line["multi_gpu"] = info
+            if other is not None:
+                line[other["scaling"]] = other
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()

@@ -48,28 +48,60 @@ TORCHMETA_SOURCE = HERE / "csrc" / "fa_torchmeta.cpp"  # tensor-metadata walks (
 TORCHMETA_OUT = HERE / "lib" / "libfa_torchmeta.so"
 
 
-def build_torchmeta(force: bool = False, verbose: bool = False) -> Path:
+def torch_stamp() -> str:
+    """What libfa_torchmeta.so's TensorImpl reads depend on: the torch build and its C++ ABI."""
+    import torch
+
+    return f"{torch.__version__}|cxx11abi={int(torch._C._GLIBCXX_USE_CXX11_ABI)}"
+
+
+def read_torchmeta_stamp(path: Path = None):
+    """The stamp compiled into a built libfa_torchmeta.so (fa_tm_stamp()), or None."""
+    import ctypes
+
+    try:
+        L = ctypes.PyDLL(str(path or TORCHMETA_OUT))
+        fn = L.fa_tm_stamp
+    except (OSError, AttributeError):
+        return None
+    fn.restype = ctypes.c_char_p
+    return fn().decode()
+
+
+def build_torchmeta(force: bool = False, verbose: bool = False):
     """libfa_torchmeta.so: g++ against this torch's headers, linked to its libtorch_python /
-    libtorch / libc10 (rpath: the same image on the GPU box)."""
+    libtorch / libc10 (rpath: the same image on the GPU box).  The torch version and C++ ABI
+    flag are compiled in (fa_tm_stamp); a library stamped for another torch is rebuilt here and
+    refused by _native.load_torchmeta.  Best effort: the library only speeds up checks the
+    Python side can also do, so a failed build removes it and the package works without it."""
     import sysconfig
 
     import torch
     from torch.utils.cpp_extension import include_paths
 
+    stamp = torch_stamp()
     newest = max(TORCHMETA_SOURCE.stat().st_mtime, Path(__file__).stat().st_mtime)
-    if TORCHMETA_OUT.exists() and not force and TORCHMETA_OUT.stat().st_mtime >= newest:
+    if (TORCHMETA_OUT.exists() and not force and TORCHMETA_OUT.stat().st_mtime >= newest
+            and read_torchmeta_stamp() == stamp):
         return TORCHMETA_OUT
     TORCHMETA_OUT.parent.mkdir(parents=True, exist_ok=True)
     tmp = TORCHMETA_OUT.with_suffix(".so.tmp")
     tlib = Path(torch.__file__).resolve().parent / "lib"
     cmd = [os.environ.get("CXX", "g++"), "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall",
            f"-D_GLIBCXX_USE_CXX11_ABI={int(torch._C._GLIBCXX_USE_CXX11_ABI)}",
+           f'-DFA_TM_STAMP="{stamp}"',
            f"-I{sysconfig.get_paths()['include']}"] + [f"-I{p}" for p in include_paths()] + [
            str(TORCHMETA_SOURCE), f"-L{tlib}", "-ltorch_python", "-ltorch", "-lc10",
            f"-Wl,-rpath,{tlib}", "-o", str(tmp)]
     if verbose:
         print(" ".join(cmd))
-    subprocess.run(cmd, check=True)
+    try:
+        subprocess.run(cmd, check=True)
+    except (subprocess.CalledProcessError, OSError) as e:
+        print(f"[flearn_amd] libfa_torchmeta.so not built ({e}); device uploads use the Python metadata path")
+        TORCHMETA_OUT.unlink(missing_ok=True)
+        tmp.unlink(missing_ok=True)
+        return None
     tmp.replace(TORCHMETA_OUT)
     return TORCHMETA_OUT
 

@@ -118,18 +118,25 @@ TORCHMETA_PATH = LIB_PATH.parent / "libfa_torchmeta.so"
 def load_torchmeta():
     """The tensor-metadata walks (csrc/fa_torchmeta.cpp: fa_tm_same_signature,
     fa_tm_tensor_ptrs), loaded with ctypes.PyDLL (GIL held), or None when the library is not
-    built — they only speed up checks the callers can also do in Python."""
+    built or was built for another torch (its fa_tm_stamp differs) — they only speed up checks
+    the callers can also do in Python."""
     global _torchmeta
     with _lock:
         if _torchmeta is None:
             if not TORCHMETA_PATH.exists():
                 _torchmeta = False
             else:
+                from ._build import read_torchmeta_stamp, torch_stamp
+
                 try:
                     L = ctypes.PyDLL(str(TORCHMETA_PATH))
                 except OSError:
                     _torchmeta = False
                 else:
+                    if read_torchmeta_stamp(TORCHMETA_PATH) != torch_stamp():
+                        # built against another torch: its TensorImpl reads would be undefined
+                        _torchmeta = False
+                        return None
                     O, P, I64 = ctypes.py_object, ctypes.c_void_p, ctypes.c_int64
                     L.fa_tm_same_signature.argtypes = [O, O]
                     L.fa_tm_same_signature.restype = ctypes.c_int

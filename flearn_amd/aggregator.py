@@ -26,6 +26,7 @@ from .bucket import BucketPlan, Packer, RowTable, make_plan
 from .semantics import KIND_F32, KIND_F64, KIND_I64, Numerics
 
 _F64 = np.dtype(np.float64)
+_ONE_W32 = Numerics(KIND_F32, na.MODE_W32_DIV64, np.ones(1, np.float32), 1.0, np.dtype(np.float32), _F64)  # fl32(1.0)
 
 
 def _ptr(t: torch.Tensor | None) -> int | None:
@@ -376,6 +377,7 @@ class DynState:
         self._covered = True
         self.dev_keys = ()
         self.skipped = ()
+        self.group = None  # (process group, world) when bound to a column-sharded Aggregator
 
     # -- state management -------------------------------------------------------------------
     def set_h(self, h):
@@ -480,6 +482,17 @@ class DynState:
 
     # -- host views ---------------------------------------------------------------------------
     def _host_flat(self, i):
+        """State i (0: h, 1: theta) over the whole bucket.  With a column-sharded process group
+        every rank holds only its columns: this is then a collective (an all-gather) that every
+        rank must call — reading `Dyn.h`, `set_h`, `set_theta` included."""
+        if self.group is not None:
+            from .bucket import rank_width
+            from .dist import gather_columns
+
+            (loc,) = [self.state[j][i] for j in sorted(self.state)]
+            group, world = self.group
+            stride = self._plan_f32.stride
+            return gather_columns(loc, rank_width(stride, world), stride, group).cpu().numpy()
         return np.concatenate([self.state[j][i].cpu().numpy() for j in sorted(self.state)])
 
     def sync_h(self):
@@ -573,8 +586,9 @@ class Aggregator:
         self.last_plan = plan
         stacks = self.packer.pack(plan, w_local_lst)
         fused = False
+        self._post_denom = None
         if server_opt is not None and KIND_F32 in plan.groups:
-            if self._dist and isinstance(server_opt, ServerOptimizer):
+            if self._dist:
                 server_opt.group = (self.group, self.packer.rank_cols[1])
             fused = server_opt.prepare(plan, [sh for sh, _ in stacks[KIND_F32]])
         results = {}
@@ -601,27 +615,46 @@ class Aggregator:
 
     def _gather_columns(self, plan: BucketPlan, parts):
         """Column-sharded group: every rank's reduced columns -> the whole f32 bucket on every
-        rank, one all_gather_into_tensor (RCCL over xGMI; equal padded widths)."""
+        rank, one all_gather_into_tensor (RCCL over xGMI; equal padded widths).
+
+        Plain mean in FA_MODE_W32_DIV64 with the reference's float64 output: the ranks reduced
+        with W = 1, i.e. they hold the exact fp32 sums acc (fl32(fl64(acc)/1) = acc), so the
+        gather moves P*4 bytes instead of P*8, and one 1-client reduce of the gathered sums
+        (weight fl32(1.0), W = np.sum(weights)) then computes fl64(acc)/W — the value the
+        unsharded kernel's epilogue computes, bit for bit."""
         from .bucket import Shard, rank_width
         from .dist import gather_columns
 
         (sh, out), = parts
         stride = plan.groups[KIND_F32].stride
         full = gather_columns(out[: sh.width], rank_width(stride, self.packer.rank_cols[1]), stride, self.group)
+        if self._post_denom is not None:
+            out64 = self.packer.device_bucket(("out64_full", KIND_F32), (stride,), torch.float64, self.device)
+            one = self._weights(_ONE_W32, self.device)
+            reduce_stack(full.view(1, stride), one, na.MODE_W32_DIV64, self._post_denom, out64=out64)
+            full = out64
         return [(Shard(0, self.device, 0, stride), full)]
 
     def _reduce_f32(self, g, sh, stack, w, server_opt, fused, first_means):
         nm = g.numerics
         want64 = self.output == "reference" and nm.out_dtype == _F64
+        # column-sharded plain mean with float64 output: gather fp32 sums, divide after
+        sums = self._dist and want64 and server_opt is None and nm.mode == na.MODE_W32_DIV64
+        if sums:
+            self._post_denom = float(nm.denom)
+        if sh.width == 0:  # a rank whose column range is empty (tiny model, many ranks)
+            if isinstance(server_opt, ServerOptimizer) and not fused:
+                first_means[sh.index] = torch.empty(0, dtype=torch.float32, device=sh.device)
+            gathers64 = want64 and not sums
+            return torch.empty(0, dtype=torch.float64 if gathers64 else torch.float32, device=sh.device)
+        if sums:
+            out32 = self.packer.device_bucket(("sum32", KIND_F32, sh.index), (sh.width,), torch.float32, sh.device)
+            reduce_stack(stack, w, nm.mode, 1.0, out32=out32, reorder=self.reorder and not isinstance(stack, RowTable))
+            return out32
         out64 = (self.packer.device_bucket(("out64", KIND_F32, sh.index), (sh.width,), torch.float64, sh.device)
                  if want64 else None)
         if isinstance(server_opt, DynState):
-            if self._dist:
-                raise NotImplementedError("FedDyn with a column-sharded process group (h would need a gather)")
             return server_opt.step(self, sh, stack, w, nm, want64)
-        if sh.width == 0:  # a rank whose column range is empty (tiny model, many ranks)
-            dt = torch.float64 if want64 else torch.float32
-            return torch.empty(0, dtype=dt, device=sh.device)
         if server_opt is not None and fused:
             # fused: prev is updated in place to fl32(w) — the model clients load next round
             prev, v = server_opt.state[sh.index]

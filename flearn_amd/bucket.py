@@ -129,16 +129,20 @@ def _as_array_meta(v, where):
     if isinstance(v, (np.ndarray, np.generic)):
         return v.dtype, v.shape, "numpy"
     if isinstance(v, torch.Tensor):
+        if v.layout != torch.strided:
+            # sparse / mkldnn / nested uploads: client data the engine does not take (TypeError ->
+            # the server_exception route), never a torch error from deep inside the pack
+            raise TypeError(f"{where}: {v.layout} tensor uploads are not supported (dense tensors only)")
         return np.dtype(str(v.dtype).replace("torch.", "")), tuple(v.shape), "torch"
     raise TypeError(f"{where}: unsupported value type {type(v).__name__} (expected ndarray or Tensor)")
 
 
 def _raw_signature(w, keys):
-    """(type, dtype, shape) of every selected value, as the objects report them (no
+    """(type, dtype, shape, layout) of every selected value, as the objects report them (no
     normalisation): equal signatures mean equal metadata, so only the first client needs the
     per-key checks (10,200 of them for 100 ResNet-18 uploads)."""
     try:
-        return tuple((type(v), v.dtype, v.shape) for v in map(w.__getitem__, keys))
+        return tuple((type(v), v.dtype, v.shape, getattr(v, "layout", None)) for v in map(w.__getitem__, keys))
     except (AttributeError, KeyError):
         return None
 
@@ -149,7 +153,7 @@ def _plain_dicts(w_local_lst) -> bool:
 
 
 def _same_signature_native(w_local_lst, keys) -> bool:
-    """True when every client's (type, dtype, shape) per key equals client 0's, read from the
+    """True when every client's (type, dtype, shape, layout) per key equals client 0's, read from the
     tensors' TensorImpl by csrc/fa_torchmeta.cpp (torch uploads; the same comparisons as
     _raw_signature without torch's per-attribute dispatch); False when it differs or cannot tell
     (numpy uploads, no library) — the caller then compares in Python."""
@@ -188,7 +192,7 @@ _PLANS_LOCK = threading.Lock()
 def make_plan(agg_weight_lst, w_local_lst, key_lst=None) -> BucketPlan:
     """The bucket plan of one aggregation.  A federated run aggregates the same model with the
     same weights round after round, so a plan is reused when the selected keys, every client's
-    (type, dtype, shape) per key, the client count and the weights (types and exact values, by
+    (type, dtype, shape, layout) per key, the client count and the weights (types and exact values, by
     repr: -0.0 and NaN included) all equal a recent call's."""
     if len(w_local_lst) == 0 or len(agg_weight_lst) == 0:
         raise IndexError("list index out of range")  # reference: agg_weight_lst[0] (strategy.py:123)

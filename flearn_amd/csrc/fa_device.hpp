@@ -1003,8 +1003,8 @@ __global__ __launch_bounds__(64 * W) void reduce_kernel_segrows_rm(const float* 
 template <typename E>
 __global__ __launch_bounds__(kThreads) void gather_rows_kernel(E* __restrict__ stack, int64_t stride, int n,
                                                                const E* const* __restrict__ rows,
-                                                               const int64_t* __restrict__ segs, int nseg) {
-  const int s = blockIdx.x, i = blockIdx.y;
+                                                               const int64_t* __restrict__ segs, int nseg, int i0) {
+  const int s = blockIdx.x, i = i0 + (int)blockIdx.y;  // i0: client tile (grid.y <= 65535)
   const int64_t col = segs[s], len = segs[nseg + s];
   const E* src = rows[(int64_t)s * n + i];
   E* dst = stack + (int64_t)i * stride + col;
@@ -1015,8 +1015,8 @@ __global__ __launch_bounds__(kThreads) void gather_rows_kernel(E* __restrict__ s
 // (segs[2*nseg + s]: FA_SRC_F64 copy, FA_SRC_I64 int64 -> double rounded to nearest, FA_SRC_F32).
 __global__ __launch_bounds__(kThreads) void gather_rows_f64_kernel(double* __restrict__ stack, int64_t stride, int n,
                                                                    const void* const* __restrict__ rows,
-                                                                   const int64_t* __restrict__ segs, int nseg) {
-  const int s = blockIdx.x, i = blockIdx.y;
+                                                                   const int64_t* __restrict__ segs, int nseg, int i0) {
+  const int s = blockIdx.x, i = i0 + (int)blockIdx.y;
   const int64_t col = segs[s], len = segs[nseg + s], kind = segs[2 * nseg + s];
   const void* src = rows[(int64_t)s * n + i];
   double* dst = stack + (int64_t)i * stride + col;

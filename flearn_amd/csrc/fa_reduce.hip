@@ -632,19 +632,20 @@ int fa_gather_rows(void* stack, int64_t row_stride, int32_t n_clients, int32_t e
   if (n_clients < 0 || n_segments < 0 || row_stride < 0) return fail(FA_ERR_ARG, "bad gather sizes");
   if (n_clients == 0 || n_segments == 0) return FA_OK;
   if (!stack || !rows || !segs) return fail(FA_ERR_ARG, "null gather pointer");
-  if (n_clients > 65535) return fail(FA_ERR_ARG, "too many clients for one gather");
   hipStream_t s = static_cast<hipStream_t>(stream);
-  const dim3 grid((unsigned)n_segments, (unsigned)n_clients);
-  if (elem_size == 4) {
-    hipLaunchKernelGGL(gather_rows_kernel<uint32_t>, grid, dim3(kThreads), 0, s, static_cast<uint32_t*>(stack),
-                       row_stride, n_clients, reinterpret_cast<const uint32_t* const*>(rows), segs, n_segments);
-  } else if (elem_size == 8) {
-    hipLaunchKernelGGL(gather_rows_kernel<uint64_t>, grid, dim3(kThreads), 0, s, static_cast<uint64_t*>(stack),
-                       row_stride, n_clients, reinterpret_cast<const uint64_t* const*>(rows), segs, n_segments);
-  } else {
-    return fail(FA_ERR_ARG, "elem_size must be 4 or 8");
+  if (elem_size != 4 && elem_size != 8) return fail(FA_ERR_ARG, "elem_size must be 4 or 8");
+  // one launch per tile of up to 65535 clients (the grid's y limit)
+  for (int32_t i0 = 0; i0 < n_clients; i0 += 65535) {
+    const dim3 grid((unsigned)n_segments, (unsigned)std::min<int32_t>(65535, n_clients - i0));
+    if (elem_size == 4)
+      hipLaunchKernelGGL(gather_rows_kernel<uint32_t>, grid, dim3(kThreads), 0, s, static_cast<uint32_t*>(stack),
+                         row_stride, n_clients, reinterpret_cast<const uint32_t* const*>(rows), segs, n_segments, i0);
+    else
+      hipLaunchKernelGGL(gather_rows_kernel<uint64_t>, grid, dim3(kThreads), 0, s, static_cast<uint64_t*>(stack),
+                         row_stride, n_clients, reinterpret_cast<const uint64_t* const*>(rows), segs, n_segments, i0);
+    if (int rc = launch_check()) return rc;
   }
-  return launch_check();
+  return FA_OK;
 }
 
 int fa_gather_rows_f64(double* stack, int64_t row_stride, int32_t n_clients, const void* const* rows,
@@ -652,10 +653,13 @@ int fa_gather_rows_f64(double* stack, int64_t row_stride, int32_t n_clients, con
   if (n_clients < 0 || n_segments < 0 || row_stride < 0) return fail(FA_ERR_ARG, "bad gather sizes");
   if (n_clients == 0 || n_segments == 0) return FA_OK;
   if (!stack || !rows || !segs) return fail(FA_ERR_ARG, "null gather pointer");
-  if (n_clients > 65535) return fail(FA_ERR_ARG, "too many clients for one gather");
-  hipLaunchKernelGGL(gather_rows_f64_kernel, dim3((unsigned)n_segments, (unsigned)n_clients), dim3(kThreads), 0,
-                     static_cast<hipStream_t>(stream), stack, row_stride, n_clients, rows, segs, n_segments);
-  return launch_check();
+  for (int32_t i0 = 0; i0 < n_clients; i0 += 65535) {
+    hipLaunchKernelGGL(gather_rows_f64_kernel, dim3((unsigned)n_segments, (unsigned)std::min<int32_t>(65535, n_clients - i0)),
+                       dim3(kThreads), 0, static_cast<hipStream_t>(stream), stack, row_stride, n_clients, rows, segs,
+                       n_segments, i0);
+    if (int rc = launch_check()) return rc;
+  }
+  return FA_OK;
 }
 
 int fa_fill_uniform_f32(float* dst, int64_t row_stride, int32_t n_rows, int64_t n_cols,

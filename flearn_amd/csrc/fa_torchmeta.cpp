@@ -32,8 +32,8 @@ const at::Tensor* tensor_of(PyObject* v) {
 
 extern "C" {
 
-// 1: every client's value for every key has client 0's Python type, dtype and shape (what
-// bucket.py _raw_signature compares); 0: some value differs; -1: cannot tell (a value is not a
+// 1: every client's value for every key has client 0's Python type, dtype, shape and layout
+// (what bucket.py _raw_signature compares); 0: some value differs; -1: cannot tell (a value is not a
 // torch tensor, a key is missing, an upload is not a dict) — the caller compares in Python.
 static int same_signature(PyObject* clients, PyObject* keys) {
   if (!PyList_Check(clients) || !PyTuple_Check(keys)) return kUnknown;
@@ -60,7 +60,8 @@ static int same_signature(PyObject* clients, PyObject* keys) {
         PyErr_Clear();
         return kUnknown;
       }
-      if (Py_TYPE(v) != Py_TYPE(v0) || t->scalar_type() != dt0 || t->sizes() != sz0) result = kDiffer;
+      if (Py_TYPE(v) != Py_TYPE(v0) || t->scalar_type() != dt0 || t->sizes() != sz0 || t->layout() != t0->layout())
+        result = kDiffer;
     }
   }
   return result;
@@ -104,6 +105,12 @@ static int tensor_ptrs(PyObject* clients, PyObject* keys, PyObject* dtypes, int6
   }
   return kOk;
 }
+
+#ifndef FA_TM_STAMP
+#error "build with -DFA_TM_STAMP=\"<torch version>|cxx11abi=<0|1>\"" (flearn_amd/_build.py)
+#endif
+// The torch build this library's TensorImpl reads were compiled against (checked at load time).
+const char* fa_tm_stamp() { return FA_TM_STAMP; }
 
 // C++ exceptions must not cross the ctypes boundary: any one answers "cannot tell" / "fallback"
 int fa_tm_same_signature(PyObject* clients, PyObject* keys) {

@@ -14,6 +14,17 @@ Column layout (block-cyclic, `stripes` stripes of per-rank widths S_c, multiples
 so the all-gather of stripe c writes one contiguous range of the global bucket, and stripe c's
 gather (on RCCL's stream) overlaps the reduce of stripe c+1 (on the compute stream).
 Optimizer state (prev, v_t) is sharded the same way and never communicated.
+
+The stripe widths come from a two-stage pipeline model (`StripeModel`, `plan_stripes`): stripe
+c's reduce costs a_r + b_r*S_c on the compute stream, its gather a_g + b_g*S_c on RCCL's, a
+gather starts when its stripe is reduced and the previous gather is done; the plan with the
+smallest simulated makespan over stripe counts and geometric width ratios wins.  bench.py fits
+the four coefficients on the running job (one full-width and one narrow launch of each) before
+it plans, so the schedule follows the node's measured HBM and xGMI rates.
+
+The same code runs on the gloo backend (CPU tests, and two processes sharing one GPU on a
+1-GPU box, where RCCL refuses two ranks on one device): device tensors are then staged through
+host memory around the collective (`all_gather_into`).
 """
 from __future__ import annotations
 
@@ -23,6 +34,85 @@ import torch
 import torch.distributed as dist
 
 ALIGN = 64
+
+
+def _host_staged(t: torch.Tensor, group) -> bool:
+    """gloo cannot be trusted with device tensors for every collective: stage them on the host."""
+    return t.device.type != "cpu" and dist.get_backend(group) == "gloo"
+
+
+def all_gather_into(dst: torch.Tensor, src: torch.Tensor, group=None, async_op: bool = False):
+    """dist.all_gather_into_tensor(dst, src), host-staged on gloo for device tensors (then
+    synchronous: returns None).  On RCCL it is the collective itself (async when asked)."""
+    if not _host_staged(src, group):
+        return dist.all_gather_into_tensor(dst, src, group=group, async_op=async_op)
+    hsrc = src.detach().to("cpu")
+    hdst = torch.empty(dst.shape, dtype=dst.dtype)
+    dist.all_gather_into_tensor(hdst, hsrc, group=group)
+    dst.copy_(hdst)
+    return None
+
+
+@dataclass(frozen=True)
+class StripeModel:
+    """Per-stripe cost model of one rank (seconds; widths in columns per rank).
+    reduce(S) = a_r + b_r*S on the compute stream; gather(S) = a_g + b_g*S on the collective's
+    stream (a stripe of S columns per rank is an all-gather of world*S columns)."""
+
+    a_r: float
+    b_r: float
+    a_g: float
+    b_g: float
+
+    @staticmethod
+    def assumed(n_clients: int, world: int, hbm_bytes_s: float = 7.0e12, ingress_bytes_s: float = 300e9,
+                launch_s: float = 10e-6, collective_s: float = 30e-6) -> "StripeModel":
+        """A priori coefficients: the reduce streams N*4 B per column at the measured 1-GPU rate
+        (~7 TB/s); an all-gather brings (world-1)*4 B per column into each GPU at the
+        assumed xGMI ingress rate.  bench.py replaces them with measured ones."""
+        return StripeModel(launch_s, n_clients * 4.0 / hbm_bytes_s, collective_s,
+                           max(world - 1, 0) * 4.0 / ingress_bytes_s)
+
+    @staticmethod
+    def fit(w_big: int, w_small: int, r_big: float, r_small: float, g_big: float, g_small: float) -> "StripeModel":
+        """Coefficients from two widths' measured reduce and gather times (non-negative)."""
+        def line(tb, ts):
+            b = max((tb - ts) / max(w_big - w_small, 1), 0.0)
+            return max(ts - b * w_small, 0.0), b
+
+        a_r, b_r = line(r_big, r_small)
+        a_g, b_g = line(g_big, g_small)
+        return StripeModel(a_r, b_r, a_g, b_g)
+
+    def makespan(self, widths) -> tuple:
+        """(step time, reduce-stream busy time, exposed gather time) of a stripe plan."""
+        t_red = t_gat = 0.0
+        for w in widths:
+            t_red += self.a_r + self.b_r * w
+            t_gat = max(t_red, t_gat) + self.a_g + self.b_g * w
+        return t_gat, t_red, t_gat - t_red
+
+
+def plan_stripes(local_cols: int, model: StripeModel, max_stripes: int = 8) -> tuple:
+    """Stripe widths (multiples of ALIGN summing to >= local_cols) minimising the model's makespan.
+    Candidates: k = 1..max_stripes stripes with geometric widths S_c ~ q**c for q on a grid
+    (q < 1: big stripes first, the usual choice when the reduce dominates; q > 1: a small first
+    stripe so the gathers start early, when the collective dominates)."""
+    units = max(1, -(-local_cols // ALIGN))
+    best = ((units * ALIGN,), model.makespan((units * ALIGN,))[0])
+    for k in range(2, min(max_stripes, units) + 1):
+        for q in (0.125, 0.25, 0.35, 0.5, 0.6, 0.7, 0.8, 0.9, 1.0, 1.15, 1.3, 1.5, 2.0, 3.0, 4.0):
+            raw = [q**c for c in range(k)]
+            tot = sum(raw)
+            u = [max(1, int(units * x / tot)) for x in raw]
+            u[0 if q <= 1 else -1] += units - sum(u)  # the remainder goes to the big end
+            if min(u) < 1:
+                continue
+            widths = tuple(x * ALIGN for x in u)
+            t = model.makespan(widths)[0]
+            if t < best[1] - 1e-12:
+                best = (widths, t)
+    return best[0]
 
 
 @dataclass(frozen=True)
@@ -45,6 +135,8 @@ class ShardPlan:
         weights = tuple(float(x) for x in weights)
         if len(weights) != stripes or min(weights) <= 0:
             raise ValueError("need one positive weight per stripe")
+        if stripes == 1:
+            return ShardPlan.make(n_cols, world, rank, 1)
         total = -(-max(n_cols, 1) // world)  # columns per rank
         total = -(-total // ALIGN) * ALIGN
         widths, acc = [], 0
@@ -55,6 +147,18 @@ class ShardPlan:
             acc += w
         widths.append(max(ALIGN, total - acc))
         return ShardPlan(n_cols, world, rank, tuple(widths))
+
+    @staticmethod
+    def from_widths(n_cols: int, world: int, rank: int, widths) -> "ShardPlan":
+        """A plan with explicit per-rank stripe widths (e.g. from plan_stripes)."""
+        widths = tuple(int(w) for w in widths)
+        if not widths or any(w <= 0 or w % ALIGN for w in widths):
+            raise ValueError("stripe widths must be positive multiples of ALIGN")
+        if world * sum(widths) < n_cols:
+            raise ValueError("stripes do not cover the bucket")
+        if world < 1 or not 0 <= rank < world:
+            raise ValueError("bad world / rank")
+        return ShardPlan(n_cols, world, rank, widths)
 
     @property
     def stripes(self) -> int:
@@ -130,8 +234,9 @@ class ShardedReducer:
             if self.gather:
                 g0 = p.world * lo  # stripe c's contiguous range of the global bucket
                 dst = self.full[g0 : g0 + p.world * sc]
-                works.append(dist.all_gather_into_tensor(dst, self.local_out[lo : lo + sc],
-                                                         group=self.group, async_op=True))
+                w = all_gather_into(dst, self.local_out[lo : lo + sc], group=self.group, async_op=True)
+                if w is not None:
+                    works.append(w)
         for w in works:
             w.wait()
         return self.full[: p.n_cols]
@@ -167,5 +272,5 @@ def gather_columns(local: torch.Tensor, width: int, stride: int, group=None) -> 
         src = torch.zeros(width, dtype=local.dtype, device=local.device)
         src[: local.numel()] = local
     full = torch.empty(world * width, dtype=local.dtype, device=local.device)
-    dist.all_gather_into_tensor(full, src, group=group)
+    all_gather_into(full, src, group=group)
     return full[:stride]

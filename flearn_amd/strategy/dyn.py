@@ -23,8 +23,8 @@ from .avg import AVG
 class Dyn(AVG):
     """Federated learning based on dynamic regularization (Acar et al., ICLR 2021)."""
 
-    def __init__(self, h, encrypt=None, output="reference", device=None, devices=None):
-        super().__init__(encrypt, output, device, devices)
+    def __init__(self, h, encrypt=None, output="reference", device=None, devices=None, group=None):
+        super().__init__(encrypt, output, device, devices, group)
         from ..aggregator import DynState
 
         self._dyn = DynState(h, alpha=0.01)  # alpha: dyn.py:15

@@ -22,7 +22,16 @@ from __future__ import annotations
 
 from abc import ABC, abstractmethod
 
-from .._native import NativeUnavailable
+import torch
+import torch.distributed as _dist
+
+from .._native import NativeError, NativeUnavailable
+
+#: exceptions that mean "the device or the environment failed", re-raised as they are; every
+#: other exception (NotImplementedError for unsupported client data included) takes the
+#: reference's server_exception -> SystemExit route
+_DEVICE_ERRORS = (NativeUnavailable, NativeError, torch.OutOfMemoryError, torch.AcceleratorError,
+                  _dist.DistError)
 
 
 class BaseEncrypt:
@@ -98,10 +107,10 @@ class Strategy(ABC):
         agg_weight_lst, w_local_lst = self.server_pre_processing(ensemble_params_lst)
         try:
             return self.server_ensemble(agg_weight_lst, w_local_lst, key_lst=key_lst, server_opt=server_opt)
-        except RuntimeError:
-            # NativeUnavailable / NativeError (a failed launch), torch.OutOfMemoryError, HIP runtime
-            # errors: a device or environment problem, not bad client data — never turned into
-            # the "check that the client model parameters are valid" exit
+        except _DEVICE_ERRORS:
+            # the HIP library or GPU missing, a failed launch, HIP out-of-memory or runtime
+            # errors, a failed collective: a device or environment problem, not bad client data —
+            # never turned into the "check that the client model parameters are valid" exit
             raise
         except Exception as e:  # the reference's convention (avg.py:28-31) for what numpy would raise
             self.server_exception(e)

@@ -20,10 +20,10 @@ OUT_OF_SCOPE = ("md", "pav")
 def setup_strategy(strategy_name, custom_strategy, **strategy_p):
     """Name -> strategy instance, as common/utils.py:16-58.  Unknown names fall back to
     `custom_strategy`, else SystemError.  Extra keyword arguments understood here:
-    shared_key_layers (LG / LG_R), h (Dyn), output / device / devices (engine),
+    shared_key_layers (LG / LG_R), h (Dyn), output / device / devices / group (engine),
     server_side (AVGM / OPT)."""
     shared_key_layers = strategy_p.get("shared_key_layers", None)
-    eng = {k: strategy_p[k] for k in ("output", "device", "devices") if k in strategy_p}
+    eng = {k: strategy_p[k] for k in ("output", "device", "devices", "group") if k in strategy_p}
     server_side = strategy_p.get("server_side", False)
     h = strategy_p.get("h", None)
     name = strategy_name.lower()

@@ -155,6 +155,7 @@ def lib():
             "ora_reduce_w32_div64": [P, I64, I32, P, D, I64, P],
             "ora_reduce_w32_div32": [P, I64, I32, P, ctypes.c_float, I64, P],
             "ora_reduce_w64": [P, I64, I32, P, D, I64, P],
+            "ora_sum_w32_splitn": [P, I64, I32, P, I32, I64, P],
             "ora_reduce_f64": [P, I64, I32, P, D, I64, P],
             "ora_reduce_i64": [P, I64, I32, P, D, I64, P],
             "ora_update_f64": [I32, P, P, P, D, D, D, D, I64, P],
@@ -207,6 +208,22 @@ def c_reduce(mode, stack, weights, denom):
     else:
         raise ValueError(mode)
     return out
+
+
+def c_reduce_splitn(mode, stack, weights, denom, splits=4):
+    """The split-N kernel's order (ora_sum_w32_splitn) for the fp32-weight modes, then the mode's
+    divide: f64 [P] for MODE_W32_DIV64, fp32 for MODE_W32_DIV32 — as c_reduce returns them."""
+    L = lib()
+    n, p = stack.shape
+    stack = np.ascontiguousarray(stack, np.float32)
+    w = np.ascontiguousarray(weights, np.float32)
+    acc = np.empty(p, np.float32)
+    L.ora_sum_w32_splitn(_ptr(stack), p, n, _ptr(w), int(splits), p, _ptr(acc))
+    if mode == MODE_W32_DIV64:
+        return acc.astype(np.float64) / float(denom)
+    if mode == MODE_W32_DIV32:
+        return acc / np.float32(denom)
+    raise ValueError("split-N order is defined here for the fp32-weight modes")
 
 
 def c_update(op, g, local32, v, beta=0.9, eta=1e-1, tau=1e-9, beta2=0.99):

@@ -58,6 +58,34 @@ void ora_reduce_w32_div32(const float* stack, int64_t stride, int32_t n, const f
   free(acc);
 }
 
+/* The ORDER of the opt-in split-N kernel (flearn_amd/csrc/fa_device.hpp reduce_kernel_splitn),
+ * not the reference's: clients cut into `nsplit` contiguous splits [v*n/nsplit, (v+1)*n/nsplit),
+ * each summed in list order from its first product (fl32(w*x) products, fp32 sums), combined by
+ * the fixed tree ((p0+p1)+(p2+p3))+...  Returns the fp32 sums (the caller divides as the mode
+ * does).  Used by the tests to pin that kernel bit for bit and to measure how far its order
+ * lies from the reference's sequential sum. */
+void ora_sum_w32_splitn(const float* stack, int64_t stride, int32_t n, const float* w, int32_t nsplit,
+                        int64_t ncols, float* out) {
+  float* part = (float*)malloc((size_t)(ncols > 0 ? ncols : 1) * (size_t)nsplit * sizeof(float));
+  for (int32_t v = 0; v < nsplit; ++v) {
+    const int32_t r0 = (int32_t)((int64_t)v * n / nsplit), r1 = (int32_t)((int64_t)(v + 1) * n / nsplit);
+    float* acc = part + (int64_t)v * ncols;
+    for (int64_t p = 0; p < ncols; ++p) acc[p] = r0 < r1 ? w[r0] * stack[(int64_t)r0 * stride + p] : 0.0f;
+    for (int32_t i = r0 + 1; i < r1; ++i) {
+      const float* row = stack + (int64_t)i * stride;
+      for (int64_t p = 0; p < ncols; ++p) {
+        const float prod = w[i] * row[p];
+        acc[p] = acc[p] + prod;
+      }
+    }
+  }
+  for (int32_t h = 1; h < nsplit; h *= 2)
+    for (int32_t v = 0; v + h < nsplit; v += 2 * h)
+      for (int64_t p = 0; p < ncols; ++p) part[(int64_t)v * ncols + p] = part[(int64_t)v * ncols + p] + part[(int64_t)(v + h) * ncols + p];
+  memcpy(out, part, (size_t)ncols * sizeof(float));
+  free(part);
+}
+
 /* np.float64 / np.int64 weights on fp32 tensors: promoted to f64 for product and sum. */
 void ora_reduce_w64(const float* stack, int64_t stride, int32_t n, const double* w, double denom,
                     int64_t ncols, double* out64) {

@@ -27,7 +27,14 @@ def _worker(rank, world, port, n, p, stripes, op, weights=None):
 
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     try:
-        plan = ShardPlan.make(p, world, rank, stripes, weights=weights)
+        if weights == "model":  # bench's default: widths from the two-stage pipeline model
+            from flearn_amd.dist import StripeModel, plan_stripes
+
+            model = StripeModel(1e-6, 5e-9, 2e-6, 1e-8)  # gather-bound: small stripes first
+            plan = ShardPlan.from_widths(p, world, rank, plan_stripes(-(-p // world), model))
+            assert plan.stripes == stripes and plan.widths[0] < plan.widths[-1], plan.widths
+        else:
+            plan = ShardPlan.make(p, world, rank, stripes, weights=weights)
         local = np.zeros((n, plan.local_cols), np.float32)
         prev = np.zeros(plan.local_cols, np.float32)
         for c in range(stripes):
@@ -76,10 +83,12 @@ def test_sharded_reduce_four_ranks():
 
 
 def test_sharded_reduce_eight_ranks():
-    """The driver's scaling run at G=8 with bench's default stripes (3:1), fused Adagrad, and a
-    width whose last rank's slices are partly padding."""
+    """The driver's scaling run at G=8, fused Adagrad, a width whose last rank's slices are
+    partly padding: 3:1 stripes, and the model-planned stripes bench.py uses by default (with
+    coefficients scaled so this small bucket gets several stripes, small ones first)."""
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     mp.spawn(_worker, args=(8, _free_port(), 3, 40_001, 2, "adagrad", (3, 1)), nprocs=8, join=True)
+    mp.spawn(_worker, args=(8, _free_port(), 3, 40_001, 3, "adagrad", "model"), nprocs=8, join=True)
 
 
 def _gather_worker(rank, world, port, stride, dtype):

@@ -1,0 +1,73 @@
+"""Multi-rank product paths with the real HIP kernels, on the one GPU of the box.
+
+Each test starts `world` FRESH processes (torch.multiprocessing, spawn context: a new
+interpreter per rank) that all use cuda:0 and form a gloo group — RCCL refuses two ranks on one
+device.  The ranks run tests/multirank_worker.py's cases: the Strategy `group=` path (SPMD
+server, the call behind flearn's Server.py:140: strategy.py:102-130, avgm.py:19-36,
+opt.py:52-63, dyn.py:17-36) and bench.py's ShardedReducer, each rank checking its reassembled
+model bit for bit against the reference's fixtures or the C oracle.  What this cannot cover on
+one GPU: RCCL itself and xGMI (the driver's multi-GPU scaling run exercises those).
+"""
+import os
+import socket
+import time
+
+import pytest
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _run_ranks(world, names, deadline_s=240):
+    from multirank_worker import rank_main
+
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    ctx = mp.start_processes(rank_main, args=(world, _free_port(), tuple(names)), nprocs=world, join=False,
+                             start_method="spawn")
+    t_end = time.monotonic() + deadline_s
+    try:
+        while not ctx.join(timeout=5):
+            if time.monotonic() > t_end:
+                raise TimeoutError(f"{world} ranks did not finish {names} within {deadline_s} s")
+    finally:
+        for p in ctx.processes:
+            if p.is_alive():
+                p.kill()
+                p.join(10)
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("world", [2, 3])
+def test_strategy_group_fixtures(world, cuda):
+    """AVG / BN / LG / LG_R(group=True) on every reduce fixture, output='float32', setup_strategy."""
+    _run_ranks(world, ["avg_fixtures", "setup_strategy"])
+
+
+@pytest.mark.timeout(300)
+def test_strategy_group_fused_and_dyn(cuda):
+    """AVGM / OPT(adagrad, yogi, adam)(server_side=True, group=True) 3-round fixtures incl. the
+    gathered v_t, the first-round adopt path, and Dyn(h, group=True) 3 rounds (w, h, theta)."""
+    _run_ranks(2, ["fused_rounds", "first_round_adopt", "dyn"])
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_strategy_group_empty_ranks(world, cuda):
+    """A model narrower than the ranks: the last ranks own no columns and still join every
+    collective (world 4 and 8: ranks with empty column ranges)."""
+    _run_ranks(world, ["empty_ranks"])
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_reducer_hip_ranks(world, cuda):
+    """bench.py's ShardedReducer with the HIP kernel on every rank: 1 stripe, 3:1 stripes and the
+    model-planned stripes; mean, fused AVGM and Adagrad over two steps."""
+    _run_ranks(world, ["sharded_reducer"])

@@ -77,6 +77,32 @@ def test_gather_rows_f64_converts_like_numpy(cuda):
         assert bitwise_equal(got[i], want), i
 
 
+def test_gather_rows_more_clients_than_one_grid_dimension(cuda):
+    """fa_gather_rows / fa_gather_rows_f64 tile the launch over blocks of 65,535
+    clients (the grid's y limit) instead of refusing a bigger round: 70,001 clients."""
+    L = na.load()
+    n, stride = 70_001, 64
+    src32 = torch.arange(2 * n, dtype=torch.float32, device=cuda) * 0.5
+    src64 = torch.arange(n, dtype=torch.int64, device=cuda) * 3 - 7
+    segs = torch.tensor([0, 5, 1, 2], dtype=torch.int64, device=cuda)  # cols 0, 5; lengths 1, 2
+    base = src32.data_ptr()
+    ptrs = torch.tensor(np.concatenate([base + 4 * np.arange(n, dtype=np.int64),  # segment 0: element i
+                                        base + 4 * (n - 2 + 0 * np.arange(n, dtype=np.int64))]),  # segment 1
+                        dtype=torch.int64, device=cuda)
+    stack = torch.full((n, stride), -1.0, dtype=torch.float32, device=cuda)
+    na.check(L.fa_gather_rows(stack.data_ptr(), stride, n, 4, ptrs.data_ptr(), segs.data_ptr(), 2,
+                              na.stream_handle(cuda)), "gather")
+    got = stack.cpu().numpy()
+    assert bitwise_equal(got[:, 0], src32[:n].cpu().numpy())
+    assert (got[:, 5:7] == src32[n - 2 : n].cpu().numpy()).all() and (got[:, 1:5] == -1).all()
+    ptr64 = torch.tensor(src64.data_ptr() + 8 * np.arange(n, dtype=np.int64), dtype=torch.int64, device=cuda)
+    segs64 = torch.tensor([3, 1, na.SRC_I64], dtype=torch.int64, device=cuda)
+    st64 = torch.zeros((n, stride), dtype=torch.float64, device=cuda)
+    na.check(L.fa_gather_rows_f64(st64.data_ptr(), stride, n, ptr64.data_ptr(), segs64.data_ptr(), 1,
+                                  na.stream_handle(cuda)), "gather f64")
+    assert bitwise_equal(st64[:, 3].cpu().numpy(), src64.cpu().numpy().astype(np.float64))
+
+
 def test_unaligned_device_uploads_take_one_gather(cuda):
     """Views at odd element offsets cannot feed 16-B buffer loads: one fa_gather_rows launch
     packs them, and the result is still bit-exact."""

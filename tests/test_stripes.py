@@ -1,0 +1,61 @@
+"""The multi-GPU stripe planner (flearn_amd.dist.StripeModel / plan_stripes): the two-stage
+pipeline model behind bench.py's stripe choice, and the plans it produces."""
+import pytest
+
+from flearn_amd.dist import ALIGN, ShardPlan, StripeModel, plan_stripes
+
+
+def test_makespan_two_stage_pipeline():
+    m = StripeModel(a_r=1.0, b_r=0.0, a_g=2.0, b_g=0.0)
+    # reduces end at 1, 2, 3; gathers run back to back from t=1: 3, 5, 7
+    assert m.makespan((64, 64, 64)) == (7.0, 3.0, 4.0)
+    m = StripeModel(a_r=0.0, b_r=1.0, a_g=0.0, b_g=0.25)
+    # reduce-bound: stripe 0's gather (48) hides behind stripe 1's reduce (64), only the last
+    # stripe's gather (16) is exposed
+    t, red, exp = m.makespan((192, 64))
+    assert (t, red, exp) == (256 + 16, 256, 16)
+    # gather-bound: stripe 1's gather waits for stripe 0's
+    t, red, exp = StripeModel(0.0, 1.0, 0.0, 0.5).makespan((192, 64))
+    assert (t, red, exp) == (192 + 96 + 32, 256, 64)
+
+
+@pytest.mark.parametrize("cols", [1, 63, 64, 5001, 3_201_269, 10_820_957])
+@pytest.mark.parametrize("model", [StripeModel.assumed(100, 8), StripeModel.assumed(1000, 8),
+                                   StripeModel.assumed(100, 2), StripeModel(1e-6, 5e-9, 2e-6, 1e-8)])
+def test_plan_covers_and_aligns(cols, model):
+    w = plan_stripes(cols, model)
+    assert all(x > 0 and x % ALIGN == 0 for x in w)
+    assert sum(w) == -(-cols // ALIGN) * ALIGN
+    assert 1 <= len(w) <= 8
+    # never worse than the unstriped step
+    assert model.makespan(w)[0] <= model.makespan((sum(w),))[0] + 1e-15
+
+
+def test_plan_shapes_follow_the_bottleneck():
+    lc = 3_201_269  # NS per rank at G = 8
+    gather_bound = StripeModel(10e-6, 100 * 4 / 7e12, 30e-6, 7 * 4 / 150e9)
+    w = plan_stripes(lc, gather_bound)
+    assert len(w) >= 2 and w[0] < w[-1]  # start the gathers early
+    reduce_bound = StripeModel(10e-6, 1000 * 4 / 7e12, 30e-6, 7 * 4 / 300e9)
+    w = plan_stripes(lc, reduce_bound)
+    assert len(w) >= 2 and w[0] > w[-1]  # hide all but a small last gather
+    no_collective = StripeModel(10e-6, 100 * 4 / 7e12, 0.0, 0.0)
+    assert len(plan_stripes(lc, no_collective)) == 1
+
+
+def test_fit_recovers_lines():
+    m = StripeModel.fit(8000, 1000, r_big=10 + 8000 * 2, r_small=10 + 1000 * 2, g_big=30 + 8000 * 5,
+                        g_small=30 + 1000 * 5)
+    assert m == pytest.approx(StripeModel(10, 2, 30, 5))
+    m = StripeModel.fit(8000, 1000, 5.0, 6.0, 1.0, 1.0)  # noisy: slopes clamp at 0
+    assert m.b_r == 0 and m.a_r == 6.0 and m.b_g == 0
+
+
+def test_from_widths_layout():
+    plan = ShardPlan.from_widths(1000, 4, 1, (64, 128, 64))
+    assert plan.local_cols == 256 and plan.padded == 1024
+    assert plan.global_begin(1) == 4 * 64 + 128  # stripe 1 starts at W*O_1, rank 1 after rank 0
+    with pytest.raises(ValueError):
+        ShardPlan.from_widths(1000, 4, 0, (64, 100))
+    with pytest.raises(ValueError):
+        ShardPlan.from_widths(10_000, 4, 0, (64, 64))
