@@ -194,7 +194,8 @@ def _event_time(fn, reps: int) -> float:
 def _max_over_ranks(vals, world, dev):
     if world == 1:
         return list(vals)
-    t = torch.tensor(list(vals), dtype=torch.float64, device=dev)
+    on = dev if dist.get_backend() == "nccl" else "cpu"  # gloo: host tensors
+    t = torch.tensor(list(vals), dtype=torch.float64, device=on)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return t.tolist()
 
@@ -315,11 +316,20 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # FLEARN_BENCH_BACKEND=gloo (tests/test_gpu_bench.py): rehearse the N>1 path with several
+    # ranks sharing the GPUs there are (RCCL refuses two ranks on one device); the gather is then
+    # host-staged and its times say nothing about xGMI.  The real runs use RCCL.
+    backend = os.environ.get("FLEARN_BENCH_BACKEND", "nccl")
     na.lib()
+    if backend != "nccl":
+        local_rank %= max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     cfg = CONFIGS[args.config]
     layout = layouts.get(cfg["layout"])
@@ -418,6 +428,8 @@ def main():
         }
         if g_eff > 1:
             line["multi_gpu"] = info
+            if world > 1 and backend != "nccl":
+                line["multi_gpu"]["backend"] = f"{backend} (rehearsal: host-staged gather, not xGMI)"
             if other is not None:
                 line[other["scaling"]] = other
         print(json.dumps(line), flush=True)

@@ -1292,6 +1292,57 @@ __global__ __launch_bounds__(64 * W) void reduce_kernel_rowmajor(const float* __
 #undef FA_RM_GROUP
 }
 
+// Row-major groups with a dynamically claimed tail.  The blocks of reduce_kernel_rowmajor end
+// their last group over a spread of ~60 us (C3: 4% of the launch; the per-block stream rate
+// differs with its XCD and HBM channels, DESIGN §4 finding 11), and a static split cannot know
+// which blocks will be late.  Here the window's first `ncols_static` columns are the static
+// row-major groups, and the rest is cut into STRIPS of W KiB of every row (one quad per lane),
+// claimed one at a time from a device counter by whichever block is free: a strip sweeps all N
+// rows TD deep (TD*W KiB in flight, like a group step) and applies the epilogue to its columns.
+// A strip is short (100 rows x 8 KiB ~ 20 us), so the blocks finish within about one strip of
+// each other.  Per element the sum is still rows 0..N-1 in list order (bit-exact): a column is
+// summed by exactly one block, static or strip.  *work must be 0 at launch.
+template <class P, typename T, int OP, int V, int D, int W, int KG, bool NT, int TD, int EPIB = (V >= 2 ? 2 : V)>
+__global__ __launch_bounds__(64 * W) void reduce_kernel_rowmajor_tail(const float* __restrict__ stack,
+                                                                      int64_t stride, int n,
+                                                                      const typename P::w_t* __restrict__ w,
+                                                                      int64_t col0, int64_t ncols_static,
+                                                                      int64_t ncols, Epi<T> e,
+                                                                      int* __restrict__ work) {
+  static_assert(sizeof(typename P::x_t) == 4, "row pipeline is for 4-byte elements");
+  const int64_t g = gridDim.x;
+  const int64_t row_bytes = stride * 4;
+  const char* base = reinterpret_cast<const char*>(stack + col0);
+  if (ncols_static > 0) {
+    const int64_t nquads_s = (ncols_static + 3) / 4;
+    const int64_t chunks_s = (nquads_s + 63) / 64;
+    const int64_t k = (chunks_s + g * W * V - 1) / (g * W * V);
+    const int64_t pc = (chunks_s + g * k - 1) / (g * k);
+    const int64_t pieces = (chunks_s + pc - 1) / pc;
+    int gi = 0;
+    for (int64_t g0 = 0; g0 < k; g0 += KG)
+      rowmajor_group<P, T, OP, V, D, W, KG, NT, EPIB, false>(base, row_bytes, n, w, g0, k, pc, pieces, nquads_s,
+                                                            ncols_static, gi++, e);
+  }
+  // the tail: strips of 64*W quads from quad ncols_static/4 (ncols_static is a multiple of 4)
+  const int64_t nquads = (ncols + 3) / 4;
+  const int64_t qt0 = ncols_static / 4;
+  const int64_t strips = (nquads - qt0 + 64 * W - 1) / (64 * W);
+  __shared__ int s_claim;
+  if (threadIdx.x == 0) s_claim = atomicAdd(work, 1);
+  __syncthreads();
+  int s = s_claim;
+  while (s < strips) {
+    const int64_t qs = qt0 + (int64_t)s * 64 * W;
+    const int64_t qe = qs + 64 * W < nquads ? qs + 64 * W : nquads;
+    rows_piece<P, T, OP, 1, TD, W, NT>(stack, stride, n, w, col0, ncols, e, qs, qe);
+    __syncthreads();  // every wave is done with s_claim and its strip
+    if (threadIdx.x == 0) s_claim = atomicAdd(work, 1);
+    __syncthreads();
+    s = s_claim;
+  }
+}
+
 // Column-blocked client stack: element (n, c) lives at ((c / B) * N + n) * B + c % B with
 // B = kThreads*V*4 columns (one tile).  Tile b's N rows are one contiguous N*B*4-byte region, so
 // a block streams its whole tile linearly (rows B*4 bytes apart) — the access pattern of a plain

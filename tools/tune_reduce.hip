@@ -373,6 +373,26 @@ Variant make_rowmajor(const float* stack, int64_t stride, int n, const float* w,
           true, {}};
 }
 
+// row-major groups over the first (1 - tail) of the window, then W-KiB strips claimed from a
+// device counter (reduce_kernel_rowmajor_tail); the counter is cleared on the stream before every
+// launch (part of the timed work, as in the product)
+template <int V, int D, int W, int KG, int TD, int OP, typename T>
+Variant make_rmtail(const float* stack, int64_t stride, int n, const float* w, int64_t ncols, Epi<T> e,
+                    double bytes, int64_t grid, double tail, int* work) {
+  const int64_t chunks = ((ncols + 3) / 4 + 63) / 64;
+  if (grid > chunks) grid = chunks;
+  const int64_t ns = (int64_t)((double)ncols * (1.0 - tail)) / 256 * 256;
+  char name[96];
+  snprintf(name, sizeof name, "rmtail V%d W%d KG%d TD%d g%lld t%.3f", V, W, KG, TD, (long long)grid, tail);
+  return {name, bytes,
+          [=] {
+            CK(hipMemsetAsync(work, 0, sizeof(int), 0));
+            hipLaunchKernelGGL((reduce_kernel_rowmajor_tail<AccF32, T, OP, V, D, W, KG, true, TD>), dim3((unsigned)grid),
+                               dim3(64 * W), 0, 0, stack, stride, n, w, (int64_t)0, ns, ncols, e, work);
+          },
+          true, {}};
+}
+
 template <int V, int W, int KG, int OP, typename T, int TM>
 Variant make_dfr(const float* stack, int64_t stride, int n, const float* w, int64_t ncols, Epi<T> e,
                  double bytes, int64_t grid) {
@@ -490,6 +510,8 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&prev, stride * 4));
   CK(hipMalloc(&v, stride * 8));
   CK(hipMalloc(&sink, 4096));
+  int* work;
+  CK(hipMalloc(&work, 256));
   const int64_t copy_quads = (int64_t)n * stride / 8;  // copy half the stack into the other half
   copy_dst = stack + copy_quads * 4;
   hipLaunchKernelGGL(fill_uniform_kernel, dim3(4096, n), dim3(256), 0, 0, stack, stride, stride, 2024ull,
@@ -663,6 +685,28 @@ int main(int argc, char** argv) {
     DFR(8, 8, 2, 196, 0);
     DFR(8, 8, 1, 192, 2);
     DFR(8, 8, 1, 192, 0);
+  }
+#define RMT(V, D, W, KG, TD, G, TAIL)                                                                            \
+  vs.push_back(op == FA_OP_AVGM      ? make_rmtail<V, D, W, KG, TD, FA_OP_AVGM, double>(stack, stride, n, w, ncols, e, bytes, G, TAIL, work)   \
+               : op == FA_OP_ADAGRAD ? make_rmtail<V, D, W, KG, TD, FA_OP_ADAGRAD, double>(stack, stride, n, w, ncols, e, bytes, G, TAIL, work) \
+                                     : make_rmtail<V, D, W, KG, TD, FA_OP_MEAN, double>(stack, stride, n, w, ncols, e, bytes, G, TAIL, work))
+  if (!strcmp(set, "tail")) {  // row-major groups + a dynamically claimed tail of W-KiB strips
+    const int64_t chunks = ((ncols + 3) / 4 + 63) / 64;
+    const int64_t k = (chunks + 192 * 64 - 1) / (192 * 64);
+    if (k % 3 == 0) {
+      RM(16, 1, 4, 3, 192);  // the product geometry of NS / C3 (first: the bitwise reference)
+    } else {
+      RM(16, 1, 4, 4, 192);  // C5 (k = 28)
+    }
+    RM(8, 1, 8, 4, 192);
+    RMT(16, 1, 4, 4, 16, 192, 0.11);  // 8 pieces of ~58 chunks static (2 groups of 4) + ~11% strips
+    RMT(16, 1, 4, 4, 16, 192, 0.06);
+    RMT(16, 1, 4, 4, 16, 192, 0.16);
+    RMT(8, 1, 8, 4, 8, 192, 0.11);
+    RMT(16, 1, 4, 3, 16, 192, 0.11);
+    RMT(16, 1, 4, 2, 16, 192, 0.11);
+    RMT(16, 1, 4, 4, 16, 208, 0.11);
+    RMT(16, 1, 4, 4, 8, 192, 0.11);
   }
   if (!strcmp(set, "nsgrid")) {  // north-star shape: group size / grid / piece width
     RM(8, 1, 8, 3, 192);
