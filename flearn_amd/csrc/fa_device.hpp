@@ -787,7 +787,10 @@ __global__ __launch_bounds__(64 * W) void reduce_kernel_segrows(const float* con
 //     split order, ((p0+p1)+(p2+p3))+..., one barrier per level;
 //   * then the epilogue of the row pipeline (divide, optional optimizer update, stores).
 // Deterministic (the tree does not depend on scheduling) but NOT the reference's sequential
-// order: opt-in, checked at <= 1e-6 normwise relative error per tensor (tests/test_gpu_splitn.py).
+// order: opt-in, checked at <= 1e-6 normwise relative error per tensor (tests/test_gpu_splitn.py)
+// — except columns whose terms nearly cancel (sum of |products| > 2 |sum|, or a non-finite
+// sum): those are re-summed in list order by wave 0 (the cancellation guard below), bit-exact.
+// oracle.c_reduce_splitn restates this exact order and guard (the tests pin it bit for bit).
 // Needs n >= W (every split non-empty; the host falls back to the sequential kernel otherwise).
 template <class P, typename T, int OP, int W, int D, bool NT, bool STRIDED = false>
 __global__ __launch_bounds__(64 * W) void reduce_kernel_splitn(const float* __restrict__ stack, int64_t stride, int n,
@@ -796,6 +799,7 @@ __global__ __launch_bounds__(64 * W) void reduce_kernel_splitn(const float* __re
   typedef typename P::acc_t A;
   typedef typename vec4<A>::type AV;
   __shared__ AV part[W][64];
+  __shared__ AV apart[W][64];  // the splits' sums of |product|: the cancellation guard
   const int lane = (int)threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);  // the split: wave-uniform
   // the chunk's columns, its last quad possibly partial: the raw buffer range check is per dword
@@ -810,16 +814,21 @@ __global__ __launch_bounds__(64 * W) void reduce_kernel_splitn(const float* __re
   const int r0 = STRIDED ? wv : (int)((int64_t)wv * n / W);
   const int r1 = STRIDED ? n : (int)((int64_t)(wv + 1) * n / W);
   constexpr int RS = STRIDED ? W : 1;  // row step of a split
-  AV acc = {A(0), A(0), A(0), A(0)};
+  typedef typename vec4<float>::type XV;
+  const char* tile00 = reinterpret_cast<const char*>(stack + col0 + qb * 4);
+  const uint32_t bytes = (uint32_t)tcols * 4u;
+  const int voff = lane * 16;
+  AV acc = {A(0), A(0), A(0), A(0)}, aacc = {A(0), A(0), A(0), A(0)};
+  auto absq = [](AV v) { return AV{v[0] < A(0) ? -v[0] : v[0], v[1] < A(0) ? -v[1] : v[1],
+                                   v[2] < A(0) ? -v[2] : v[2], v[3] < A(0) ? -v[3] : v[3]}; };
   if (nq > 0) {
     // this split's rows through a D-deep rolling pipeline with NO guarded loads: a slot past the
     // split's end re-reads its last row (a cache hit) and the product is discarded by a select,
-    // so the loads stay unconditional and the ramp is not serialised by waitcnt merges
-    typedef typename vec4<float>::type XV;
-    const char* tile0 = reinterpret_cast<const char*>(stack + col0 + qb * 4) + (int64_t)r0 * stride * 4;
+    // so the loads stay unconditional and the ramp is not serialised by waitcnt merges.  Each
+    // product p = fl(w*x) feeds the running sum (acc + p: the same rounding as acc + w*x, no
+    // contraction) and the running sum of |p|
+    const char* tile0 = tile00 + (int64_t)r0 * stride * 4;
     const int64_t row_bytes = stride * 4 * RS;
-    const uint32_t bytes = (uint32_t)tcols * 4u;
-    const int voff = lane * 16;
     const int cnt = (r1 - r0 + RS - 1) / RS;  // >= 1
     const typename P::w_t* ws = w + r0;
     XV x[D];
@@ -827,14 +836,16 @@ __global__ __launch_bounds__(64 * W) void reduce_kernel_splitn(const float* __re
     for (int d = 0; d < D; ++d)
       x[d] = buf_load_quad<NT>(row_rsrc(tile0 + (int64_t)(d < cnt ? d : cnt - 1) * row_bytes, bytes), voff, 0);
     acc = quad_mul<P>(ws[0], x[0]);
+    aacc = absq(acc);
     {
       const int r = D < cnt ? D : cnt - 1;
       x[0] = buf_load_quad<NT>(row_rsrc(tile0 + (int64_t)r * row_bytes, bytes), voff, 0);
     }
 #pragma unroll
     for (int d = 1; d < D; ++d) {  // rows 1..D-1
-      const AV t = quad_axpy<P>(acc, ws[(d < cnt ? d : 0) * RS], x[d]);
-      acc = d < cnt ? t : acc;
+      const AV p = quad_mul<P>(ws[(d < cnt ? d : 0) * RS], x[d]);
+      acc = d < cnt ? acc + p : acc;
+      aacc = d < cnt ? aacc + absq(p) : aacc;
       __builtin_amdgcn_sched_barrier(0);
       const int r = d + D < cnt ? d + D : cnt - 1;
       x[d] = buf_load_quad<NT>(row_rsrc(tile0 + (int64_t)r * row_bytes, bytes), voff, 0);
@@ -844,8 +855,9 @@ __global__ __launch_bounds__(64 * W) void reduce_kernel_splitn(const float* __re
 #pragma unroll
       for (int d = 0; d < D; ++d) {
         const int i = base + d;
-        const AV t = quad_axpy<P>(acc, ws[(i < cnt ? i : 0) * RS], x[d]);
-        acc = i < cnt ? t : acc;
+        const AV p = quad_mul<P>(ws[(i < cnt ? i : 0) * RS], x[d]);
+        acc = i < cnt ? acc + p : acc;
+        aacc = i < cnt ? aacc + absq(p) : aacc;
         __builtin_amdgcn_sched_barrier(0);
         const int r = i + D < cnt ? i + D : cnt - 1;
         x[d] = buf_load_quad<NT>(row_rsrc(tile0 + (int64_t)r * row_bytes, bytes), voff, 0);
@@ -854,15 +866,38 @@ __global__ __launch_bounds__(64 * W) void reduce_kernel_splitn(const float* __re
     }
   }
   part[wv][lane] = acc;
+  apart[wv][lane] = aacc;
   __syncthreads();
 #pragma unroll
   for (int h = 1; h < W; h *= 2) {  // fixed tree over the splits, one level per barrier
-    if ((wv % (2 * h)) == 0 && wv + h < W) part[wv][lane] = part[wv][lane] + part[wv + h][lane];
+    if ((wv % (2 * h)) == 0 && wv + h < W) {
+      part[wv][lane] = part[wv][lane] + part[wv + h][lane];
+      apart[wv][lane] = apart[wv][lane] + apart[wv + h][lane];
+    }
     __syncthreads();
   }
   if (wv == 0) {
-    const AV r[1] = {part[0][lane]};
-    finish_piece<T, OP, A, 1, 64, 1>(e, qb, tcols, r);
+    // cancellation guard: a column whose sum is not at least half its sum of |products|
+    // (!(S_abs <= 2|S|): also NaN / inf) takes the reference's sequential sum instead — a
+    // reordered sum of nearly cancelling terms can lie arbitrarily far (relatively) from the
+    // sequential one; every other column is within the reordering's rounding error of it
+    AV r = part[0][lane];
+    const AV aa = apart[0][lane];
+    bool flag[4], any = false;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const A ab = r[k] < A(0) ? -r[k] : r[k];
+      flag[k] = !(aa[k] <= A(2) * ab) || !(ab <= A(3.0e38));
+      any |= flag[k];
+    }
+    if (__builtin_amdgcn_ballot_w64(any && lane < nq) != 0) {  // (wave-uniform)
+      AV seq[1];
+      rows_sweep<P, 1, 16, 1, NT>(StackRows{tile00, stride * 4}, bytes, n, w, seq);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) r[k] = flag[k] ? seq[0][k] : r[k];
+    }
+    const AV rr[1] = {r};
+    finish_piece<T, OP, A, 1, 64, 1>(e, qb, tcols, rr);
   }
 }
 
@@ -1290,57 +1325,6 @@ __global__ __launch_bounds__(64 * W) void reduce_kernel_rowmajor(const float* __
   int gi = 0;
   for (int64_t g0 = 0; g0 < k; g0 += KG) FA_RM_GROUP(KG, g0, gi++);
 #undef FA_RM_GROUP
-}
-
-// Row-major groups with a dynamically claimed tail.  The blocks of reduce_kernel_rowmajor end
-// their last group over a spread of ~60 us (C3: 4% of the launch; the per-block stream rate
-// differs with its XCD and HBM channels, DESIGN §4 finding 11), and a static split cannot know
-// which blocks will be late.  Here the window's first `ncols_static` columns are the static
-// row-major groups, and the rest is cut into STRIPS of W KiB of every row (one quad per lane),
-// claimed one at a time from a device counter by whichever block is free: a strip sweeps all N
-// rows TD deep (TD*W KiB in flight, like a group step) and applies the epilogue to its columns.
-// A strip is short (100 rows x 8 KiB ~ 20 us), so the blocks finish within about one strip of
-// each other.  Per element the sum is still rows 0..N-1 in list order (bit-exact): a column is
-// summed by exactly one block, static or strip.  *work must be 0 at launch.
-template <class P, typename T, int OP, int V, int D, int W, int KG, bool NT, int TD, int EPIB = (V >= 2 ? 2 : V)>
-__global__ __launch_bounds__(64 * W) void reduce_kernel_rowmajor_tail(const float* __restrict__ stack,
-                                                                      int64_t stride, int n,
-                                                                      const typename P::w_t* __restrict__ w,
-                                                                      int64_t col0, int64_t ncols_static,
-                                                                      int64_t ncols, Epi<T> e,
-                                                                      int* __restrict__ work) {
-  static_assert(sizeof(typename P::x_t) == 4, "row pipeline is for 4-byte elements");
-  const int64_t g = gridDim.x;
-  const int64_t row_bytes = stride * 4;
-  const char* base = reinterpret_cast<const char*>(stack + col0);
-  if (ncols_static > 0) {
-    const int64_t nquads_s = (ncols_static + 3) / 4;
-    const int64_t chunks_s = (nquads_s + 63) / 64;
-    const int64_t k = (chunks_s + g * W * V - 1) / (g * W * V);
-    const int64_t pc = (chunks_s + g * k - 1) / (g * k);
-    const int64_t pieces = (chunks_s + pc - 1) / pc;
-    int gi = 0;
-    for (int64_t g0 = 0; g0 < k; g0 += KG)
-      rowmajor_group<P, T, OP, V, D, W, KG, NT, EPIB, false>(base, row_bytes, n, w, g0, k, pc, pieces, nquads_s,
-                                                            ncols_static, gi++, e);
-  }
-  // the tail: strips of 64*W quads from quad ncols_static/4 (ncols_static is a multiple of 4)
-  const int64_t nquads = (ncols + 3) / 4;
-  const int64_t qt0 = ncols_static / 4;
-  const int64_t strips = (nquads - qt0 + 64 * W - 1) / (64 * W);
-  __shared__ int s_claim;
-  if (threadIdx.x == 0) s_claim = atomicAdd(work, 1);
-  __syncthreads();
-  int s = s_claim;
-  while (s < strips) {
-    const int64_t qs = qt0 + (int64_t)s * 64 * W;
-    const int64_t qe = qs + 64 * W < nquads ? qs + 64 * W : nquads;
-    rows_piece<P, T, OP, 1, TD, W, NT>(stack, stride, n, w, col0, ncols, e, qs, qe);
-    __syncthreads();  // every wave is done with s_claim and its strip
-    if (threadIdx.x == 0) s_claim = atomicAdd(work, 1);
-    __syncthreads();
-    s = s_claim;
-  }
 }
 
 // Column-blocked client stack: element (n, c) lives at ((c / B) * N + n) * B + c % B with

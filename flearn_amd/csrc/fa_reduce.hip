@@ -268,9 +268,12 @@ int dispatch_segrows(int op, const float* const* rows, int n, const void* w, con
 // 1000 x 1 M (3907 chunks): 738 vs 572 us — so the split form is used only for windows of fewer
 // 1-KiB chunks than CUs, and with at least 2 * kSplitW clients.  And at most kSplitMaxN clients:
 // a reordered fp32 sum differs from the sequential one by about the sequential sum's own rounding
-// error, which grows like sqrt(N) — U(-1,1) uploads: 5.9e-7 normwise at N = 1000, 1.18e-6 at
-// N = 4000 (tune_splitn) — and the contract is <= 1e-6.
-constexpr int kSplitW = 4, kSplitD = 8, kSplitMaxN = 2048;
+// error, which grows like sqrt(N), and the contract is <= 1e-6 per tensor.  The exact CPU
+// restatement of both orders (tests/splitn_error.py, profiles/r03/splitn_error.json; LeNet5
+// tensors, 3 seeds x 3 weight kinds x 2 data kinds) puts the worst tensor at 6.2e-7 for N = 256,
+// 7.4e-7 at 512, 2.5e-6 at 1024 (a 6-element bias, MOON weights), 1.3e-6 at 2048 — so 256.
+// Columns whose terms nearly cancel are re-summed in order by the kernel's guard.
+constexpr int kSplitW = 4, kSplitD = 8, kSplitMaxN = 256;
 constexpr int kSplitS = kSplitW;
 
 template <class P, typename T, int OP>

@@ -105,10 +105,12 @@ int fa_reduce_f32(const float* stack, int64_t row_stride, int32_t n_clients, int
  * column's clients are cut into 4 contiguous splits summed in list order, and the partial sums
  * are combined by a fixed binary tree in split order (staged in LDS).  Deterministic, but NOT
  * the reference's sequential order: results agree with strategy.py:123-129 to rounding
- * (normwise relative error <= 1e-6 per tensor), not bit for bit; the caller opts in.  Used only
- * where it is faster and within the tolerance — a window of fewer 1-KiB row chunks than the GPU
- * has CUs and 8..2048 clients; otherwise this runs fa_reduce_f32's bit-exact sequential kernel.  Same arguments,
- * modes and epilogues as fa_reduce_f32.                                                       */
+ * (normwise relative error <= 1e-6 per tensor), not bit for bit; the caller opts in.  A column
+ * whose terms nearly cancel (sum of |w*x| > 2 |sum of w*x|, or a non-finite sum) is re-summed in
+ * list order, bit-exact.  Used only where it is faster and within the tolerance — a window of
+ * fewer 1-KiB row chunks than the GPU has CUs and 8..256 clients; otherwise this runs
+ * fa_reduce_f32's bit-exact sequential kernel.  Same arguments, modes and epilogues as
+ * fa_reduce_f32.                                                                               */
 int fa_reduce_f32_splitn(const float* stack, int64_t row_stride, int32_t n_clients, int32_t mode,
                          const void* weights, double denom, int64_t col_begin, int64_t n_cols,
                          const fa_epilogue* epi, float* out32, double* out64, void* stream);

@@ -155,7 +155,7 @@ def lib():
             "ora_reduce_w32_div64": [P, I64, I32, P, D, I64, P],
             "ora_reduce_w32_div32": [P, I64, I32, P, ctypes.c_float, I64, P],
             "ora_reduce_w64": [P, I64, I32, P, D, I64, P],
-            "ora_sum_w32_splitn": [P, I64, I32, P, I32, I64, P],
+            "ora_sum_w32_splitn": [P, I64, I32, P, I32, I64, P, I32],
             "ora_reduce_f64": [P, I64, I32, P, D, I64, P],
             "ora_reduce_i64": [P, I64, I32, P, D, I64, P],
             "ora_update_f64": [I32, P, P, P, D, D, D, D, I64, P],
@@ -210,15 +210,16 @@ def c_reduce(mode, stack, weights, denom):
     return out
 
 
-def c_reduce_splitn(mode, stack, weights, denom, splits=4):
-    """The split-N kernel's order (ora_sum_w32_splitn) for the fp32-weight modes, then the mode's
-    divide: f64 [P] for MODE_W32_DIV64, fp32 for MODE_W32_DIV32 — as c_reduce returns them."""
+def c_reduce_splitn(mode, stack, weights, denom, splits=4, guard=True):
+    """The split-N kernel's order and cancellation guard (ora_sum_w32_splitn) for the fp32-weight
+    modes, then the mode's divide: f64 [P] for MODE_W32_DIV64, fp32 for MODE_W32_DIV32 — as
+    c_reduce returns them.  guard=False: the bare reordered sum (to measure the reordering)."""
     L = lib()
     n, p = stack.shape
     stack = np.ascontiguousarray(stack, np.float32)
     w = np.ascontiguousarray(weights, np.float32)
     acc = np.empty(p, np.float32)
-    L.ora_sum_w32_splitn(_ptr(stack), p, n, _ptr(w), int(splits), p, _ptr(acc))
+    L.ora_sum_w32_splitn(_ptr(stack), p, n, _ptr(w), int(splits), p, _ptr(acc), int(bool(guard)))
     if mode == MODE_W32_DIV64:
         return acc.astype(np.float64) / float(denom)
     if mode == MODE_W32_DIV32:

@@ -61,29 +61,56 @@ void ora_reduce_w32_div32(const float* stack, int64_t stride, int32_t n, const f
 /* The ORDER of the opt-in split-N kernel (flearn_amd/csrc/fa_device.hpp reduce_kernel_splitn),
  * not the reference's: clients cut into `nsplit` contiguous splits [v*n/nsplit, (v+1)*n/nsplit),
  * each summed in list order from its first product (fl32(w*x) products, fp32 sums), combined by
- * the fixed tree ((p0+p1)+(p2+p3))+...  Returns the fp32 sums (the caller divides as the mode
- * does).  Used by the tests to pin that kernel bit for bit and to measure how far its order
- * lies from the reference's sequential sum. */
+ * the fixed tree ((p0+p1)+(p2+p3))+...  With `guard`, the kernel's cancellation guard: the sums
+ * of |product| are formed the same way, and a column with !(A <= 2|S|) or !(|S| <= 3e38) takes
+ * the sequential (reference-order) sum instead.  Returns the fp32 sums (the caller divides as
+ * the mode does).  Used by the tests to pin that kernel bit for bit and to measure how far its
+ * order lies from the reference's sequential sum. */
 void ora_sum_w32_splitn(const float* stack, int64_t stride, int32_t n, const float* w, int32_t nsplit,
-                        int64_t ncols, float* out) {
-  float* part = (float*)malloc((size_t)(ncols > 0 ? ncols : 1) * (size_t)nsplit * sizeof(float));
+                        int64_t ncols, float* out, int32_t guard) {
+  const size_t cells = (size_t)(ncols > 0 ? ncols : 1) * (size_t)nsplit;
+  float* part = (float*)malloc(cells * sizeof(float));
+  float* apart = (float*)malloc(cells * sizeof(float));
   for (int32_t v = 0; v < nsplit; ++v) {
     const int32_t r0 = (int32_t)((int64_t)v * n / nsplit), r1 = (int32_t)((int64_t)(v + 1) * n / nsplit);
     float* acc = part + (int64_t)v * ncols;
-    for (int64_t p = 0; p < ncols; ++p) acc[p] = r0 < r1 ? w[r0] * stack[(int64_t)r0 * stride + p] : 0.0f;
+    float* aacc = apart + (int64_t)v * ncols;
+    for (int64_t p = 0; p < ncols; ++p) {
+      const float prod = r0 < r1 ? w[r0] * stack[(int64_t)r0 * stride + p] : 0.0f;
+      acc[p] = prod;
+      aacc[p] = fabsf(prod);
+    }
     for (int32_t i = r0 + 1; i < r1; ++i) {
       const float* row = stack + (int64_t)i * stride;
       for (int64_t p = 0; p < ncols; ++p) {
         const float prod = w[i] * row[p];
         acc[p] = acc[p] + prod;
+        aacc[p] = aacc[p] + fabsf(prod);
       }
     }
   }
   for (int32_t h = 1; h < nsplit; h *= 2)
     for (int32_t v = 0; v + h < nsplit; v += 2 * h)
-      for (int64_t p = 0; p < ncols; ++p) part[(int64_t)v * ncols + p] = part[(int64_t)v * ncols + p] + part[(int64_t)(v + h) * ncols + p];
-  memcpy(out, part, (size_t)ncols * sizeof(float));
+      for (int64_t p = 0; p < ncols; ++p) {
+        part[(int64_t)v * ncols + p] = part[(int64_t)v * ncols + p] + part[(int64_t)(v + h) * ncols + p];
+        apart[(int64_t)v * ncols + p] = apart[(int64_t)v * ncols + p] + apart[(int64_t)(v + h) * ncols + p];
+      }
+  for (int64_t p = 0; p < ncols; ++p) {
+    const float sum = part[p], ab = fabsf(sum), two_ab = 2.0f * ab;
+    const int flag = guard && (!(apart[p] <= two_ab) || !(ab <= 3.0e38f));
+    if (flag) {  /* the reference's sequential sum */
+      float acc = w[0] * stack[p];
+      for (int32_t i = 1; i < n; ++i) {
+        const float prod = w[i] * stack[(int64_t)i * stride + p];
+        acc = acc + prod;
+      }
+      out[p] = acc;
+    } else {
+      out[p] = sum;
+    }
+  }
   free(part);
+  free(apart);
 }
 
 /* np.float64 / np.int64 weights on fp32 tensors: promoted to f64 for product and sum. */

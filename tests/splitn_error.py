@@ -1,7 +1,8 @@
 """How far the opt-in split-N order (reduce_kernel_splitn) lies from the reference's sequential
 sum, per fp32 tensor, as a function of the client count — computed exactly on the CPU with the
 oracle's restatement of both orders (oracle.c_reduce vs oracle.c_reduce_splitn, which the GPU
-tests pin bit for bit to the kernels).  Drives the split-N selection limit (kSplitMaxN in
+tests pin bit for bit to the kernels); --guard applies the kernel's cancellation guard (columns
+whose terms nearly cancel take the sequential sum).  Drives the split-N selection limit (kSplitMaxN in
 flearn_amd/csrc/fa_reduce.hip).  Test infrastructure / measurement only.
 
     python tests/splitn_error.py [--out profiles/r03/splitn_error.json]
@@ -34,6 +35,12 @@ def data(kind, n, p, seed):
     if kind == "near_common":  # clients trained from one global model: a shared value + 1% noise
         m = oracle.fill_uniform(1, p, seed + 1)
         x = (m + np.float32(0.01) * x).astype(np.float32)
+    if kind == "cancelling":  # client pairs that nearly cancel: the mean is ~1e-4 of the values
+        half = x[: (n + 1) // 2]
+        y = np.empty_like(x)
+        y[0::2] = half[: y[0::2].shape[0]]
+        y[1::2] = -half[: y[1::2].shape[0]] + np.float32(1e-4) * oracle.fill_uniform(n // 2, p, seed + 7)
+        x = y
     return x
 
 
@@ -49,12 +56,14 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=None)
     ap.add_argument("--ns", default="128,256,512,768,1024,1536,2048,3072,4096")
+    ap.add_argument("--guard", action="store_true", help="with the kernel's cancellation guard")
+    ap.add_argument("--data", default="zero_mean,near_common,cancelling")
     args = ap.parse_args()
     lay, p = tensors(layouts.get("lenet5"))
     rng = np.random.default_rng(0)
     rows = []
     for n in [int(v) for v in args.ns.split(",")]:
-        for dk in ("zero_mean", "near_common"):
+        for dk in args.data.split(","):
             for wk in ("ones", "moon_int", "float"):
                 errs = []
                 for seed in (1, 2, 3):
@@ -63,12 +72,13 @@ def main():
                     w32 = np.asarray(w, np.float64).astype(np.float32)
                     denom = float(np.sum(w))
                     a = oracle.c_reduce(oracle.MODE_W32_DIV64, x, w32, denom)
-                    b = oracle.c_reduce_splitn(oracle.MODE_W32_DIV64, x, w32, denom)
+                    b = oracle.c_reduce_splitn(oracle.MODE_W32_DIV64, x, w32, denom, guard=args.guard)
                     for k, off, m in lay:
                         ra, rb = a[off : off + m], b[off : off + m]
                         nrm = np.linalg.norm(ra)
                         errs.append(float(np.linalg.norm(ra - rb) / nrm) if nrm else 0.0)
-                row = dict(n=n, data=dk, weights=wk, max_rel=max(errs), median_rel=float(np.median(errs)))
+                row = dict(n=n, data=dk, weights=wk, guard=args.guard, max_rel=max(errs),
+                           median_rel=float(np.median(errs)))
                 rows.append(row)
                 print(json.dumps(row), flush=True)
     if args.out:

@@ -280,6 +280,173 @@ __global__ __launch_bounds__(64 * W) void reduce_kernel_rowmajor_dfr(const float
   }
 }
 
+// ---- tuning-only kernels measured in round 3 and NOT adopted (DESIGN.md §4 findings 17, 18) ----
+
+// [tuning only, not adopted: slower than reduce_kernel_narrow on every shape] LDS-staged narrow reduce (deep, narrow windows: LeNet-sized models of many clients), bit-exact.
+// reduce_kernel_narrow gives each 1-KiB chunk of the window ONE wave, and a wave's vmcnt caps its
+// loads in flight at 63 — so 1000 LeNet5 uploads (174 chunks) keep only ~7 MB in flight on the
+// whole chip and stream at ~74% of spec.  Splitting the CLIENTS over waves (split-N) gets more
+// loads in flight but changes the summation order.  Here the LOADING is split and the SUMMING
+// is not:
+//   * a block owns one chunk (256 columns) and W waves; rows go in STAGES of R = W*DW rows, wave
+//     v loading rows [s*R + v*DW, +DW) of stage s (whole 1-KiB rows, one buffer descriptor each)
+//     L stages ahead, so W*L*DW KiB stay in flight per block (e.g. 4 x 3 x 8 = 96 KiB);
+//   * at stage s every wave writes its landed rows into an LDS row buffer (double-buffered,
+//     2 x R KiB), one barrier, and then EVERY wave sums its own 64 columns over all R rows of the
+//     stage in row order — lane l of wave v owns column 64v + l, reads it from LDS (a 256-B
+//     conflict-free ds_read_b32 row slice) and runs the reference's sequential chain:
+//     acc = fl(w0*x0), acc = fl(acc + fl(w_i*x_i)) for i = 1..N-1 in list order;
+//   * the stage's weights are loaded with its rows (one VGPR of wave 0, lane j: w[s*R + j]) and
+//     ride through LDS with them (a broadcast read; no scalar-cache round trip in the chain);
+//   * the per-column sums meet in LDS and wave 0 applies the usual piece epilogue.
+// The double buffer needs one barrier per stage: buffer s&1 is rewritten at stage s+2, after the
+// barrier of stage s+1, which no wave passes before it has finished consuming stage s.
+template <class P, typename T, int OP, int W, int DW, int L, bool NT>
+__global__ __launch_bounds__(64 * W) void reduce_kernel_lds(const float* __restrict__ stack, int64_t stride, int n,
+                                                            const typename P::w_t* __restrict__ w, int64_t col0,
+                                                            int64_t ncols, Epi<T> e) {
+  typedef typename P::acc_t A;
+  typedef typename P::w_t WT;
+  typedef typename vec4<float>::type XV;
+  typedef typename vec4<A>::type AV;
+  constexpr int R = W * DW;  // rows per stage
+  static_assert(sizeof(typename P::x_t) == 4 && R <= 64 && L * (DW + 1) <= 63, "stage geometry");
+  static_assert(W == 4, "4 waves x 64 lanes = the chunk's 256 columns, one per lane");
+  __shared__ XV rowbuf[2][R][64];
+  __shared__ WT wbuf[2][R];
+  __shared__ A accbuf[256];
+  const int lane = (int)threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+  const int64_t qb = (int64_t)blockIdx.x * 64;  // the chunk's first quad
+  const int64_t cleft = ncols - qb * 4;
+  if (cleft <= 0) return;  // (uniform over the block)
+  const int tcols = cleft < 256 ? (int)cleft : 256;
+  const uint32_t bytes = (uint32_t)tcols * 4u;
+  const char* base = reinterpret_cast<const char*>(stack + col0 + qb * 4);
+  const int64_t rb = stride * 4;
+  const int stages = (n + R - 1) / R;
+  const int voff = lane * 16;
+  const __amdgpu_buffer_rsrc_t wrs = row_rsrc(w, (uint32_t)n * (uint32_t)sizeof(WT));
+  auto wload = [&](int first) {  // lane j: w[first + j] (0 past the end)
+    if constexpr (sizeof(WT) == 4)
+      return __builtin_bit_cast(WT, __builtin_amdgcn_raw_buffer_load_b32(wrs, (lane + first) * 4, 0, 0));
+    else
+      return __builtin_bit_cast(WT, __builtin_amdgcn_raw_buffer_load_b64(wrs, (lane + first) * 8, 0, 0));
+  };
+
+  XV x[L][DW];
+  WT ws[L];
+  // stage s into slot t: this wave's DW rows (clamped to the last row: the refills of the at most
+  // L-1 padding stages past the end re-read row n-1, an L2 hit) and the stage's weights.  No
+  // branch around any load: the compiler's vmcnt bookkeeping then sees the same L*(DW+1) loads
+  // in flight at every stage and waits only for the oldest stage's
+#define FA_LDS_ISSUE(t, s)                                                                           \
+  {                                                                                                  \
+    const int r0_ = (s) * R + wv * DW;                                                               \
+    _Pragma("unroll") for (int i = 0; i < DW; ++i) {                                                 \
+      const int r_ = r0_ + i < n ? r0_ + i : n - 1;                                                  \
+      x[t][i] = buf_load_quad<NT>(row_rsrc(base + (int64_t)r_ * rb, bytes), voff, 0);                \
+    }                                                                                                \
+    ws[t] = wload((s) * R);                                                                          \
+  }
+#pragma unroll
+  for (int t = 0; t < L; ++t) FA_LDS_ISSUE(t, t);
+  const float* lrow = reinterpret_cast<const float*>(&rowbuf[0][0][0]);
+  const int c = wv * 64 + lane;  // this lane's column of the chunk
+  A acc = A(0);
+  for (int s0 = 0; s0 < stages; s0 += L) {
+#pragma unroll
+    for (int t = 0; t < L; ++t) {
+      const int s = s0 + t;  // may be a padding stage past the end (its rows are not summed)
+      const int buf = s & 1;
+#pragma unroll
+      for (int i = 0; i < DW; ++i) rowbuf[buf][wv * DW + i][lane] = x[t][i];
+      if (wv == 0 && lane < R) wbuf[buf][lane] = ws[t];  // the stage's weights ride along
+      // LDS-only barrier: this wave's row writes are done (lgkmcnt(0)); the global loads in
+      // flight are NOT waited for (__syncthreads() would drain vmcnt and serialise the stages)
+      __builtin_amdgcn_s_waitcnt(0xC07F);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      FA_LDS_ISSUE(t, s + L);
+      __builtin_amdgcn_sched_barrier(0);
+      const float* lb = lrow + buf * R * 256 + c;
+      const int rows = n - s * R;  // rows of this stage to sum (<= 0: padding)
+      // all R row values first (one LDS round trip per stage, not one per row pair), then the chain
+      float xs[R];
+      WT wj[R];
+#pragma unroll
+      for (int j = 0; j < R; ++j) xs[j] = lb[j * 256];
+#pragma unroll
+      for (int j = 0; j < R; ++j) wj[j] = wbuf[buf][j];  // (a broadcast read)
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int j = 0; j < R; ++j) {
+        const A p = P::mul(wj[j], xs[j]);
+        const A a2 = (s == 0 && j == 0) ? p : add<A>(acc, p);
+        acc = j < rows ? a2 : acc;
+      }
+    }
+  }
+#undef FA_LDS_ISSUE
+  accbuf[c] = acc;
+  __syncthreads();  // (after the last stage: draining the padding refills costs nothing here)
+  if (wv == 0) {
+    const AV r[1] = {AV{accbuf[lane * 4], accbuf[lane * 4 + 1], accbuf[lane * 4 + 2], accbuf[lane * 4 + 3]}};
+    finish_piece<T, OP, A, 1, 64, 1>(e, qb, tcols, r);
+  }
+}
+
+// [tuning only, not adopted: slower than reduce_kernel_rowmajor on NS / C3 / C5] Row-major groups with a dynamically claimed tail.  The blocks of reduce_kernel_rowmajor end
+// their last group over a spread of ~60 us (C3: 4% of the launch; the per-block stream rate
+// differs with its XCD and HBM channels, DESIGN §4 finding 11), and a static split cannot know
+// which blocks will be late.  Here the window's first `ncols_static` columns are the static
+// row-major groups, and the rest is cut into STRIPS of W KiB of every row (one quad per lane),
+// claimed one at a time from a device counter by whichever block is free: a strip sweeps all N
+// rows TD deep (TD*W KiB in flight, like a group step) and applies the epilogue to its columns.
+// A strip is short (100 rows x 8 KiB ~ 20 us), so the blocks finish within about one strip of
+// each other.  Per element the sum is still rows 0..N-1 in list order (bit-exact): a column is
+// summed by exactly one block, static or strip.  *work must be 0 at launch.
+template <class P, typename T, int OP, int V, int D, int W, int KG, bool NT, int TD, int EPIB = (V >= 2 ? 2 : V)>
+__global__ __launch_bounds__(64 * W) void reduce_kernel_rowmajor_tail(const float* __restrict__ stack,
+                                                                      int64_t stride, int n,
+                                                                      const typename P::w_t* __restrict__ w,
+                                                                      int64_t col0, int64_t ncols_static,
+                                                                      int64_t ncols, Epi<T> e,
+                                                                      int* __restrict__ work) {
+  static_assert(sizeof(typename P::x_t) == 4, "row pipeline is for 4-byte elements");
+  const int64_t g = gridDim.x;
+  const int64_t row_bytes = stride * 4;
+  const char* base = reinterpret_cast<const char*>(stack + col0);
+  if (ncols_static > 0) {
+    const int64_t nquads_s = (ncols_static + 3) / 4;
+    const int64_t chunks_s = (nquads_s + 63) / 64;
+    const int64_t k = (chunks_s + g * W * V - 1) / (g * W * V);
+    const int64_t pc = (chunks_s + g * k - 1) / (g * k);
+    const int64_t pieces = (chunks_s + pc - 1) / pc;
+    int gi = 0;
+    for (int64_t g0 = 0; g0 < k; g0 += KG)
+      rowmajor_group<P, T, OP, V, D, W, KG, NT, EPIB, false>(base, row_bytes, n, w, g0, k, pc, pieces, nquads_s,
+                                                            ncols_static, gi++, e);
+  }
+  // the tail: strips of 64*W quads from quad ncols_static/4 (ncols_static is a multiple of 4)
+  const int64_t nquads = (ncols + 3) / 4;
+  const int64_t qt0 = ncols_static / 4;
+  const int64_t strips = (nquads - qt0 + 64 * W - 1) / (64 * W);
+  __shared__ int s_claim;
+  if (threadIdx.x == 0) s_claim = atomicAdd(work, 1);
+  __syncthreads();
+  int s = s_claim;
+  while (s < strips) {
+    const int64_t qs = qt0 + (int64_t)s * 64 * W;
+    const int64_t qe = qs + 64 * W < nquads ? qs + 64 * W : nquads;
+    rows_piece<P, T, OP, 1, TD, W, NT>(stack, stride, n, w, col0, ncols, e, qs, qe);
+    __syncthreads();  // every wave is done with s_claim and its strip
+    if (threadIdx.x == 0) s_claim = atomicAdd(work, 1);
+    __syncthreads();
+    s = s_claim;
+  }
+}
+
 }  // namespace fa
 
 struct Variant {
@@ -391,6 +558,31 @@ Variant make_rmtail(const float* stack, int64_t stride, int n, const float* w, i
                                dim3(64 * W), 0, 0, stack, stride, n, w, (int64_t)0, ns, ncols, e, work);
           },
           true, {}};
+}
+
+template <int W, int DW, int L, int OP, typename T>
+Variant make_lds(const float* stack, int64_t stride, int n, const float* w, int64_t ncols, Epi<T> e, double bytes) {
+  const int64_t chunks = ((ncols + 3) / 4 + 63) / 64;
+  char name[96];
+  snprintf(name, sizeof name, "lds W%d DW%d L%d g%lld", W, DW, L, (long long)chunks);
+  return {name, bytes,
+          [=] {
+            hipLaunchKernelGGL((reduce_kernel_lds<AccF32, T, OP, W, DW, L, true>), dim3((unsigned)chunks), dim3(64 * W), 0,
+                               0, stack, stride, n, w, (int64_t)0, ncols, e);
+          },
+          true, {}};
+}
+
+// the opt-in split-N kernel (reordered sum: not bit-checked here)
+template <int OP, typename T>
+Variant make_splitn(const float* stack, int64_t stride, int n, const float* w, int64_t ncols, Epi<T> e, double bytes) {
+  const int64_t chunks = ((ncols + 3) / 4 + 63) / 64;
+  return {"splitn W4 D8 (reordered)", bytes,
+          [=] {
+            hipLaunchKernelGGL((reduce_kernel_splitn<AccF32, T, OP, 4, 8, true>), dim3((unsigned)chunks), dim3(256), 0, 0,
+                               stack, stride, n, w, (int64_t)0, ncols, e);
+          },
+          false, {}};
 }
 
 template <int V, int W, int KG, int OP, typename T, int TM>
@@ -707,6 +899,25 @@ int main(int argc, char** argv) {
     RMT(16, 1, 4, 2, 16, 192, 0.11);
     RMT(16, 1, 4, 4, 16, 208, 0.11);
     RMT(16, 1, 4, 4, 8, 192, 0.11);
+  }
+#define LDSK(W, DW, L)                                                                                      \
+  vs.push_back(op == FA_OP_AVGM      ? make_lds<W, DW, L, FA_OP_AVGM, double>(stack, stride, n, w, ncols, e, bytes)   \
+               : op == FA_OP_ADAGRAD ? make_lds<W, DW, L, FA_OP_ADAGRAD, double>(stack, stride, n, w, ncols, e, bytes) \
+                                     : make_lds<W, DW, L, FA_OP_MEAN, double>(stack, stride, n, w, ncols, e, bytes))
+  if (!strcmp(set, "lds")) {  // LDS-staged bit-exact narrow kernel vs the one-wave narrow kernel and split-N
+    NARROW(40, 1);
+    NARROW(32, 1);
+    LDSK(4, 8, 3);
+    LDSK(4, 8, 4);
+    LDSK(4, 8, 5);
+    LDSK(4, 4, 6);
+    LDSK(4, 4, 10);
+    LDSK(4, 16, 2);
+    LDSK(4, 16, 3);
+    LDSK(4, 12, 4);
+    vs.push_back(op == FA_OP_AVGM      ? make_splitn<FA_OP_AVGM, double>(stack, stride, n, w, ncols, e, bytes)
+                 : op == FA_OP_ADAGRAD ? make_splitn<FA_OP_ADAGRAD, double>(stack, stride, n, w, ncols, e, bytes)
+                                       : make_splitn<FA_OP_MEAN, double>(stack, stride, n, w, ncols, e, bytes));
   }
   if (!strcmp(set, "nsgrid")) {  // north-star shape: group size / grid / piece width
     RM(8, 1, 8, 3, 192);
