@@ -26,9 +26,11 @@ def hipcc() -> str:
 
 
 def build_pyhost(force: bool = False, verbose: bool = False) -> Path:
-    """libfa_pyhost.so: gcc against this interpreter's headers; Python symbols stay undefined and
-    resolve against the interpreter that loads it."""
+    """libfa_pyhost.so: gcc against this interpreter's and numpy's headers; Python and numpy
+    symbols stay undefined / are imported at first use from the interpreter that loads it."""
     import sysconfig
+
+    import numpy
 
     newest = max(PYHOST_SOURCE.stat().st_mtime, Path(__file__).stat().st_mtime)
     if PYHOST_OUT.exists() and not force and PYHOST_OUT.stat().st_mtime >= newest:
@@ -36,7 +38,7 @@ def build_pyhost(force: bool = False, verbose: bool = False) -> Path:
     PYHOST_OUT.parent.mkdir(parents=True, exist_ok=True)
     tmp = PYHOST_OUT.with_suffix(".so.tmp")
     cmd = [os.environ.get("CC", "gcc"), "-O2", "-fPIC", "-shared", "-Wall", "-Werror",
-           f"-I{sysconfig.get_paths()['include']}", str(PYHOST_SOURCE), "-o", str(tmp)]
+           f"-I{sysconfig.get_paths()['include']}", f"-I{numpy.get_include()}", str(PYHOST_SOURCE), "-o", str(tmp)]
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)

@@ -107,6 +107,8 @@ def load_pyhost():
             P, I64, O = ctypes.c_void_p, ctypes.c_int64, ctypes.py_object
             L.fa_py_pack_rows.argtypes = [O, O, I64, P, I64, I64]
             L.fa_py_pack_rows.restype = ctypes.c_int
+            L.fa_py_same_signature.argtypes = [O, O]
+            L.fa_py_same_signature.restype = ctypes.c_int
             _pyhost = L
     return _pyhost
 

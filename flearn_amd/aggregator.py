@@ -584,6 +584,10 @@ class Aggregator:
     def ensemble(self, agg_weight_lst, w_local_lst, key_lst=None, server_opt: ServerOptimizer | None = None):
         plan = make_plan(agg_weight_lst, w_local_lst, key_lst)
         self.last_plan = plan
+        if server_opt is None and not self._dist and len(self.devices) == 1 and self.output != "device":
+            glob = self._small_round(plan, w_local_lst)
+            if glob is not None:
+                return glob
         stacks = self.packer.pack(plan, w_local_lst)
         fused = False
         self._post_denom = None
@@ -612,6 +616,90 @@ class Aggregator:
         if self._dist and KIND_F32 in results:
             results[KIND_F32] = self._gather_columns(plan, results[KIND_F32])
         return self._finish(plan, results)
+
+    # -- small host rounds ---------------------------------------------------------------------
+    def _small_record(self, plan: BucketPlan, w_local_lst):
+        """The prebuilt round of a small host-upload plan (every bucket together < SMALL_BYTES:
+        LeNet-sized models, flearn's config 1), cached on the plan: per bucket kind its own
+        pinned staging, device stack, device weights and result buffers, the native pack table
+        and the ctypes arguments of its reduce launch, and the (key, offset, size, shape) list
+        of the result.  None (cached as False) when the plan does not qualify."""
+        key = ("small_round", id(self.packer), str(self.device), self.output)
+        rec = plan.memo.get(key)
+        if rec is not None:
+            return rec or None
+        from .bucket import SMALL_BYTES, Packer, Shard, _NativeRows, _STORE, _TORCH
+
+        n = plan.n_clients
+        total = sum(n * g.stride * np.dtype(_STORE[k]).itemsize for k, g in plan.groups.items())
+        if plan.input_kind != "numpy" or total >= SMALL_BYTES or not plan.groups:
+            plan.memo[key] = False
+            return None
+        L, dev = na.lib(), self.device
+        kinds = []
+        for kind, g in plan.groups.items():
+            tdt = _TORCH[_STORE[kind]]
+            pieces = Packer._pieces(g, [Shard(0, dev, 0, g.stride)])
+            host = torch.zeros((n, g.stride), dtype=tdt, pin_memory=True)
+            if not _NativeRows.usable(pieces, [host]):
+                plan.memo[key] = False
+                return None
+            nat = _NativeRows(pieces, [host], w_local_lst, [None] * n)
+            stack = torch.empty((n, g.stride), dtype=tdt, device=dev)
+            nm = g.numerics
+            w = self._weights(nm, dev)
+            f64 = kind != KIND_F32 or (self.output == "reference" and nm.out_dtype == _F64)
+            dout = torch.empty(g.stride, dtype=torch.float64 if f64 else torch.float32, device=dev)
+            hout = torch.empty(g.stride, dtype=dout.dtype, pin_memory=True)
+            if kind == KIND_F32:
+                fn = L.fa_reduce_f32
+                args = (stack.data_ptr(), g.stride, n, nm.mode, w.data_ptr(), float(nm.denom), 0, g.stride, None,
+                        None if f64 else dout.data_ptr(), dout.data_ptr() if f64 else None)
+            else:
+                fn = L.fa_reduce_f64 if kind == KIND_F64 else L.fa_reduce_i64
+                args = (stack.data_ptr(), g.stride, n, w.data_ptr(), float(nm.denom), 0, g.stride, dout.data_ptr())
+            out = [(s.key, s.offset, s.numel, s.shape) for s in g.segments]
+            kinds.append((nat, host, stack, w, dout, hout, hout.numpy(), fn, args, out))
+        g32 = plan.groups.get(KIND_F32)
+        wsig = (tuple((s.key, s.shape, s.offset) for s in g32.segments) + (g32.stride,)) if g32 is not None else None
+        rec = plan.memo[key] = (tuple(kinds), na.load_pyhost().fa_py_pack_rows, wsig)
+        return rec
+
+    def _small_round(self, plan: BucketPlan, w_local_lst):
+        """One small host round with no per-key Python: the uploads are packed natively into the
+        record's pinned staging (every value checked against the plan: C-contiguous, dtype, byte
+        size), each bucket is one H2D, one reduce launch and one D2H on torch's current stream,
+        one synchronisation, and the result is handed out as views of one fresh array per bucket
+        (numpy scalars for 0-d keys) — what Packer.unpack returns.  Returns None (nothing queued)
+        when a value does not fit the record; the caller then takes the general path."""
+        rec = self._small_record(plan, w_local_lst)
+        if rec is None:
+            return None
+        kinds, pack, wsig = rec
+        lst = w_local_lst if type(w_local_lst) is list else list(w_local_lst)
+        if wsig is not None:
+            from .wire import wire_row
+
+            if wire_row(lst[0], wsig) is not None:  # decoded by the wire codec into pinned rows of
+                return None                          # this layout: the general path DMAs them as is
+        for nat, *_ in kinds:
+            if pack(lst, nat.keys, len(nat.keys), nat.ptr, 0, len(lst)) != 0:
+                return None
+        dev = self.device
+        stream = torch.cuda.current_stream(dev)
+        sh = stream.cuda_stream
+        for nat, host, stack, w, dout, hout, hnp, fn, args, out in kinds:
+            stack.copy_(host, non_blocking=True)
+            na.check(fn(*args, sh), fn.__name__)
+            hout.copy_(dout, non_blocking=True)
+        stream.synchronize()  # also: the staging may be rewritten by the next call
+        parts = {}
+        for nat, host, stack, w, dout, hout, hnp, fn, args, out in kinds:
+            fresh = hnp.copy()
+            for k, off, m, shape in out:
+                a = fresh[off : off + m].reshape(shape)
+                parts[k] = a.dtype.type(a[()]) if shape == () else a
+        return {k: parts[k] for k in plan.keys}
 
     def _gather_columns(self, plan: BucketPlan, parts):
         """Column-sharded group: every rank's reduced columns -> the whole f32 bucket on every

@@ -152,17 +152,21 @@ def _plain_dicts(w_local_lst) -> bool:
     return all(type(w) in (dict, collections.OrderedDict) for w in w_local_lst)
 
 
-def _same_signature_native(w_local_lst, keys) -> bool:
-    """True when every client's (type, dtype, shape, layout) per key equals client 0's, read from the
-    tensors' TensorImpl by csrc/fa_torchmeta.cpp (torch uploads; the same comparisons as
-    _raw_signature without torch's per-attribute dispatch); False when it differs or cannot tell
-    (numpy uploads, no library) — the caller then compares in Python."""
+def _same_signature_native(w_local_lst, keys, sig0=None) -> bool:
+    """True when every client's (type, dtype, shape, layout) per key equals client 0's, read
+    natively: numpy uploads through the buffer protocol (csrc/fa_pyhost.c fa_py_same_signature:
+    type, format, itemsize, shape — numpy arrays are always strided), torch uploads from the
+    tensors' TensorImpl (csrc/fa_torchmeta.cpp) — the same comparisons as _raw_signature without
+    the per-attribute interpreter work; False when it differs or cannot tell (the caller then
+    compares in Python)."""
     if len(w_local_lst) < 2 or not _plain_dicts(w_local_lst):
         return False
+    lst = w_local_lst if type(w_local_lst) is list else list(w_local_lst)
+    if sig0 is not None and sig0 and all(t[0] is np.ndarray for t in sig0):
+        return na.load_pyhost().fa_py_same_signature(lst, tuple(keys)) == 1
     L = na.load_torchmeta()
     if L is None:
         return False
-    lst = w_local_lst if type(w_local_lst) is list else list(w_local_lst)
     return L.fa_tm_same_signature(lst, tuple(keys)) == 1
 
 
@@ -200,7 +204,7 @@ def make_plan(agg_weight_lst, w_local_lst, key_lst=None) -> BucketPlan:
         raise ValueError("agg_weight_lst and w_local_lst differ in length")
     keys = select_keys(w_local_lst, key_lst)
     sig0 = _raw_signature(w_local_lst[0], keys)
-    if sig0 is not None and _same_signature_native(w_local_lst, keys):
+    if sig0 is not None and _same_signature_native(w_local_lst, keys, sig0):
         slow = []
     else:
         slow = [n for n in range(1, len(w_local_lst))

@@ -987,3 +987,25 @@ def test_float64_model_with_int64_counters(weights, cuda):
     want = oracle.server_ensemble(weights, [{k: v.copy() for k, v in c.items()} for c in clients])
     got = AVG().server(upload(clients, weights), 0)["w_glob"]
     assert_dict_bitwise(got, want, f"f64 model, weights {type(weights[0]).__name__}")
+
+
+def test_small_round_fast_path_reuses_its_record_safely(cuda):
+    """Small host rounds (every bucket < 4 MiB: flearn's config 1) take Aggregator._small_round:
+    natively packed pinned staging, one H2D / launch / D2H per bucket, one sync.  Round after round
+    with new values (the record's staging reused) and with a value the native pack refuses (a
+    non-contiguous view: the general path takes over) every result is bit-equal to the oracle."""
+    layout = layouts.get("lenet5")
+    p = layouts.fp32_elems(layout)
+    s = AVG()
+    for r in range(4):
+        flat = oracle.fill_uniform(10, p, seed=40 + r)
+        clients = [layouts.synthetic_state_dict(layout, flat[i]) for i in range(10)]
+        if r == 2:  # a Fortran-ordered copy: same shape and dtype, not C-contiguous
+            k = next(k for k, v in clients[3].items() if v.ndim == 2)
+            clients[3][k] = np.asfortranarray(clients[3][k])
+        weights = [1.0 + 0.5 * i for i in range(10)]
+        got = s.server(upload(clients, weights), r)["w_glob"]
+        want = oracle.server_ensemble(weights, [{k: v.copy() for k, v in c.items()} for c in clients])
+        assert_dict_bitwise(got, want, f"round {r}")
+        rec = s.engine.last_plan.memo.get(("small_round", id(s.engine.packer), str(s.engine.device), "reference"))
+        assert rec, "the small-round record was not built"

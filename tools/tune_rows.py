@@ -1,6 +1,6 @@
 """Work-plan sweep for fa_reduce_f32_rows (device uploads read in place), one MI355X.
 
-    python tools/tune_rows.py [--config c2|ns] [--alloc views|clones] [--reps R]
+    python tools/tune_rows.py [--config c2|ns] [--alloc views|clones|stack] [--reps R]
 
 Times the product kernel (lib: fa_reduce_f32_rows with fa_rows_plan's table) against variants
 of its geometry (V quads per lane, D rows in flight, W waves; pieces of C KiB of a row, largest
@@ -104,6 +104,20 @@ def rr(pieces, g, kg=1):
     return block_major(per, kg)
 
 
+def by_alloc(arr, ptrs):
+    """arr (a fa_rows_plan table) with its wide pieces, then its narrow pieces, each sorted by the
+    address of client 0's bytes of the piece; pieces[0].aux = the wide count, as the kernel reads."""
+    nw = int(arr[0]["aux"]) if len(arr) else 0
+    addr = ptrs[arr["seg"], 0] + arr["seg_off"] * 4
+    out = arr.copy()
+    for lo, hi in ((0, nw), (nw, len(arr))):
+        out[lo:hi] = arr[lo + np.argsort(addr[lo:hi], kind="stable")]
+    out["aux"] = 0
+    if len(out):
+        out[0]["aux"] = nw
+    return out
+
+
 def lib_plan(segs, g):
     L = na.load()
     cols = np.array([c for c, _ in segs], np.int64)
@@ -177,6 +191,11 @@ def main():
                "v8d2w4_c16": (0, 16), "v16d1w4_c32": (1, 32)}
     T.tune_rows_rm_launch.argtypes = T.tune_rows_launch.argtypes
     variants = {"stack": None, "lib": (None,) + lib_plan(segs, 0)}
+    # the product plan with its pieces in ALLOCATION order (address of client
+    # 0's bytes of the piece; wide pieces stay first, so groups are claimed the same way) instead
+    # of largest first: do blocks streaming neighbouring addresses read the scattered uploads better?
+    base, gb = lib_plan(segs, 0)
+    variants["lib_alloc_order"] = (None, by_alloc(base, ptrs), gb)
     for spec in filter(None, a.plans.split(",")):
         pc, g = (int(x) for x in spec.split(":"))
         variants[f"plan_pc{pc}_g{g}"] = (None, product_plan(segs, pc), g)
