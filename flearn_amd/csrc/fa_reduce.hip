@@ -123,7 +123,12 @@ int launch_rowmajor(const float* stack, int64_t stride, int n, const typename P:
     const int64_t chunks = ((ncols + 3) / 4 + 63) / 64;
     const int64_t k = (chunks + grid * kPieceChunks - 1) / (grid * kPieceChunks);
     if (k >= 6) {
-      hipLaunchKernelGGL((reduce_kernel_rowmajor<P, T, OP, 16, 1, 4, KG, kNT>), dim3((unsigned)grid), dim3(256), 0,
+      // fused epilogues batch the state of 4 slots per lane (EPIB 4) instead of 2: one process,
+      // 9 interleaved rounds, each variant twice (tools/tune_reduce.hip set "epib4",
+      // profiles/r03/tune_epib4/): Adagrad 100 x 86.6 M 5315 -> 5272 us, AVGM 100 x 25.6 M
+      // 1599 -> 1595 us, AVGM 100 x 11.7 M 711 -> 707 us; the plain mean has no state (+-0.1%)
+      constexpr int EB = OP == FA_OP_MEAN ? 2 : 4;
+      hipLaunchKernelGGL((reduce_kernel_rowmajor<P, T, OP, 16, 1, 4, KG, kNT, EB>), dim3((unsigned)grid), dim3(256), 0,
                          s, stack, stride, n, w, col0, ncols, e);
       return launch_check();
     }

@@ -20,6 +20,8 @@ case $SET in
   deep3) SHAPES="1000:177704:mean 800:365632:mean 400:731200:mean 100:1462400:mean 200:5849600:mean 1000:177704:avgm" ;;
   deep2) SHAPES="1000:44426:mean 1000:44426:avgm 400:44426:mean 100:44426:mean 2000:44426:mean 300:70001:mean 1000:3:mean" ;;
   lds) SHAPES="1000:44426:mean 400:44426:mean 100:44426:mean 2000:44426:mean 1000:177704:mean 300:70001:mean 1000:44426:avgm" ;;
+  epib4) SHAPES="100:25610176:avgm 100:86567680:adagrad 100:25610176:mean 100:11699136:avgm 1000:11699136:mean" ;;
+  epib16) SHAPES="100:25610176:avgm 100:86567680:adagrad 100:25610176:mean" ;;
   tail) SHAPES="100:25610176:avgm 100:25610176:mean 100:86567680:adagrad" ;;
   deep) SHAPES="1000:44426:mean 1000:44426:avgm 400:44426:mean 100:44426:mean 2000:44426:mean 1000:177704:mean" ;;
   dfr) SHAPES="100:25610176:avgm 100:25610176:mean 100:86567680:adagrad 100:11699136:avgm" ;;
@@ -28,6 +30,6 @@ case $SET in
 esac
 for s in $SHAPES; do
   IFS=: read -r n p op <<< "$s"
-  TUNE_SET=$SET timeout -k 10 200 $T $n $p 3 $op > $O/n${n}_p${p}_$op.txt 2>&1
+  TUNE_SET=$SET timeout -k 10 200 $T $n $p ${ROUNDS:-3} $op > $O/n${n}_p${p}_$op.txt 2>&1
 done
 echo done

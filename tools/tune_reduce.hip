@@ -960,6 +960,39 @@ int main(int argc, char** argv) {
     RME(16, 1, 4, 4, 192, 1);
     RME(16, 1, 4, 3, 192, 1);
   }
+  if (!strcmp(set, "epib4")) {  // product EPIB 2 vs 4, each twice (the duplicates gauge the noise)
+    const int64_t chunks = ((ncols + 3) / 4 + 63) / 64;
+    const int64_t k = (chunks + 192 * 64 - 1) / (192 * 64);
+    if (k % 3 == 0) {
+      RME(16, 1, 4, 3, 192, 2);
+      RME(16, 1, 4, 3, 192, 4);
+      RME(16, 1, 4, 3, 192, 2);
+      RME(16, 1, 4, 3, 192, 4);
+    } else {
+      RME(16, 1, 4, 4, 192, 2);
+      RME(16, 1, 4, 4, 192, 4);
+      RME(16, 1, 4, 4, 192, 2);
+      RME(16, 1, 4, 4, 192, 4);
+    }
+  }
+  if (!strcmp(set, "epib16")) {  // the product's 4-wave x 16 KiB geometry: epilogue batch size B
+    const int64_t chunks = ((ncols + 3) / 4 + 63) / 64;
+    const int64_t k = (chunks + 192 * 64 - 1) / (192 * 64);
+    if (k % 3 == 0) {
+      RME(16, 1, 4, 3, 192, 2);  // product (first: the bitwise reference)
+      RME(16, 1, 4, 3, 192, 1);
+      RME(16, 1, 4, 3, 192, 4);
+      RME(16, 1, 4, 3, 192, 8);
+    } else {
+      RME(16, 1, 4, 4, 192, 2);  // product
+      RME(16, 1, 4, 4, 192, 1);
+      RME(16, 1, 4, 4, 192, 4);
+      RME(16, 1, 4, 4, 192, 8);
+    }
+    RME(16, 1, 4, 2, 192, 2);  // half the accumulators: no AGPR traffic in the sweep
+    RME(8, 1, 8, 2, 192, 2);
+    RME(8, 1, 8, 4, 192, 2);
+  }
   if (!strcmp(set, "epib")) {  // piece epilogue: per-quad guarded loads (0) vs batched buffer loads of B slots
     RME(8, 1, 8, 4, 192, 0);
     RME(8, 1, 8, 4, 192, 2);
