@@ -4,7 +4,7 @@
 set -e
 R=$GRAFT_REPO_ROOT
 SET=${SET:-rm}
-O=$R/gpurun_out/$SET
+O=$R/gpurun_out/${OUTSET:-$SET}
 mkdir -p $O
 T=$R/tools/tune_reduce
 case $SET in

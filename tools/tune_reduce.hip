@@ -1161,16 +1161,34 @@ int main(int argc, char** argv) {
   }
   // copy_roof overwrites the second half of the stack: run the roofs after the checks, and the
   // reduce variants only read, so timings stay valid.
+  // TUNE_FLUSH=1: every timed launch starts from cold caches (a 1-GiB memset between launches
+  // evicts L2 and the 256-MiB Infinity Cache), each launch timed alone
+  const bool flush = getenv("TUNE_FLUSH") && atoi(getenv("TUNE_FLUSH"));
+  void* flush_buf = nullptr;
+  if (flush) CK(hipMalloc(&flush_buf, (size_t)1 << 30));
   for (int r = 0; r < rounds; ++r) {
     for (auto& var : vs) {
       var.launch();  // warm
-      CK(hipEventRecord(a, 0));
       const int reps = 5;
-      for (int k = 0; k < reps; ++k) var.launch();
-      CK(hipEventRecord(b, 0));
-      CK(hipEventSynchronize(b));
-      float ms;
-      CK(hipEventElapsedTime(&ms, a, b));
+      float ms = 0.f;
+      if (flush) {
+        for (int k = 0; k < reps; ++k) {
+          CK(hipMemsetAsync(flush_buf, k & 0xff, (size_t)1 << 30, 0));
+          CK(hipEventRecord(a, 0));
+          var.launch();
+          CK(hipEventRecord(b, 0));
+          CK(hipEventSynchronize(b));
+          float t;
+          CK(hipEventElapsedTime(&t, a, b));
+          ms += t;
+        }
+      } else {
+        CK(hipEventRecord(a, 0));
+        for (int k = 0; k < reps; ++k) var.launch();
+        CK(hipEventRecord(b, 0));
+        CK(hipEventSynchronize(b));
+        CK(hipEventElapsedTime(&ms, a, b));
+      }
       var.times.push_back(ms / reps);
     }
   }
