@@ -54,8 +54,8 @@ sys.path.insert(0, str(REPO))
 from flearn_amd import _native as na  # noqa: E402
 from flearn_amd import aggregator as agg  # noqa: E402
 from flearn_amd import launch, layouts  # noqa: E402
-from flearn_amd.dist import (ALIGN, ShardedReducer, ShardPlan, StripeModel, all_gather_into,  # noqa: E402
-                             hip_reduce_fn, plan_stripes)
+from flearn_amd.dist import (ALIGN, PingPong, ShardedReducer, ShardPlan, StripeModel,  # noqa: E402
+                             all_gather_into, hip_reduce_fn, plan_stripes)
 
 METRIC = "device-resident GiB/s, FedAVG N-client weighted tensor reduce; %HBM peak"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
@@ -155,18 +155,18 @@ class Job:
                              n_cols=plan.shard_of(c))
         self.weights = torch.ones(n, dtype=torch.float32, device=dev)  # Python 1.0 -> fl32(1.0)
         denom = float(np.sum([1.0] * n))  # np.sum(agg_weight_lst), strategy.py:127
-        epi, local_out = {}, None
+        epi, state = {}, None
         if cfg["op"] != "mean":
             prev = torch.empty((1, cols), dtype=torch.float32, device=dev)
             for c in range(plan.stripes):
                 lo = plan.local_begin(c)
                 agg.fill_uniform(prev[:, lo:], seed=1, col_begin=plan.global_begin(c), n_cols=plan.shard_of(c))
-            prev = prev[0]
-            v = torch.zeros(cols, dtype=torch.float64, device=dev)
-            epi = dict(op=na.OP_BY_NAME[cfg["op"]], prev=prev, v=v)
-            local_out = prev  # the fused step advances the global model in place
+            # the fused step reads (prev, v_t) and writes the new global model and v_t into a
+            # second pair, swapped every step — as the product's ServerOptimizer does
+            state = PingPong(prev[0], torch.zeros(cols, dtype=torch.float64, device=dev))
+            epi = dict(op=na.OP_BY_NAME[cfg["op"]], state=state)
         self.fn = hip_reduce_fn(self.stack, self.weights, na.MODE_W32_DIV64, denom, reorder=reorder, **epi)
-        self.red = ShardedReducer(plan, self.fn, dev, local_out=local_out, gather=world > 1)
+        self.red = ShardedReducer(plan, self.fn, dev, gather=world > 1, state=state)
 
     def release(self):
         self.stack = self.red = self.fn = None

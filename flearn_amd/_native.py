@@ -17,7 +17,7 @@ from pathlib import Path
 import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 
 LIB_PATH = Path(__file__).resolve().parent / "lib" / "libflearn_amd.so"
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 FA_OK = 0
 FA_ERR_ARG, FA_ERR_ALIGN, FA_ERR_LAUNCH = -1, -2, -3
@@ -83,6 +83,7 @@ class Epilogue(ctypes.Structure):
         ("h", ctypes.c_void_p),
         ("alpha", ctypes.c_double),
         ("n_clients", ctypes.c_double),
+        ("v_out", ctypes.c_void_p),
     ]
 
 

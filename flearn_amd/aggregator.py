@@ -42,8 +42,18 @@ def _check_cuda(t: torch.Tensor, name: str, dtype: torch.dtype, ndim: int | None
         raise ValueError(f"{name} must be {ndim}-D, got shape {tuple(t.shape)}")
 
 
-def _epilogue(op: int, prev, v, beta=0.9, eta=1e-1, tau=1e-9, beta2=0.99, h=None, alpha=0.0, n_dyn=0):
-    return na.Epilogue(op, 0, _ptr(prev), _ptr(v), beta, eta, tau, beta2, _ptr(h), alpha, float(n_dyn))
+def _epilogue(op: int, prev, v, beta=0.9, eta=1e-1, tau=1e-9, beta2=0.99, h=None, alpha=0.0, n_dyn=0, v_out=None):
+    return na.Epilogue(op, 0, _ptr(prev), _ptr(v), beta, eta, tau, beta2, _ptr(h), alpha, float(n_dyn), _ptr(v_out))
+
+
+def _check_v_out(v_out, v, ncols):
+    if v_out is None:
+        return
+    _check_cuda(v_out, "v_out", v.dtype)
+    if v_out.numel() < ncols or not v_out.is_contiguous():
+        raise ValueError("v_out too small or not contiguous")
+    if v_out.data_ptr() == v.data_ptr():
+        raise ValueError("v_out must be None (in place) or another buffer")
 
 
 # ---------------------------------------------------------------------------------------------
@@ -72,11 +82,15 @@ def reduce_stack(
     h: torch.Tensor | None = None,
     alpha: float = 0.01,
     reorder: bool = False,
+    v_out: torch.Tensor | None = None,
 ) -> None:
     """Weighted mean of the fp32 client stack [N, stride] over columns [col_begin, +n_cols)
     (+ fused update), queued on torch's current stream.  out32/out64/prev/v/h are indexed from
     col_begin.  weights: fp32 for MODE_W32_*, f64 for MODE_W64 (device tensors).
-    op=OP_DYN: FedDyn with h (fp32, in place) and v = theta (in place); prev unused.
+    op=OP_DYN: FedDyn with h (fp32, in place) and v = theta; prev unused.
+    v_out: where the updated v / theta goes (None: back into v).  The fast form of a fused step
+    is double-buffered — out32 not prev, v_out not v, the caller swapping the pairs — because
+    stores onto the lines the epilogue has just loaded cost 1-3% (DESIGN.md §4 finding 20).
     reorder=True: allow fa_reduce_f32_splitn (client splits + a fixed tree: deterministic, within
     1e-6 normwise of the reference, not bit-exact) where it is faster — narrow windows, many
     clients; stack input only."""
@@ -115,14 +129,16 @@ def reduce_stack(
         _check_cuda(v, "theta", vdt)
         if h.numel() < ncols or v.numel() < ncols:
             raise ValueError("h / theta too small")
-        epi = _epilogue(op, None, v, h=h, alpha=alpha, n_dyn=n)
+        _check_v_out(v_out, v, ncols)
+        epi = _epilogue(op, None, v, h=h, alpha=alpha, n_dyn=n, v_out=v_out)
     elif op != na.OP_MEAN:
         vdt = torch.float32 if mode == na.MODE_W32_DIV32 else torch.float64
         _check_cuda(prev, "prev", torch.float32)
         _check_cuda(v, "v", vdt)
         if prev.numel() < ncols or v.numel() < ncols:
             raise ValueError("prev / v too small")
-        epi = _epilogue(op, prev, v, beta, eta, tau, beta2)
+        _check_v_out(v_out, v, ncols)
+        epi = _epilogue(op, prev, v, beta, eta, tau, beta2, v_out=v_out)
     if rows:
         pieces, npieces, grid = stack.piece_table(op)
         rc = L.fa_reduce_f32_rows(
@@ -274,7 +290,8 @@ class ServerOptimizer:
         self.op = na.OP_BY_NAME[op]
         self.name = op
         self.beta, self.eta, self.tau, self.beta2 = beta, eta, tau, beta2
-        self.state = {}  # shard index -> (prev, v)
+        self.state = {}  # shard index -> (prev, v): the current previous global model and v_t
+        self.spare = {}  # shard index -> (prev, v) buffers the next fused step writes into
         self._sig = None
         self._pending_init = None
         self.group = None  # (process group, world) when bound to a column-sharded Aggregator
@@ -323,6 +340,17 @@ class ServerOptimizer:
                                  torch.zeros(sh.width, dtype=self._vdtype(plan), device=sh.device))
                       for sh in shards}
         self._sig = self._signature(plan, shards)
+
+    def swap_buffers(self, sh):
+        """(prev, v, prev_out, v_out) of a fused step on shard sh, and the state advanced to the
+        output pair: the step reads the current pair and writes the other one (double-buffered,
+        DESIGN.md §4 finding 20); the pair it read becomes the next step's output."""
+        prev, v = self.state[sh.index]
+        spare = self.spare.get(sh.index)
+        if spare is None or spare[0].shape != prev.shape or spare[1].dtype != v.dtype or spare[0].device != prev.device:
+            spare = (torch.empty_like(prev), torch.empty_like(v))
+        self.state[sh.index], self.spare[sh.index] = spare, (prev, v)
+        return prev, v, spare[0], spare[1]
 
     def v_t(self, plan: BucketPlan) -> dict:
         """The state as the reference exposes it (self.v_t dict of arrays).  With a column-sharded
@@ -744,12 +772,13 @@ class Aggregator:
         if isinstance(server_opt, DynState):
             return server_opt.step(self, sh, stack, w, nm, want64)
         if server_opt is not None and fused:
-            # fused: prev is updated in place to fl32(w) — the model clients load next round
-            prev, v = server_opt.state[sh.index]
-            reduce_stack(stack, w, nm.mode, nm.denom, out32=prev, out64=out64, op=server_opt.op, prev=prev, v=v,
-                         beta=server_opt.beta, eta=server_opt.eta, tau=server_opt.tau, beta2=server_opt.beta2,
-                         reorder=self.reorder and not isinstance(stack, RowTable))
-            return out64 if want64 else prev
+            # fused: fl32(w) becomes the next round's prev (the model clients load), v_t advances;
+            # both into the spare pair, which then becomes the state (double-buffered)
+            prev, v, prev_o, v_o = server_opt.swap_buffers(sh)
+            reduce_stack(stack, w, nm.mode, nm.denom, out32=prev_o, out64=out64, op=server_opt.op, prev=prev, v=v,
+                         v_out=v_o, beta=server_opt.beta, eta=server_opt.eta, tau=server_opt.tau,
+                         beta2=server_opt.beta2, reorder=self.reorder and not isinstance(stack, RowTable))
+            return out64 if want64 else prev_o
         out32 = None
         if not want64 or server_opt is not None:
             out32 = self.packer.device_bucket(("out32", KIND_F32, sh.index), (sh.width,), torch.float32, sh.device)

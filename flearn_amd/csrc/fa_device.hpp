@@ -121,6 +121,7 @@ struct Epi {
   float* out32;
   double* out64;
   unsigned long long* trace;  // tuning only (reduce_kernel_rowmajor<..., TR = true>): phase timestamps
+  T* v_out;                   // where the updated v goes; NULL: back into v (in place)
 };
 
 template <typename T>
@@ -189,7 +190,7 @@ __device__ __forceinline__ void finish_quad(const Epi<T>& e, int64_t c, int vali
       vv[j] = vj;
     }
   }
-  if constexpr (OP != FA_OP_MEAN) store_quad<T>(e.v + c, vv, valid);
+  if constexpr (OP != FA_OP_MEAN) store_quad<T>((e.v_out ? e.v_out : e.v) + c, vv, valid);
   if (e.out32) {
     typename vec4<float>::type o = {(float)w[0], (float)w[1], (float)w[2], (float)w[3]};
     store_quad<float>(e.out32 + c, o, valid);
@@ -349,10 +350,11 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t col_rsrc(E* base, int64_t qbas
 // the plain mean, the state gets an empty range.
 template <typename T, int OP>
 struct EpiRsrc {
-  __amdgpu_buffer_rsrc_t rl, rv, r32, r64;
+  __amdgpu_buffer_rsrc_t rl, rv, rvo, r32, r64;
   __device__ __forceinline__ EpiRsrc(const Epi<T>& e, int64_t qbase, int cols)
       : rl(col_rsrc<const float>(OP == FA_OP_DYN ? e.h : e.prev, qbase, OP == FA_OP_MEAN ? 0 : cols)),
         rv(col_rsrc<T>(e.v, qbase, OP == FA_OP_MEAN ? 0 : cols)),
+        rvo(col_rsrc<T>(e.v_out ? e.v_out : e.v, qbase, OP == FA_OP_MEAN ? 0 : cols)),
         r32(col_rsrc<float>(e.out32, qbase, cols)),
         r64(col_rsrc<double>(e.out64, qbase, cols)) {}
 };
@@ -406,7 +408,7 @@ __device__ __forceinline__ void epi_store(const Epi<T>& e, const EpiRsrc<T, OP>&
                                           const typename vec4<float>::type l, const typename vec4<T>::type vv,
                                           const typename vec4<T>::type w) {
   if constexpr (OP == FA_OP_DYN) buf_store_tquad<float>(r.rl, q, l);
-  if constexpr (OP != FA_OP_MEAN) buf_store_tquad<T>(r.rv, q, vv);
+  if constexpr (OP != FA_OP_MEAN) buf_store_tquad<T>(r.rvo, q, vv);
   if (!GUARD || e.out32) buf_store_tquad<float>(r.r32, q, typename vec4<float>::type{(float)w[0], (float)w[1], (float)w[2], (float)w[3]});
   if (!GUARD || e.out64) buf_store_tquad<double>(r.r64, q, typename vec4<double>::type{(double)w[0], (double)w[1], (double)w[2], (double)w[3]});
 }

@@ -321,6 +321,8 @@ int dispatch_op(int op, const typename P::x_t* stack, int64_t stride, int n, con
   }
 }
 
+bool aligned_to(const void* p, size_t a) { return ((uintptr_t)p % a) == 0; }
+
 template <typename T>
 int make_epi(const fa_epilogue* in, double denom, int n_reduced, float* out32, double* out64, Epi<T>* e) {
   e->denom = (T)denom;
@@ -328,6 +330,7 @@ int make_epi(const fa_epilogue* in, double denom, int n_reduced, float* out32, d
   e->v = nullptr;
   e->h = nullptr;
   e->trace = nullptr;
+  e->v_out = nullptr;
   e->beta = e->eta = e->tau = e->beta2 = e->c = e->n = T(0);
   e->alpha32 = 0.f;
   e->out32 = out32;
@@ -336,6 +339,11 @@ int make_epi(const fa_epilogue* in, double denom, int n_reduced, float* out32, d
   if (in->op < FA_OP_AVGM || in->op > FA_OP_DYN) return fail(FA_ERR_ARG, "unknown epilogue op");
   if (!in->v) return fail(FA_ERR_ARG, "epilogue needs v");
   e->v = static_cast<T*>(in->v);
+  if (in->v_out) {
+    if (!aligned_to(in->v_out, 4 * sizeof(T))) return fail(FA_ERR_ALIGN, "v_out must be 4-element aligned");
+    if (in->v_out == in->v) return fail(FA_ERR_ARG, "v_out must be NULL (in place) or another array");
+    e->v_out = static_cast<T*>(in->v_out);
+  }
   if (in->op == FA_OP_DYN) {
     if (!in->h) return fail(FA_ERR_ARG, "FedDyn epilogue needs h");
     const double nc = in->n_clients > 0 ? in->n_clients : (double)n_reduced;
@@ -356,7 +364,6 @@ int make_epi(const fa_epilogue* in, double denom, int n_reduced, float* out32, d
   return FA_OK;
 }
 
-bool aligned_to(const void* p, size_t a) { return ((uintptr_t)p % a) == 0; }
 
 // per-column arrays are accessed with 4-element vector loads/stores
 int check_columns(const float* out32, const double* out64, const void* prev, const void* v,

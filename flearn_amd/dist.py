@@ -202,6 +202,31 @@ class ShardPlan:
         return max(0, min(self.widths[stripe], self.n_cols - g0))
 
 
+class PingPong:
+    """Double-buffered state of a fused server step on one rank's columns (FedAVGM / FedOPT):
+    step k reads (prev[k % 2], v[k % 2]) and writes the global model and v_t into the other pair,
+    so the kernel's epilogue stores never land on the lines it has just loaded (in place costs
+    1-3% per launch, DESIGN.md §4 finding 20).  `out` is where the current step writes the fp32
+    model (the next step's prev); `flip()` advances after every stripe of a step is launched."""
+
+    def __init__(self, prev: torch.Tensor, v: torch.Tensor):
+        self.prev = [prev, torch.empty_like(prev)]
+        self.v = [v, torch.empty_like(v)]
+        self.cur = 0
+
+    @property
+    def out(self) -> torch.Tensor:
+        return self.prev[1 - self.cur]
+
+    def window(self, c0: int, n: int):
+        """(prev, v, v_out) of local columns [c0, c0 + n) for the current step."""
+        i, o = self.cur, 1 - self.cur
+        return self.prev[i][c0 : c0 + n], self.v[i][c0 : c0 + n], self.v[o][c0 : c0 + n]
+
+    def flip(self):
+        self.cur ^= 1
+
+
 class ShardedReducer:
     """Runs one aggregation step on this rank's shard and reassembles the full bucket.
 
@@ -210,7 +235,7 @@ class ShardedReducer:
     the oracle to check the sharding and gather logic with gloo.
     """
 
-    def __init__(self, plan: ShardPlan, reduce_fn, device, group=None, local_out=None, gather=None):
+    def __init__(self, plan: ShardPlan, reduce_fn, device, group=None, local_out=None, gather=None, state=None):
         self.plan = plan
         self.reduce_fn = reduce_fn
         self.device = torch.device(device)
@@ -218,41 +243,57 @@ class ShardedReducer:
         # gather=None: all-gather only when there is more than one rank; True forces the
         # collective path (a 1-rank RCCL group exercises the exact multi-GPU call sequence)
         self.gather = plan.world > 1 if gather is None else gather
-        # local_out may alias the sharded `prev` of a fused optimizer (updated in place)
-        self.local_out = (torch.empty(plan.local_cols, dtype=torch.float32, device=self.device)
-                          if local_out is None else local_out)
+        # state: the PingPong of a fused optimizer — each step writes into its `out` buffer;
+        # local_out may alias the sharded `prev` of a fused optimizer updated in place
+        self.state = state
+        self._local_out = (None if state is not None else
+                           torch.empty(plan.local_cols, dtype=torch.float32, device=self.device)
+                           if local_out is None else local_out)
         # one rank: local columns ARE the global columns, nothing to reassemble
         self.full = (torch.empty(plan.padded, dtype=torch.float32, device=self.device) if self.gather
-                     else self.local_out)
+                     else None)
+
+    @property
+    def local_out(self) -> torch.Tensor:
+        """Where the current step writes this rank's columns."""
+        return self.state.out if self.state is not None else self._local_out
 
     def step(self) -> torch.Tensor:
         p = self.plan
         works = []
+        out = self.local_out
         for c in range(p.stripes):
             lo, sc = p.local_begin(c), p.shard_of(c)
-            self.reduce_fn(lo, sc, self.local_out[lo : lo + sc])
+            self.reduce_fn(lo, sc, out[lo : lo + sc])
             if self.gather:
                 g0 = p.world * lo  # stripe c's contiguous range of the global bucket
                 dst = self.full[g0 : g0 + p.world * sc]
-                w = all_gather_into(dst, self.local_out[lo : lo + sc], group=self.group, async_op=True)
+                w = all_gather_into(dst, out[lo : lo + sc], group=self.group, async_op=True)
                 if w is not None:
                     works.append(w)
+        if self.state is not None:
+            self.state.flip()
         for w in works:
             w.wait()
-        return self.full[: p.n_cols]
+        return self.full[: p.n_cols] if self.gather else out[: p.n_cols]
 
 
-def hip_reduce_fn(stack, weights, mode, denom, reorder=False, **epilogue):
+def hip_reduce_fn(stack, weights, mode, denom, reorder=False, state: PingPong | None = None, **epilogue):
     """reduce_fn over a device-resident local stack [N, local_cols] with the fused HIP kernel.
-    Epilogue state tensors (prev, v), if any, are local-column tensors and are sliced alike.
-    reorder: allow the split-N kernel (aggregator.reduce_stack)."""
+    Epilogue state: a PingPong (double-buffered: the step reads its current pair, writes the
+    model into out_slice — the PingPong's `out` — and v_t into the other v), or prev / v
+    local-column tensors updated in place.  reorder: allow the split-N kernel
+    (aggregator.reduce_stack)."""
     from .aggregator import reduce_stack
 
     prev, v = epilogue.pop("prev", None), epilogue.pop("v", None)
 
     def fn(col_begin, n_cols, out_slice):
         kw = dict(epilogue)
-        if prev is not None:
+        if state is not None:
+            p_in, v_in, v_out = state.window(col_begin, n_cols)
+            kw.update(prev=p_in, v=v_in, v_out=v_out)
+        elif prev is not None:
             kw.update(prev=prev[col_begin : col_begin + n_cols], v=v[col_begin : col_begin + n_cols])
         reduce_stack(stack, weights, mode, denom, col_begin=col_begin, n_cols=n_cols, out32=out_slice, reorder=reorder,
                      **kw)

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define FA_ABI_VERSION 5
+#define FA_ABI_VERSION 6
 
 /* return codes */
 #define FA_OK 0
@@ -79,9 +79,15 @@ typedef struct fa_epilogue {
   float* h;          /* FA_OP_DYN: [n_cols] fp32 h, updated in place; else NULL          */
   double alpha;      /* FA_OP_DYN alpha (dyn.py:15, 0.01)                                */
   double n_clients;  /* FA_OP_DYN len(w_local_lst) (dyn.py:21,26); 0 = the reduce's N    */
+  void* v_out;       /* NULL: the updated v_t / theta is written back into v (in place);
+                        else [n_cols] of v's element type, not overlapping v: the updated
+                        state goes here and v is only read (ABI 6)                          */
 } fa_epilogue;
-/* FA_OP_DYN: v is theta (double* / float*, updated in place to w); prev is unused.  out32 /
- * out64 may alias v when they have its element type (each element is read before written). */
+/* FA_OP_DYN: v is theta (double* / float*, updated to w); prev is unused.  out32 / out64 may
+ * alias v or prev when they have its element type (each element is read before written).
+ * Double-buffered state (out32 != prev, v_out != v, the caller swapping the pairs each round)
+ * is the fast form: in place, the epilogue's stores land on the lines it has just loaded and
+ * the fused launch runs 1-3% slower (DESIGN.md §4 finding 20).                                */
 
 int fa_abi_version(void);
 const char* fa_last_error(void);

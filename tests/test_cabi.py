@@ -56,18 +56,18 @@ def test_epilogue_struct_layout_matches_c(tmp_path):
     src = tmp_path / "layout.c"
     src.write_text(
         '#include <stddef.h>\n#include <stdio.h>\n#include "flearn_amd.h"\n'
-        "int main(void){printf(\"%zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu\\n\", sizeof(fa_epilogue),"
+        "int main(void){printf(\"%zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu\\n\", sizeof(fa_epilogue),"
         "offsetof(fa_epilogue,op),offsetof(fa_epilogue,reserved),offsetof(fa_epilogue,prev),"
         "offsetof(fa_epilogue,v),offsetof(fa_epilogue,beta),offsetof(fa_epilogue,eta),"
         "offsetof(fa_epilogue,tau),offsetof(fa_epilogue,beta2),offsetof(fa_epilogue,h),"
-        "offsetof(fa_epilogue,alpha),offsetof(fa_epilogue,n_clients));return 0;}\n"
+        "offsetof(fa_epilogue,alpha),offsetof(fa_epilogue,n_clients),offsetof(fa_epilogue,v_out));return 0;}\n"
     )
     exe = tmp_path / "layout"
     subprocess.run(["gcc", "-I", str(HEADER.parent), str(src), "-o", str(exe)], check=True)
     c = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True).stdout.split()]
     E = na.Epilogue
     py = [ctypes.sizeof(E)] + [getattr(E, f).offset for f in ("op", "reserved", "prev", "v", "beta", "eta", "tau", "beta2",
-                                                           "h", "alpha", "n_clients")]
+                                                           "h", "alpha", "n_clients", "v_out")]
     assert c == py
 
 

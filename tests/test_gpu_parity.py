@@ -561,6 +561,63 @@ def test_sharded_reducer_rccl_one_rank(op, stripes, weights, cuda, tmp_path):
             dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("op", ["avgm", "adagrad", "yogi", "adam"])
+def test_fused_v_out_equals_in_place(op, cuda):
+    """ABI 6 v_out: the double-buffered form (out32 into a fresh buffer, v_t into v_out) gives the
+    in-place results bit for bit and leaves prev and v untouched."""
+    n, p = 7, 300_001
+    stack = torch.empty((n, p + 63), dtype=torch.float32, device=cuda)
+    agg.fill_uniform(stack, seed=11)
+    w = torch.ones(n, dtype=torch.float32, device=cuda)
+    prev = torch.empty((1, p + 63), dtype=torch.float32, device=cuda)
+    agg.fill_uniform(prev, seed=12)
+    prev = prev[0, :p].contiguous()
+    v0 = torch.full((p,), 0.125, dtype=torch.float64, device=cuda)
+    kw = dict(op=na.OP_BY_NAME[op], n_cols=p)
+    # in place
+    prev_a, v_a = prev.clone(), v0.clone()
+    agg.reduce_stack(stack, w, na.MODE_W32_DIV64, float(n), out32=prev_a, prev=prev_a, v=v_a, **kw)
+    # double-buffered
+    prev_b, v_b = prev.clone(), v0.clone()
+    out_b, vo_b = torch.empty_like(prev_b), torch.full_like(v_b, -1.0)
+    agg.reduce_stack(stack, w, na.MODE_W32_DIV64, float(n), out32=out_b, prev=prev_b, v=v_b, v_out=vo_b, **kw)
+    assert bitwise_equal(out_b.cpu().numpy(), prev_a.cpu().numpy())
+    assert bitwise_equal(vo_b.cpu().numpy(), v_a.cpu().numpy())
+    assert bitwise_equal(prev_b.cpu().numpy(), prev.cpu().numpy())
+    assert bitwise_equal(v_b.cpu().numpy(), v0.cpu().numpy())
+    with pytest.raises(ValueError):
+        agg.reduce_stack(stack, w, na.MODE_W32_DIV64, float(n), out32=out_b, prev=prev_b, v=v_b, v_out=v_b, **kw)
+
+
+@pytest.mark.parametrize("op,stripes", [("avgm", 1), ("adagrad", 2)])
+def test_pingpong_reducer_three_steps(op, stripes, cuda):
+    """bench.py's fused job: PingPong state over three steps (the buffers swap every step) equals
+    three in-place oracle steps, model and v_t."""
+    from flearn_amd.dist import PingPong, ShardedReducer, ShardPlan, hip_reduce_fn
+
+    n, p = 5, 200_003
+    plan = ShardPlan.make(p, 1, 0, stripes=stripes, weights=(3, 1) if stripes == 2 else None)
+    stack = torch.empty((n, plan.local_cols), dtype=torch.float32, device=cuda)
+    for c in range(plan.stripes):
+        agg.fill_uniform(stack[:, plan.local_begin(c):], seed=21, col_begin=plan.global_begin(c),
+                         n_cols=plan.shard_of(c))
+    prev = torch.empty((1, plan.local_cols), dtype=torch.float32, device=cuda)
+    agg.fill_uniform(prev, seed=22)
+    prev_h = prev[0, :p].cpu().numpy().copy()
+    state = PingPong(prev[0], torch.zeros(plan.local_cols, dtype=torch.float64, device=cuda))
+    w = torch.ones(n, dtype=torch.float32, device=cuda)
+    red = ShardedReducer(plan, hip_reduce_fn(stack, w, na.MODE_W32_DIV64, float(n), op=na.OP_BY_NAME[op],
+                                             state=state), cuda, state=state)
+    mean = oracle.c_reduce(oracle.MODE_W32_DIV64, oracle.fill_uniform(n, p, 21), np.ones(n, np.float32), float(n))
+    v_h = np.zeros(p)
+    for k in range(3):
+        got = red.step().cpu().numpy()
+        want = oracle.c_update(op, mean, prev_h, v_h).astype(np.float32)
+        assert bitwise_equal(got, want), f"step {k}"
+        assert bitwise_equal(state.v[state.cur][:p].cpu().numpy(), v_h), f"v step {k}"
+        prev_h = want
+
+
 # ---------------------------------------------------------------------------------------------
 # column shards over several devices (per-GPU parallel ingest); here 2-3 shards on one GPU
 # ---------------------------------------------------------------------------------------------

@@ -960,6 +960,34 @@ int main(int argc, char** argv) {
     RME(16, 1, 4, 4, 192, 1);
     RME(16, 1, 4, 3, 192, 1);
   }
+  if (!strcmp(set, "inplace")) {  // product geometry, separate out32 vs out32 == prev (bench.py's in-place step)
+    const int64_t chunks = ((ncols + 3) / 4 + 63) / 64;
+    const int64_t k = (chunks + 192 * 64 - 1) / (192 * 64);
+    const int kg = k % 3 == 0 ? 3 : 4;
+    double* v2 = nullptr;
+    if (avgm) CK(hipMalloc(&v2, stride * 8));
+    for (int rep = 0; rep < 2; ++rep) {
+      for (int mode = 0; mode < 4; ++mode) {  // bit 0: out32 == prev; bit 1: v_out = a second v
+        const int inpl = mode & 1;
+        if (!avgm && mode) continue;
+        Epi<double> e2 = e;
+        if (inpl && avgm) e2.out32 = prev;
+        if (mode & 2) e2.v_out = v2;
+        Variant v = kg == 3 ? (op == FA_OP_AVGM      ? make_rowmajor<16, 1, 4, 3, FA_OP_AVGM, double, 4>(stack, stride, n, w, ncols, e2, bytes, 192)
+                               : op == FA_OP_ADAGRAD ? make_rowmajor<16, 1, 4, 3, FA_OP_ADAGRAD, double, 4>(stack, stride, n, w, ncols, e2, bytes, 192)
+                                                     : make_rowmajor<16, 1, 4, 3, FA_OP_MEAN, double, 4>(stack, stride, n, w, ncols, e2, bytes, 192))
+                            : (op == FA_OP_AVGM      ? make_rowmajor<16, 1, 4, 4, FA_OP_AVGM, double, 4>(stack, stride, n, w, ncols, e2, bytes, 192)
+                               : op == FA_OP_ADAGRAD ? make_rowmajor<16, 1, 4, 4, FA_OP_ADAGRAD, double, 4>(stack, stride, n, w, ncols, e2, bytes, 192)
+                                                     : make_rowmajor<16, 1, 4, 4, FA_OP_MEAN, double, 4>(stack, stride, n, w, ncols, e2, bytes, 192));
+        if (mode & 2) v.name += " v2";
+        if (inpl && avgm) {
+          v.name += " inplace";
+          v.checks_output = false;
+        }
+        vs.push_back(v);
+      }
+    }
+  }
   if (!strcmp(set, "epib4")) {  // product EPIB 2 vs 4, each twice (the duplicates gauge the noise)
     const int64_t chunks = ((ncols + 3) / 4 + 63) / 64;
     const int64_t k = (chunks + 192 * 64 - 1) / (192 * 64);
