@@ -725,6 +725,11 @@ int main(int argc, char** argv) {
     e.prev = prev;
     e.v = v;
   }
+  if (avgm && getenv("TUNE_V2") && atoi(getenv("TUNE_V2"))) {  // double-buffered v_t (the product's form)
+    double* vdb;
+    CK(hipMalloc(&vdb, stride * 8));
+    e.v_out = vdb;
+  }
   const double bytes = (double)n * ncols * 4 + ncols * 4 + (avgm ? ncols * (4.0 + 16.0) : 0.0);
 
   std::vector<Variant> vs;
