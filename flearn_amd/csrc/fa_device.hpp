@@ -308,6 +308,11 @@ __device__ __forceinline__ vec4<float>::type buf_load_quad(__amdgpu_buffer_rsrc_
 #ifndef FA_EPI_STORE_AUX
 #define FA_EPI_STORE_AUX 2
 #endif
+// 8-byte elements (v_t / theta state in f64, the f64 result) are stored as two 16-B halves per
+// quad, each instruction covering every other 16 B of a wave's 2 KiB: partial 128-B lines.
+#ifndef FA_EPI_STORE64_AUX
+#define FA_EPI_STORE64_AUX FA_EPI_STORE_AUX
+#endif
 template <typename T>
 __device__ __forceinline__ typename vec4<T>::type buf_load_tquad(__amdgpu_buffer_rsrc_t r, int q) {
   if constexpr (sizeof(T) == 4) {
@@ -327,8 +332,8 @@ __device__ __forceinline__ void buf_store_tquad(__amdgpu_buffer_rsrc_t r, int q,
   } else {
     typedef double d2 __attribute__((ext_vector_type(2)));
     const d2 lo = {v[0], v[1]}, hi = {v[2], v[3]};
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, lo), r, q * 32, 0, FA_EPI_STORE_AUX);
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, hi), r, q * 32 + 16, 0, FA_EPI_STORE_AUX);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, lo), r, q * 32, 0, FA_EPI_STORE64_AUX);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, hi), r, q * 32 + 16, 0, FA_EPI_STORE64_AUX);
   }
 }
 

@@ -1,0 +1,14 @@
+# f64 state / result stores: non-temporal (product) vs cached (FA_EPI_STORE64_AUX=0), double-buffered
+# v_t (TUNE_V2=1), alternating binaries on one box.
+set -e
+R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out/s64
+mkdir -p $O
+cd $R
+for s in 100:86567680:adagrad 100:25610176:avgm; do
+  IFS=: read -r n p op <<< "$s"
+  for b in tune_reduce tune_reduce_s64c tune_reduce tune_reduce_s64c; do
+    TUNE_V2=1 TUNE_SET=epib4 timeout -k 10 200 tools/$b $n $p 3 $op >> $O/${b}_n${n}_p${p}_$op.txt 2>&1
+  done
+done
+echo done
