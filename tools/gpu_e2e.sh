@@ -10,8 +10,9 @@ for c in c1 c2; do timeout -k 10 300 python3 $R/tools/bench_wire.py --config $c 
 timeout -k 10 300 python3 $R/tools/bench_wire.py --config c2 --stage > $O/wire_c2_stage.json 2> $O/wire_c2_stage.err
 for c in c2 ns c3; do timeout -k 10 300 python3 $R/tools/bench_rows.py --config $c > $O/rows_$c.json 2> $O/rows_$c.err; done
 for g in 2 4 8; do
-  timeout -k 10 200 python3 $R/bench.py --emulate-world $g --no-cpu-baseline --steps 30 > $O/emu_ns_weak_g$g.json 2> $O/emu_ns_weak_g$g.err
+  timeout -k 10 200 python3 $R/bench.py --emulate-world $g --scaling weak --no-cpu-baseline --steps 30 > $O/emu_ns_weak_g$g.json 2> $O/emu_ns_weak_g$g.err
   timeout -k 10 200 python3 $R/bench.py --emulate-world $g --scaling strong --no-cpu-baseline --steps 30 > $O/emu_ns_strong_g$g.json 2> $O/emu_ns_strong_g$g.err
   timeout -k 10 200 python3 $R/bench.py --config c4 --scaling strong --emulate-world $g --no-cpu-baseline --steps 20 > $O/emu_c4strong_g$g.json 2> $O/emu_c4strong_g$g.err
+  timeout -k 10 200 python3 $R/bench.py --config c5 --scaling strong --emulate-world $g --no-cpu-baseline --steps 20 > $O/emu_c5strong_g$g.json 2> $O/emu_c5strong_g$g.err
 done
 echo done
