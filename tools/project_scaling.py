@@ -1,0 +1,68 @@
+"""Strong-scaling projection of bench.py --gpus G from the stripe model
+(flearn_amd.dist.StripeModel / plan_stripes) with a per-link xGMI assumption.
+
+On an 8-GPU MI355X node every GPU has one xGMI link to each peer, so an all-gather among G GPUs
+brings (G-1)/G of the bucket into each GPU over G-1 links: ingress(G) = (G-1) * link rate.  The
+reduce coefficients are the measured 1-GPU kernel rates (profiles/r03/final), the launch and
+collective constants the model's a priori ones.  A PROJECTION: nothing here has run on more than
+one GPU.
+
+    python tools/project_scaling.py [--link-gbs 50,64] [--json]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import sys
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(REPO))
+
+from flearn_amd.dist import ALIGN, StripeModel, plan_stripes  # noqa: E402
+
+# config -> (clients, fp32 params, 1-GPU step of the final profile pass in s, algorithmic bytes/col)
+CONFIGS = {
+    "ns": (100, 25_610_152),
+    "c4": (1000, 11_699_112),
+    "c5": (100, 86_567_656),
+}
+
+
+def one_gpu_step(cfg: str) -> float:
+    d = json.loads((REPO / "profiles" / "r03" / "final" / cfg / f"bench_{cfg}.json").read_text())
+    return d["ms_per_step"] / 1e3
+
+
+def project(cfg: str, g: int, link_bs: float, launch_s=10e-6, collective_s=30e-6):
+    n, p = CONFIGS[cfg]
+    t1 = one_gpu_step(cfg)
+    local = -(-p // g)
+    local = -(-local // ALIGN) * ALIGN
+    b_r = t1 / p  # the 1-GPU per-column cost (fused state traffic included)
+    b_g = (g - 1) * 4.0 / ((g - 1) * link_bs) if g > 1 else 0.0
+    m = StripeModel(launch_s, b_r, collective_s if g > 1 else 0.0, b_g)
+    widths = plan_stripes(local, m) if g > 1 else (local,)
+    step, red, exposed = m.makespan(widths)
+    return {"config": cfg, "gpus": g, "link_GBs": link_bs / 1e9, "ingress_GBs": (g - 1) * link_bs / 1e9,
+            "stripes": len(widths), "step_ms": round(step * 1e3, 3), "reduce_ms": round(red * 1e3, 3),
+            "exposed_gather_ms": round(exposed * 1e3, 3), "speedup": round(t1 / step, 2)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--link-gbs", default="50,64")
+    ap.add_argument("--json", action="store_true")
+    a = ap.parse_args()
+    rows = [project(c, g, float(l) * 1e9) for l in a.link_gbs.split(",") for c in CONFIGS for g in (2, 4, 8)]
+    if a.json:
+        print(json.dumps(rows, indent=1))
+        return
+    for r in rows:
+        print(f"{r['link_GBs']:>5.0f} GB/s/link  {r['config']:>3}  G={r['gpus']}  ingress {r['ingress_GBs']:>4.0f} GB/s  "
+              f"{r['stripes']} stripes  step {r['step_ms']:.3f} ms  (reduce {r['reduce_ms']:.3f}, exposed gather "
+              f"{r['exposed_gather_ms']:.3f})  {r['speedup']:.2f}x")
+
+
+if __name__ == "__main__":
+    main()
