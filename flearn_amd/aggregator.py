@@ -399,6 +399,7 @@ class DynState:
         self.h_host = h
         self._theta_init = None if h is None else {k: np.array(_as_host(v), copy=True) for k, v in h.items()}
         self.state = {}  # shard index -> (h fp32, theta)
+        self._spare = {}  # shard index -> the theta buffer the next fused round writes into
         self._sig = None
         self._tdt = None
         self._dirty = False
@@ -480,9 +481,15 @@ class DynState:
         if self._covered:
             out32 = None if want64 else agg.packer.device_bucket(("out32", KIND_F32, sh.index), (sh.width,),
                                                                    torch.float32, sh.device)
-            reduce_stack(stack, w, nm.mode, nm.denom, out32=out32, out64=th if want64 else None, op=na.OP_DYN,
-                         v=th, h=hs, alpha=self.alpha)
-            return th if want64 else out32
+            # theta double-buffered (read one, write the other, swap; DESIGN.md §4 finding 20); h, the
+            # caller-visible state synced back by sync_h, stays in place
+            th_o = self._spare.get(sh.index)
+            if th_o is None or th_o.shape != th.shape or th_o.dtype != th.dtype or th_o.device != th.device:
+                th_o = torch.empty_like(th)
+            reduce_stack(stack, w, nm.mode, nm.denom, out32=out32, out64=th_o if want64 else None,
+                         op=na.OP_DYN, v=th, v_out=th_o, h=hs, alpha=self.alpha)
+            self.state[sh.index], self._spare[sh.index] = (hs, th_o), th
+            return th_o if want64 else out32
         # partial coverage: mean in theta's precision, then the update on the covered runs
         gbuf = agg.packer.device_bucket(("dyn_g", KIND_F32, sh.index), (sh.width,), th.dtype, sh.device)
         reduce_stack(stack, w, nm.mode, nm.denom, out32=None if f64 else gbuf, out64=gbuf if f64 else None)
