@@ -447,6 +447,138 @@ __global__ __launch_bounds__(64 * W) void reduce_kernel_rowmajor_tail(const floa
   }
 }
 
+// [tuning] The narrow-window kernel with narrower strips per wave: lane l reads LB bytes (one
+// dword, a dword pair or a quad) of every row, so a single-wave block owns a 64*LB-byte strip of
+// the window.  With LB = 4 a row slot costs one VGPR instead of four, so the same vmcnt budget
+// (63 loads) is reached with a quarter of the registers, and a LeNet-wide window is 4x as many
+// waves (695 instead of 174 for 44,426 columns), spread over every CU instead of 174 of the 256.
+// Same pipeline as reduce_kernel_narrow (no drain code, weights broadcast by readlane), same sums,
+// same order.  The epilogue regroups the strip into quads with cross-lane reads (lane q gets the
+// columns 4q..4q+3) and applies the usual piece epilogue; lanes past the strip's quads are dropped
+// by the descriptor range.
+template <int LB>
+struct LaneCols;
+template <>
+struct LaneCols<4> {
+  static constexpr int C = 1;
+  template <bool NT>
+  static __device__ __forceinline__ void load(__amdgpu_buffer_rsrc_t r, int voff, float (&x)[1]) {
+    x[0] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, voff, 0, NT ? 2 : 0));
+  }
+};
+template <>
+struct LaneCols<8> {
+  static constexpr int C = 2;
+  template <bool NT>
+  static __device__ __forceinline__ void load(__amdgpu_buffer_rsrc_t r, int voff, float (&x)[2]) {
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    const f2 v = __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(r, voff, 0, NT ? 2 : 0));
+    x[0] = v[0];
+    x[1] = v[1];
+  }
+};
+
+template <class P, typename T, int OP, int LB, int D, bool NT>
+__global__ __launch_bounds__(64) void reduce_kernel_narrow_lb(const float* __restrict__ stack, int64_t stride, int n,
+                                                              const typename P::w_t* __restrict__ w, int64_t col0,
+                                                              int64_t ncols, Epi<T> e) {
+  static_assert(sizeof(typename P::x_t) == 4 && D <= 62, "4-byte rows; vmcnt counts 63 loads (+ the weights)");
+  typedef LaneCols<LB> LC;
+  constexpr int C = LC::C;
+  constexpr int SC = 64 * C;  // columns of the strip
+  typedef typename P::acc_t A;
+  typedef typename P::w_t WT;
+  const int64_t cb = (int64_t)blockIdx.x * SC;
+  if (cb >= ncols) return;
+  const int cols = ncols - cb < SC ? (int)(ncols - cb) : SC;
+  const uint32_t bytes = (uint32_t)cols * 4u;
+  const int lane = (int)threadIdx.x & 63;
+  const int voff = lane * LB;
+  const int64_t rb = stride * 4;
+  const char* base = reinterpret_cast<const char*>(stack + col0 + cb);
+  const char* lastp = base + (int64_t)(n - 1) * rb;
+  const char* p = base + rb;
+#define FA_NL_LOAD(dst, CLAMP)                                  \
+  {                                                             \
+    const char* q_ = p;                                         \
+    if (CLAMP) q_ = p <= lastp ? p : lastp;                     \
+    LC::template load<NT>(row_rsrc(q_, bytes), voff, dst);      \
+    p += rb;                                                    \
+    asm volatile("" : "+s"(p));                                 \
+  }
+  const __amdgpu_buffer_rsrc_t wr = row_rsrc(w, (uint32_t)n * (uint32_t)sizeof(WT));
+  auto wload = [&](int first) {
+    if constexpr (sizeof(WT) == 4)
+      return __builtin_bit_cast(WT, __builtin_amdgcn_raw_buffer_load_b32(wr, (lane + first) * 4, 0, 0));
+    else
+      return __builtin_bit_cast(WT, __builtin_amdgcn_raw_buffer_load_b64(wr, (lane + first) * 8, 0, 0));
+  };
+  auto wlane = [](WT v, int l) {
+    if constexpr (sizeof(WT) == 4) {
+      return __builtin_bit_cast(WT, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
+    } else {
+      const long long b = __builtin_bit_cast(long long, v);
+      const int lo = __builtin_amdgcn_readlane((int)b, l), hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+      return __builtin_bit_cast(WT, (long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+    }
+  };
+  WT wcur = wload(1);
+  float x[D][C];
+#pragma unroll
+  for (int d = 0; d < D; ++d) FA_NL_LOAD(x[d], true);
+  A acc[C];
+  {
+    float x0[C];
+    LC::template load<NT>(row_rsrc(base, bytes), voff, x0);
+    const WT w0 = w[0];
+#pragma unroll
+    for (int c = 0; c < C; ++c) acc[c] = P::mul(w0, x0[c]);
+  }
+  int i = 1;
+  for (; i + 2 * D <= n; i += D) {
+    const WT wnext = wload(i + D);
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      const WT wd = wlane(wcur, d);
+#pragma unroll
+      for (int c = 0; c < C; ++c) acc[c] = add<A>(acc[c], P::mul(wd, x[d][c]));
+      __builtin_amdgcn_sched_barrier(0);
+      FA_NL_LOAD(x[d], false);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    wcur = wnext;
+  }
+  for (; i < n; i += D) {
+    const WT wnext = wload(i + D);
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      const WT wd = wlane(wcur, d);
+      const bool live = i + d < n;
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        const A t = add<A>(acc[c], P::mul(wd, x[d][c]));
+        acc[c] = live ? t : acc[c];
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      FA_NL_LOAD(x[d], true);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    wcur = wnext;
+  }
+#undef FA_NL_LOAD
+  // regroup into quads: lane q takes columns 4q + j = lane (4q + j) / C, element (4q + j) % C
+  typename vec4<A>::type q;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    A v = acc[0];
+#pragma unroll
+    for (int c = 1; c < C; ++c) v = (j % C == c) ? acc[c] : v;
+    q[j] = __shfl(v, (4 * lane + j) / C);
+  }
+  const typename vec4<A>::type accs[1] = {q};
+  finish_piece<T, OP, A, 1, 64, 1>(e, cb / 4, cols, accs);
+}
+
 }  // namespace fa
 
 struct Variant {
@@ -521,6 +653,21 @@ Variant make_narrow(const float* stack, int64_t stride, int n, const float* w, i
           [=] {
             hipLaunchKernelGGL((reduce_kernel_narrow<AccF32, T, OP, D, W, true>), dim3((unsigned)grid),
                                dim3(64 * W), 0, 0, stack, stride, n, w, (int64_t)0, ncols, e);
+          },
+          true, {}};
+}
+
+template <int LB, int D, int OP, typename T>
+Variant make_narrow_lb(const float* stack, int64_t stride, int n, const float* w, int64_t ncols, Epi<T> e,
+                       double bytes) {
+  const int64_t sc = 16 * LB;  // columns per single-wave strip
+  const int64_t grid = (ncols + sc - 1) / sc;
+  char name[96];
+  snprintf(name, sizeof name, "narrow-lb LB%d D%d g%lld", LB, D, (long long)grid);
+  return {name, bytes,
+          [=] {
+            hipLaunchKernelGGL((reduce_kernel_narrow_lb<AccF32, T, OP, LB, D, true>), dim3((unsigned)grid), dim3(64),
+                               0, 0, stack, stride, n, w, (int64_t)0, ncols, e);
           },
           true, {}};
 }
@@ -846,6 +993,22 @@ int main(int argc, char** argv) {
     NARROW(16, 1);
     NARROW(32, 1);
     NARROW(40, 1);
+  }
+#define NARROWLB(LB, D)                                                                                      \
+  vs.push_back(op == FA_OP_AVGM      ? make_narrow_lb<LB, D, FA_OP_AVGM, double>(stack, stride, n, w, ncols, e, bytes)   \
+               : op == FA_OP_ADAGRAD ? make_narrow_lb<LB, D, FA_OP_ADAGRAD, double>(stack, stride, n, w, ncols, e, bytes) \
+                                     : make_narrow_lb<LB, D, FA_OP_MEAN, double>(stack, stride, n, w, ncols, e, bytes))
+  if (!strcmp(set, "nlb")) {  // narrow strips per wave (LB bytes per lane) vs the product's narrow kernel
+    NARROW(40, 1);
+    NARROW(32, 1);
+    NARROWLB(4, 16);
+    NARROWLB(4, 32);
+    NARROWLB(4, 48);
+    NARROWLB(4, 60);
+    NARROWLB(8, 16);
+    NARROWLB(8, 32);
+    NARROWLB(8, 48);
+    NARROWLB(8, 60);
   }
   if (!strcmp(set, "deep2")) {  // the narrow-window kernel: depth, waves per block
     ROWSG(1, 32, 1, 192);
