@@ -576,6 +576,12 @@ class Aggregator:
     devices: the HIP devices the f32 bucket is split over (column shards); each ingests its
     columns through its own PCIe link.  Default: torch's current device only."""
 
+    #: small host rounds (_small_round): the reduce kernel reads the uploads straight from the
+    #: pinned staging and writes the result into pinned host memory (zero-copy over PCIe) instead
+    #: of an H2D copy, the launch and a D2H copy: C1 server call 141 -> 123 us on one box, same
+    #: process, bit-equal (tools/prof_host_c1.py --ab, profiles/r03/c1_zc/); False = copy engines
+    small_zero_copy = True
+
     def __init__(self, device=None, output: str = "reference", workers: int = 8, devices=None, group=None,
                  reorder: bool = False):
         na.lib()  # fail loudly right away if the HIP path is unavailable
@@ -659,7 +665,8 @@ class Aggregator:
         pinned staging, device stack, device weights and result buffers, the native pack table
         and the ctypes arguments of its reduce launch, and the (key, offset, size, shape) list
         of the result.  None (cached as False) when the plan does not qualify."""
-        key = ("small_round", id(self.packer), str(self.device), self.output)
+        zc = bool(self.small_zero_copy)
+        key = ("small_round", id(self.packer), str(self.device), self.output, zc)
         rec = plan.memo.get(key)
         if rec is not None:
             return rec or None
@@ -680,12 +687,16 @@ class Aggregator:
                 plan.memo[key] = False
                 return None
             nat = _NativeRows(pieces, [host], w_local_lst, [None] * n)
-            stack = torch.empty((n, g.stride), dtype=tdt, device=dev)
             nm = g.numerics
             w = self._weights(nm, dev)
             f64 = kind != KIND_F32 or (self.output == "reference" and nm.out_dtype == _F64)
-            dout = torch.empty(g.stride, dtype=torch.float64 if f64 else torch.float32, device=dev)
-            hout = torch.empty(g.stride, dtype=dout.dtype, pin_memory=True)
+            odt = torch.float64 if f64 else torch.float32
+            hout = torch.empty(g.stride, dtype=odt, pin_memory=True)
+            if zc:  # the kernel reads the pinned staging and writes the pinned result over PCIe
+                stack, dout = host, hout
+            else:
+                stack = torch.empty((n, g.stride), dtype=tdt, device=dev)
+                dout = torch.empty(g.stride, dtype=odt, device=dev)
             if kind == KIND_F32:
                 fn = L.fa_reduce_f32
                 args = (stack.data_ptr(), g.stride, n, nm.mode, w.data_ptr(), float(nm.denom), 0, g.stride, None,
@@ -724,6 +735,9 @@ class Aggregator:
         stream = torch.cuda.current_stream(dev)
         sh = stream.cuda_stream
         for nat, host, stack, w, dout, hout, hnp, fn, args, out in kinds:
+            if stack is host:  # zero-copy record
+                na.check(fn(*args, sh), fn.__name__)
+                continue
             stack.copy_(host, non_blocking=True)
             na.check(fn(*args, sh), fn.__name__)
             hout.copy_(dout, non_blocking=True)

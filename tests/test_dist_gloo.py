@@ -4,7 +4,7 @@ reduce_fn is the HIP kernel; here the C oracle stands in as the per-shard reduce
 checks the sharding + exchange logic: the reassembled model must equal the unsharded reduce
 bit for bit."""
 import os
-import socket
+import tempfile
 
 import numpy as np
 import pytest
@@ -16,16 +16,15 @@ SEED = 77
 
 
 def _free_port():
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
+    """A fresh file:// rendezvous (no TCP port to race for when test workers run in parallel)."""
+    return "file://" + os.path.join(tempfile.mkdtemp(prefix="fa_gloo_"), "pg")
 
 
 def _worker(rank, world, port, n, p, stripes, op, weights=None):
     import oracle
     from flearn_amd.dist import ShardedReducer, ShardPlan
 
-    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method=port, rank=rank, world_size=world)
     try:
         if weights == "model":  # bench's default: widths from the two-stage pipeline model
             from flearn_amd.dist import StripeModel, plan_stripes
@@ -95,7 +94,7 @@ def _gather_worker(rank, world, port, stride, dtype):
     from flearn_amd.bucket import rank_width
     from flearn_amd.dist import gather_columns
 
-    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method=port, rank=rank, world_size=world)
     try:
         w = rank_width(stride, world)
         assert w % 64 == 0 and w * world >= stride

@@ -1046,15 +1046,20 @@ def test_float64_model_with_int64_counters(weights, cuda):
     assert_dict_bitwise(got, want, f"f64 model, weights {type(weights[0]).__name__}")
 
 
-def test_small_round_fast_path_reuses_its_record_safely(cuda):
+@pytest.mark.parametrize("zero_copy", [False, True])
+def test_small_round_fast_path_reuses_its_record_safely(zero_copy, cuda, monkeypatch):
     """Small host rounds (every bucket < 4 MiB: flearn's config 1) take Aggregator._small_round:
-    natively packed pinned staging, one H2D / launch / D2H per bucket, one sync.  Round after round
-    with new values (the record's staging reused) and with a value the native pack refuses (a
-    non-contiguous view: the general path takes over) every result is bit-equal to the oracle."""
+    natively packed pinned staging, one H2D / launch / D2H per bucket (or, zero-copy, the kernel
+    reading the pinned staging and writing the pinned result over PCIe), one sync.  Round after
+    round with new values (the record's staging reused) and with a value the native pack refuses
+    (a non-contiguous view: the general path takes over) every result is bit-equal to the oracle."""
+    from flearn_amd.aggregator import Aggregator
+
+    monkeypatch.setattr(Aggregator, "small_zero_copy", zero_copy)
     layout = layouts.get("lenet5")
     p = layouts.fp32_elems(layout)
     s = AVG()
-    for r in range(4):
+    for r in range(6):
         flat = oracle.fill_uniform(10, p, seed=40 + r)
         clients = [layouts.synthetic_state_dict(layout, flat[i]) for i in range(10)]
         if r == 2:  # a Fortran-ordered copy: same shape and dtype, not C-contiguous
@@ -1064,5 +1069,6 @@ def test_small_round_fast_path_reuses_its_record_safely(cuda):
         got = s.server(upload(clients, weights), r)["w_glob"]
         want = oracle.server_ensemble(weights, [{k: v.copy() for k, v in c.items()} for c in clients])
         assert_dict_bitwise(got, want, f"round {r}")
-        rec = s.engine.last_plan.memo.get(("small_round", id(s.engine.packer), str(s.engine.device), "reference"))
+        rec = s.engine.last_plan.memo.get(("small_round", id(s.engine.packer), str(s.engine.device), "reference",
+                                           zero_copy))
         assert rec, "the small-round record was not built"
