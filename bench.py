@@ -29,7 +29,11 @@ Multi-GPU (element-range column shards + RCCL all-gather, flearn_amd/dist.py):
                    model whose coefficients are fitted on the running job (reduce of the whole
                    and 1/8 of the local width, RCCL all-gather of both; max over ranks): the
                    "multi_gpu" field reports the widths, the model, its prediction, the measured
-                   per-rank reduce time and the exposed gather time; --stripes K fixes K stripes
+                   per-rank reduce time and the exposed gather time; --stripes K fixes K stripes.
+                   The plan may end in a replicated tail (flearn_amd.dist.plan_shards): the last
+                   columns are reduced by EVERY rank instead of gathered — redundant HBM reads
+                   traded for xGMI bytes where the gather sets the step (G = 2, 4: one link per
+                   peer); `value` counts every column once ("replicated_cols" in "multi_gpu")
   --emulate-world G  one GPU runs rank 0's share of a G-GPU job (no collective): the per-rank
                    reduce of the multi-GPU runs, measurable on a single-GPU box
 Prints ONE JSON line on rank 0 (stdout); progress goes to stderr.
@@ -55,7 +59,7 @@ from flearn_amd import _native as na  # noqa: E402
 from flearn_amd import aggregator as agg  # noqa: E402
 from flearn_amd import launch, layouts  # noqa: E402
 from flearn_amd.dist import (ALIGN, PingPong, ShardedReducer, ShardPlan, StripeModel,  # noqa: E402
-                             all_gather_into, hip_reduce_fn, plan_stripes)
+                             all_gather_into, hip_reduce_fn, plan_shards)
 
 METRIC = "device-resident GiB/s, FedAVG N-client weighted tensor reduce; %HBM peak"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
@@ -146,24 +150,22 @@ class Job:
 
     def __init__(self, cfg, layout, n, plan, dev, world, reorder):
         self.cfg, self.n, self.plan, self.dev = cfg, n, plan, dev
-        cols = plan.local_cols
-        log(f"[rank {plan.rank}] alloc {n} x {cols} fp32 = {n * cols * 4 / 1e9:.2f} GB, stripes {plan.widths}")
-        self.stack = torch.empty((n, cols), dtype=torch.float32, device=dev)
-        for c in range(plan.stripes):
-            lo = plan.local_begin(c)
-            agg.fill_uniform(self.stack[:, lo:], seed=2024, row_begin=0, col_begin=plan.global_begin(c),
-                             n_cols=plan.shard_of(c))
+        cols, stride = plan.local_cols, plan.local_stride
+        log(f"[rank {plan.rank}] alloc {n} x {cols} fp32 = {n * cols * 4 / 1e9:.2f} GB, stripes {plan.widths}"
+            + (f" + replicated tail {plan.rep}" if plan.rep else ""))
+        self.stack = torch.empty((n, stride), dtype=torch.float32, device=dev)
+        for lo, g0, width in plan.segments():
+            agg.fill_uniform(self.stack[:, lo:], seed=2024, row_begin=0, col_begin=g0, n_cols=width)
         self.weights = torch.ones(n, dtype=torch.float32, device=dev)  # Python 1.0 -> fl32(1.0)
         denom = float(np.sum([1.0] * n))  # np.sum(agg_weight_lst), strategy.py:127
         epi, state = {}, None
         if cfg["op"] != "mean":
-            prev = torch.empty((1, cols), dtype=torch.float32, device=dev)
-            for c in range(plan.stripes):
-                lo = plan.local_begin(c)
-                agg.fill_uniform(prev[:, lo:], seed=1, col_begin=plan.global_begin(c), n_cols=plan.shard_of(c))
+            prev = torch.empty((1, stride), dtype=torch.float32, device=dev)
+            for lo, g0, width in plan.segments():
+                agg.fill_uniform(prev[:, lo:], seed=1, col_begin=g0, n_cols=width)
             # the fused step reads (prev, v_t) and writes the new global model and v_t into a
             # second pair, swapped every step — as the product's ServerOptimizer does
-            state = PingPong(prev[0], torch.zeros(cols, dtype=torch.float64, device=dev))
+            state = PingPong(prev[0], torch.zeros(stride, dtype=torch.float64, device=dev))
             epi = dict(op=na.OP_BY_NAME[cfg["op"]], state=state)
         self.fn = hip_reduce_fn(self.stack, self.weights, na.MODE_W32_DIV64, denom, reorder=reorder, **epi)
         self.red = ShardedReducer(plan, self.fn, dev, gather=world > 1, state=state)
@@ -173,11 +175,9 @@ class Job:
         torch.cuda.empty_cache()
 
     def reduce_only(self):
-        """The reduce launches of one step (every stripe), no collective."""
-        p = self.plan
-        for c in range(p.stripes):
-            lo, sc = p.local_begin(c), p.shard_of(c)
-            self.fn(lo, sc, self.red.local_out[lo : lo + sc])
+        """The reduce launches of one step (every stripe and the replicated tail), no collective."""
+        for lo, _, width in self.plan.segments():
+            self.fn(lo, width, self.red.local_out[lo : lo + width])
 
 
 def _event_time(fn, reps: int) -> float:
@@ -248,15 +248,18 @@ def run_job(cfg, layout, n, args, world, rank, dev, g_eff):
             probe.reduce_only()
         model, cal = calibrate(probe, world, dev)
         probe.release()
-        widths = plan_stripes(-(-p_real // g_eff), model)
-        plan = ShardPlan.from_widths(p_real, g_eff, rank, widths)
-        pred, red_s, exposed = model.makespan(plan.widths)
-        info.update(stripe_choice="model (flearn_amd.dist.plan_stripes), coefficients fitted on this job",
+        widths, rep = plan_shards(p_real, g_eff, model)
+        plan = ShardPlan.from_widths(p_real, g_eff, rank, widths, rep=rep)
+        pred, red_s, exposed = model.makespan(plan.widths, plan.rep)
+        info.update(stripe_choice="model (flearn_amd.dist.plan_shards: stripes + replicated tail), coefficients "
+                                  "fitted on this job",
                     model={"a_r_us": round(model.a_r * 1e6, 3), "b_r_ns_per_col": round(model.b_r * 1e9, 5),
                            "a_g_us": round(model.a_g * 1e6, 3), "b_g_ns_per_col": round(model.b_g * 1e9, 5)},
                     calibration=cal, predicted_ms=round(pred * 1e3, 4),
                     predicted_exposed_gather_ms=round(exposed * 1e3, 4))
     info["stripe_widths"] = list(plan.widths)
+    # columns every rank reduces itself (no gather): redundant work, counted once in `value`
+    info["replicated_cols"] = plan.rep
     job = Job(cfg, layout, n, plan, dev, world, args.reorder)
     for _ in range(args.warmup):
         job.red.step()
@@ -417,7 +420,9 @@ def main():
                 "parallelism": ("single GPU" if g_eff == 1 else
                                 f"element-range shards x{g_eff} + RCCL all-gather ({job.plan.stripes} stripes"
                                 + (f", widths {'/'.join(str(x) for x in job.plan.widths)}" if job.plan.stripes > 1
-                                   else "") + ")"
+                                   else "")
+                                + (f"; the last {job.plan.rep} columns reduced by every rank, not gathered"
+                                   if job.plan.rep else "") + ")"
                                 + (f"; EMULATED: rank 0's reduce of a {emu}-GPU job on one GPU, no gather"
                                    if emu else "")),
                 "hbm_peak_frac_of_value": round(value * GIB / 1e9 / HBM_PEAK_GBS, 4),

@@ -352,6 +352,11 @@ class ServerOptimizer:
         self.state[sh.index], self.spare[sh.index] = spare, (prev, v)
         return prev, v, spare[0], spare[1]
 
+    def unswap(self, sh):
+        """Undo swap_buffers(sh) when the fused step it was for did not run (the state keeps the
+        pair it had: the spare buffers hold nothing yet)."""
+        self.state[sh.index], self.spare[sh.index] = self.spare[sh.index], self.state[sh.index]
+
     def v_t(self, plan: BucketPlan) -> dict:
         """The state as the reference exposes it (self.v_t dict of arrays).  With a column-sharded
         process group (Aggregator(group=...)) every rank holds only its columns: this is then a
@@ -714,8 +719,9 @@ class Aggregator:
     def _small_round(self, plan: BucketPlan, w_local_lst):
         """One small host round with no per-key Python: the uploads are packed natively into the
         record's pinned staging (every value checked against the plan: C-contiguous, dtype, byte
-        size), each bucket is one H2D, one reduce launch and one D2H on torch's current stream,
-        one synchronisation, and the result is handed out as views of one fresh array per bucket
+        size), each bucket is one reduce launch reading that staging and writing a pinned result
+        over PCIe (zero-copy; with small_zero_copy False: one H2D, the launch and one D2H) on
+        torch's current stream, one synchronisation, and the result is handed out as views of one fresh array per bucket
         (numpy scalars for 0-d keys) — what Packer.unpack returns.  Returns None (nothing queued)
         when a value does not fit the record; the caller then takes the general path."""
         rec = self._small_record(plan, w_local_lst)
@@ -796,9 +802,13 @@ class Aggregator:
             # fused: fl32(w) becomes the next round's prev (the model clients load), v_t advances;
             # both into the spare pair, which then becomes the state (double-buffered)
             prev, v, prev_o, v_o = server_opt.swap_buffers(sh)
-            reduce_stack(stack, w, nm.mode, nm.denom, out32=prev_o, out64=out64, op=server_opt.op, prev=prev, v=v,
-                         v_out=v_o, beta=server_opt.beta, eta=server_opt.eta, tau=server_opt.tau,
-                         beta2=server_opt.beta2, reorder=self.reorder and not isinstance(stack, RowTable))
+            try:
+                reduce_stack(stack, w, nm.mode, nm.denom, out32=prev_o, out64=out64, op=server_opt.op, prev=prev,
+                             v=v, v_out=v_o, beta=server_opt.beta, eta=server_opt.eta, tau=server_opt.tau,
+                             beta2=server_opt.beta2, reorder=self.reorder and not isinstance(stack, RowTable))
+            except BaseException:
+                server_opt.unswap(sh)  # a refused launch must not leave the state on the empty spare pair
+                raise
             return out64 if want64 else prev_o
         out32 = None
         if not want64 or server_opt is not None:

@@ -13,14 +13,22 @@ Column layout (block-cyclic, `stripes` stripes of per-rank widths S_c, multiples
     rank r's local stack is [N, sum S_c]: local column O_c + j <-> global W*O_c + r*S_c + j
 so the all-gather of stripe c writes one contiguous range of the global bucket, and stripe c's
 gather (on RCCL's stream) overlaps the reduce of stripe c+1 (on the compute stream).
+Optionally the plan ends in a REPLICATED tail of `rep` columns, [W*sum(S), W*sum(S) + rep) =
+[n_cols - rep, n_cols): every rank holds those columns of all N clients and reduces them itself,
+after its stripes, while the last gathers are in flight — redundant compute instead of
+communication, worth it where the all-gather, not the reduce, sets the step (few GPUs, one xGMI
+link per peer: at G = 2 every GPU receives half the model over ONE link).  The rank's local
+columns are then [stripes..., tail]; the tail's results are written straight into the global
+bucket (bit-identical on every rank: same data, same kernel, same order).
 Optimizer state (prev, v_t) is sharded the same way and never communicated.
 
-The stripe widths come from a two-stage pipeline model (`StripeModel`, `plan_stripes`): stripe
-c's reduce costs a_r + b_r*S_c on the compute stream, its gather a_g + b_g*S_c on RCCL's, a
-gather starts when its stripe is reduced and the previous gather is done; the plan with the
-smallest simulated makespan over stripe counts and geometric width ratios wins.  bench.py fits
-the four coefficients on the running job (one full-width and one narrow launch of each) before
-it plans, so the schedule follows the node's measured HBM and xGMI rates.
+The stripe widths come from a two-stage pipeline model (`StripeModel`, `plan_stripes`,
+`plan_shards`): stripe c's reduce costs a_r + b_r*S_c on the compute stream, its gather
+a_g + b_g*S_c on RCCL's, a gather starts when its stripe is reduced and the previous gather is
+done, the replicated tail's reduce follows the last stripe's; the plan with the smallest simulated
+makespan over tail sizes, stripe counts and geometric width ratios wins.  bench.py fits the four
+coefficients on the running job (one full-width and one narrow launch of each) before it plans,
+so the schedule follows the node's measured HBM and xGMI rates.
 
 The same code runs on the gloo backend (CPU tests, and two processes sharing one GPU on a
 1-GPU box, where RCCL refuses two ranks on one device): device tensors are then staged through
@@ -65,13 +73,15 @@ class StripeModel:
     b_g: float
 
     @staticmethod
-    def assumed(n_clients: int, world: int, hbm_bytes_s: float = 7.0e12, ingress_bytes_s: float = 300e9,
+    def assumed(n_clients: int, world: int, hbm_bytes_s: float = 7.0e12, link_bytes_s: float = 50e9,
                 launch_s: float = 10e-6, collective_s: float = 30e-6) -> "StripeModel":
         """A priori coefficients: the reduce streams N*4 B per column at the measured 1-GPU rate
-        (~7 TB/s); an all-gather brings (world-1)*4 B per column into each GPU at the
-        assumed xGMI ingress rate.  bench.py replaces them with measured ones."""
+        (~7 TB/s); an all-gather brings (world-1)*4 B per column into each GPU over
+        its world-1 xGMI links (one per peer on an MI355X node) at an assumed per-link rate.
+        bench.py replaces them with measured ones."""
+        ingress = max(world - 1, 1) * link_bytes_s
         return StripeModel(launch_s, n_clients * 4.0 / hbm_bytes_s, collective_s,
-                           max(world - 1, 0) * 4.0 / ingress_bytes_s)
+                           max(world - 1, 0) * 4.0 / ingress)
 
     @staticmethod
     def fit(w_big: int, w_small: int, r_big: float, r_small: float, g_big: float, g_small: float) -> "StripeModel":
@@ -84,22 +94,27 @@ class StripeModel:
         a_g, b_g = line(g_big, g_small)
         return StripeModel(a_r, b_r, a_g, b_g)
 
-    def makespan(self, widths) -> tuple:
-        """(step time, reduce-stream busy time, exposed gather time) of a stripe plan."""
+    def makespan(self, widths, rep: int = 0) -> tuple:
+        """(step time, reduce-stream busy time, exposed gather time) of a stripe plan; `rep`
+        replicated columns are reduced after the stripes, with no gather."""
         t_red = t_gat = 0.0
         for w in widths:
             t_red += self.a_r + self.b_r * w
             t_gat = max(t_red, t_gat) + self.a_g + self.b_g * w
-        return t_gat, t_red, t_gat - t_red
+        if rep:
+            t_red += self.a_r + self.b_r * rep
+        step = max(t_gat, t_red)
+        return step, t_red, step - t_red
 
 
-def plan_stripes(local_cols: int, model: StripeModel, max_stripes: int = 8) -> tuple:
-    """Stripe widths (multiples of ALIGN summing to >= local_cols) minimising the model's makespan.
+def plan_stripes(local_cols: int, model: StripeModel, max_stripes: int = 8, rep: int = 0) -> tuple:
+    """Stripe widths (multiples of ALIGN summing to >= local_cols) minimising the model's makespan
+    (followed by `rep` replicated columns).
     Candidates: k = 1..max_stripes stripes with geometric widths S_c ~ q**c for q on a grid
     (q < 1: big stripes first, the usual choice when the reduce dominates; q > 1: a small first
     stripe so the gathers start early, when the collective dominates)."""
     units = max(1, -(-local_cols // ALIGN))
-    best = ((units * ALIGN,), model.makespan((units * ALIGN,))[0])
+    best = ((units * ALIGN,), model.makespan((units * ALIGN,), rep)[0])
     for k in range(2, min(max_stripes, units) + 1):
         for q in (0.125, 0.25, 0.35, 0.5, 0.6, 0.7, 0.8, 0.9, 1.0, 1.15, 1.3, 1.5, 2.0, 3.0, 4.0):
             raw = [q**c for c in range(k)]
@@ -109,10 +124,40 @@ def plan_stripes(local_cols: int, model: StripeModel, max_stripes: int = 8) -> t
             if min(u) < 1:
                 continue
             widths = tuple(x * ALIGN for x in u)
-            t = model.makespan(widths)[0]
+            t = model.makespan(widths, rep)[0]
             if t < best[1] - 1e-12:
                 best = (widths, t)
     return best[0]
+
+
+#: replicated-tail sizes plan_shards tries, as fractions of the bucket
+REP_FRACTIONS = (0.0, 0.01, 0.02, 0.03, 0.05, 0.075, 0.1, 0.125, 0.15, 0.175, 0.2, 0.25, 0.3, 0.35, 0.4,
+                 0.45, 0.5, 0.55, 0.6)
+
+
+def plan_shards(n_cols: int, world: int, model: StripeModel, max_stripes: int = 8,
+                fractions=REP_FRACTIONS) -> tuple:
+    """(stripe widths, replicated tail columns) minimising the model's makespan for an n_cols
+    bucket on `world` ranks: the padded plan with no tail, against plans whose stripes cover
+    exactly world*sum(widths) = n_cols - rep columns and whose last `rep` columns every rank
+    reduces itself (ShardPlan.rep).  A tail pays where the gather dominates: each replicated
+    column costs every rank one column of reduce and saves (world-1)/world of a column of
+    gather ingress."""
+    lc = -(-max(n_cols, 1) // max(world, 1))
+    w0 = plan_stripes(lc, model, max_stripes)
+    best = (w0, 0, model.makespan(w0)[0])
+    if world < 2:
+        return best[0], 0
+    for f in fractions:
+        units = int(n_cols * (1.0 - f)) // (world * ALIGN)
+        rep = n_cols - world * units * ALIGN
+        if units < 1 or rep <= 0:
+            continue
+        w = plan_stripes(units * ALIGN, model, max_stripes, rep=rep)
+        t = model.makespan(w, rep)[0]
+        if t < best[2] - 1e-12:
+            best = (w, rep, t)
+    return best[0], best[1]
 
 
 @dataclass(frozen=True)
@@ -121,6 +166,7 @@ class ShardPlan:
     world: int
     rank: int
     widths: tuple  # S_c: columns per (stripe c, rank) slice, each a multiple of ALIGN
+    rep: int = 0  # replicated tail: global columns [n_cols - rep, n_cols), reduced by every rank
 
     @staticmethod
     def make(n_cols: int, world: int, rank: int, stripes: int = 4, weights=None) -> "ShardPlan":
@@ -149,16 +195,21 @@ class ShardPlan:
         return ShardPlan(n_cols, world, rank, tuple(widths))
 
     @staticmethod
-    def from_widths(n_cols: int, world: int, rank: int, widths) -> "ShardPlan":
-        """A plan with explicit per-rank stripe widths (e.g. from plan_stripes)."""
+    def from_widths(n_cols: int, world: int, rank: int, widths, rep: int = 0) -> "ShardPlan":
+        """A plan with explicit per-rank stripe widths (e.g. from plan_stripes / plan_shards);
+        rep > 0: the stripes cover exactly the first n_cols - rep columns (no padding) and every
+        rank reduces the last rep itself."""
         widths = tuple(int(w) for w in widths)
+        rep = int(rep)
         if not widths or any(w <= 0 or w % ALIGN for w in widths):
             raise ValueError("stripe widths must be positive multiples of ALIGN")
-        if world * sum(widths) < n_cols:
+        if rep < 0 or (rep and world * sum(widths) + rep != n_cols):
+            raise ValueError("a replicated tail needs stripes covering exactly n_cols - rep columns")
+        if world * sum(widths) + rep < n_cols:
             raise ValueError("stripes do not cover the bucket")
         if world < 1 or not 0 <= rank < world:
             raise ValueError("bad world / rank")
-        return ShardPlan(n_cols, world, rank, widths)
+        return ShardPlan(n_cols, world, rank, widths, rep)
 
     @property
     def stripes(self) -> int:
@@ -176,11 +227,36 @@ class ShardPlan:
 
     @property
     def padded(self) -> int:
+        """Global columns the stripes cover (the gathered range; padding included when rep == 0)."""
         return self.world * sum(self.widths)
 
     @property
-    def local_cols(self) -> int:
+    def full_cols(self) -> int:
+        """Columns of the reassembled bucket: the gathered range and the replicated tail."""
+        return self.padded + self.rep
+
+    @property
+    def local_stripes(self) -> int:
+        """Local columns of the stripes (the tail's local columns follow them)."""
         return sum(self.widths)
+
+    @property
+    def local_cols(self) -> int:
+        return sum(self.widths) + self.rep
+
+    @property
+    def local_stride(self) -> int:
+        """Row stride of the rank's local stack and state (local_cols rounded up to ALIGN, so
+        every row stays 16-B aligned whatever the tail's width)."""
+        return -(-self.local_cols // ALIGN) * ALIGN
+
+    def segments(self):
+        """(local begin, global begin, width) of every local column range: the stripes, then the
+        replicated tail."""
+        out = [(self.local_begin(c), self.global_begin(c), self.widths[c]) for c in range(self.stripes)]
+        if self.rep:
+            out.append((self.local_stripes, self.padded, self.rep))
+        return out
 
     def local_begin(self, stripe: int) -> int:
         return sum(self.widths[:stripe])
@@ -190,10 +266,9 @@ class ShardPlan:
         return self.world * self.local_begin(stripe) + r * self.widths[stripe]
 
     def local_to_global(self, local_col: int) -> int:
-        for c in range(self.stripes):
-            lo = self.local_begin(c)
-            if local_col < lo + self.widths[c]:
-                return self.global_begin(c) + (local_col - lo)
+        for lo, g0, w in self.segments():
+            if lo <= local_col < lo + w:
+                return g0 + (local_col - lo)
         raise IndexError(local_col)
 
     def real_cols_in_slice(self, stripe: int, rank: int | None = None) -> int:
@@ -247,10 +322,13 @@ class ShardedReducer:
         # local_out may alias the sharded `prev` of a fused optimizer updated in place
         self.state = state
         self._local_out = (None if state is not None else
-                           torch.empty(plan.local_cols, dtype=torch.float32, device=self.device)
+                           torch.empty(plan.local_stride, dtype=torch.float32, device=self.device)
                            if local_out is None else local_out)
+        # the replicated tail goes straight into the global bucket unless its local results are
+        # state (a fused optimizer's next prev): then it is reduced locally and copied across
+        self._tail_direct = state is None and local_out is None
         # one rank: local columns ARE the global columns, nothing to reassemble
-        self.full = (torch.empty(plan.padded, dtype=torch.float32, device=self.device) if self.gather
+        self.full = (torch.empty(plan.full_cols, dtype=torch.float32, device=self.device) if self.gather
                      else None)
 
     @property
@@ -271,6 +349,14 @@ class ShardedReducer:
                 w = all_gather_into(dst, out[lo : lo + sc], group=self.group, async_op=True)
                 if w is not None:
                     works.append(w)
+        if p.rep:  # the replicated tail, while the last gathers are in flight
+            lo, g0 = p.local_stripes, p.padded
+            if self.gather and self._tail_direct:
+                self.reduce_fn(lo, p.rep, self.full[g0 : g0 + p.rep])
+            else:
+                self.reduce_fn(lo, p.rep, out[lo : lo + p.rep])
+                if self.gather:
+                    self.full[g0 : g0 + p.rep].copy_(out[lo : lo + p.rep])
         if self.state is not None:
             self.state.flip()
         for w in works:

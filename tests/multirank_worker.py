@@ -191,31 +191,32 @@ def case_sharded_reducer(rank, world):
     import oracle
     from flearn_amd import _native as na
     from flearn_amd import aggregator as agg
-    from flearn_amd.dist import ShardedReducer, ShardPlan, StripeModel, hip_reduce_fn, plan_stripes
+    from flearn_amd.dist import ShardedReducer, ShardPlan, StripeModel, hip_reduce_fn, plan_shards, plan_stripes
 
     cuda = torch.device("cuda", 0)
     n, p = 9, 700_001
     lc = -(-p // world)
+    widths, rep = plan_shards(p, world, StripeModel(1e-6, 2e-9, 2e-6, 1e-8))  # gather-bound: a replicated tail
+    assert rep > 0
     plans = [ShardPlan.make(p, world, rank, 1), ShardPlan.make(p, world, rank, 2, weights=(3, 1)),
-             ShardPlan.from_widths(p, world, rank, plan_stripes(lc, StripeModel.assumed(n, world)))]
+             ShardPlan.from_widths(p, world, rank, plan_stripes(lc, StripeModel.assumed(n, world))),
+             ShardPlan.from_widths(p, world, rank, widths, rep=rep)]
     w_h = np.linspace(0.5, 1.5, n).astype(np.float32)
     denom = float(np.sum([float(x) for x in w_h]))
     want_mean = oracle.c_reduce(oracle.MODE_W32_DIV64, oracle.fill_uniform(n, p, 3), w_h, denom)
     for plan in plans:
         for op in ("mean", "avgm", "adagrad"):
-            stack = torch.empty((n, plan.local_cols), dtype=torch.float32, device=cuda)
-            for c in range(plan.stripes):
-                agg.fill_uniform(stack[:, plan.local_begin(c):], seed=3, col_begin=plan.global_begin(c),
-                                 n_cols=plan.shard_of(c))
+            stack = torch.empty((n, plan.local_stride), dtype=torch.float32, device=cuda)
+            for lo, g0, width in plan.segments():
+                agg.fill_uniform(stack[:, lo:], seed=3, col_begin=g0, n_cols=width)
             w = torch.from_numpy(w_h).to(cuda)
             epi, local_out = {}, None
             if op != "mean":
-                prev = torch.empty((1, plan.local_cols), dtype=torch.float32, device=cuda)
-                for c in range(plan.stripes):
-                    agg.fill_uniform(prev[:, plan.local_begin(c):], seed=4, col_begin=plan.global_begin(c),
-                                     n_cols=plan.shard_of(c))
+                prev = torch.empty((1, plan.local_stride), dtype=torch.float32, device=cuda)
+                for lo, g0, width in plan.segments():
+                    agg.fill_uniform(prev[:, lo:], seed=4, col_begin=g0, n_cols=width)
                 epi = dict(op=na.OP_BY_NAME[op], prev=prev[0],
-                           v=torch.zeros(plan.local_cols, dtype=torch.float64, device=cuda))
+                           v=torch.zeros(plan.local_stride, dtype=torch.float64, device=cuda))
                 local_out = prev[0]
             red = ShardedReducer(plan, hip_reduce_fn(stack, w, na.MODE_W32_DIV64, denom, **epi), cuda,
                                  local_out=local_out, gather=True)

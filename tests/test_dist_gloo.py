@@ -32,15 +32,21 @@ def _worker(rank, world, port, n, p, stripes, op, weights=None):
             model = StripeModel(1e-6, 5e-9, 2e-6, 1e-8)  # gather-bound: small stripes first
             plan = ShardPlan.from_widths(p, world, rank, plan_stripes(-(-p // world), model))
             assert plan.stripes == stripes and plan.widths[0] < plan.widths[-1], plan.widths
+        elif weights == "tail":  # model-planned stripes + a replicated tail (plan_shards)
+            from flearn_amd.dist import StripeModel, plan_shards
+
+            widths, rep = plan_shards(p, world, StripeModel(1e-6, 2e-9, 2e-6, 1e-8))
+            plan = ShardPlan.from_widths(p, world, rank, widths, rep=rep)
+            assert plan.rep > 0 and plan.full_cols == p, (plan.widths, plan.rep)
         else:
             plan = ShardPlan.make(p, world, rank, stripes, weights=weights)
         local = np.zeros((n, plan.local_cols), np.float32)
         prev = np.zeros(plan.local_cols, np.float32)
-        for c in range(stripes):
-            lo, width = plan.local_begin(c), plan.real_cols_in_slice(c)
+        for lo, g0, width in plan.segments():
+            width = max(0, min(width, p - g0))  # the last slices may be padding
             if width:
-                local[:, lo : lo + width] = oracle.fill_uniform(n, width, SEED, col0=plan.global_begin(c))
-                prev[lo : lo + width] = oracle.fill_uniform(1, width, 1, col0=plan.global_begin(c))[0]
+                local[:, lo : lo + width] = oracle.fill_uniform(n, width, SEED, col0=g0)
+                prev[lo : lo + width] = oracle.fill_uniform(1, width, 1, col0=g0)[0]
         w = np.linspace(0.5, 1.5, n).astype(np.float32)
         denom = float(np.sum([float(x) for x in w]))
         v = np.zeros(plan.local_cols)
@@ -73,6 +79,15 @@ def _worker(rank, world, port, n, p, stripes, op, weights=None):
 def test_sharded_reduce_two_ranks(p, stripes, op, weights):
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     mp.spawn(_worker, args=(2, _free_port(), 7, p, stripes, op, weights), nprocs=2, join=True)
+
+
+@pytest.mark.parametrize("world,op", [(2, "mean"), (2, "avgm"), (4, "adagrad"), (8, "mean")])
+def test_sharded_reduce_replicated_tail(world, op):
+    """Stripes + a replicated tail (plan_shards on a gather-bound model): every rank reduces the
+    last columns itself — straight into the global bucket for the plain mean, through its local
+    state for a fused optimizer — and the reassembled model is still the unsharded reduce."""
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    mp.spawn(_worker, args=(world, _free_port(), 5, 90_001, None, op, "tail"), nprocs=world, join=True)
 
 
 def test_sharded_reduce_four_ranks():

@@ -97,6 +97,34 @@ def test_server_side_fused_optimizer_matches_reference(name, cuda):
         assert_dict_bitwise(v, g.output(f"v{r}"), f"{name} v{r}")
 
 
+def test_fused_round_refused_keeps_optimizer_state(cuda, monkeypatch):
+    """A fused step whose launch is refused (here: reduce_stack raising before it queues anything)
+    leaves the double-buffered state on the pair it had, so the rounds after it still match the
+    reference (ServerOptimizer.swap_buffers / unswap)."""
+    from flearn_amd import aggregator
+
+    name = next(n for n in ROUND_CASES if Golden(n).meta["op"] == "avgm")
+    g = Golden(name)
+    s = AVGM(server_side=True)
+    s.server_opt.init_global({k[6:]: v for k, v in g.arrays.items() if k.startswith("prev0:")})
+    real = aggregator.reduce_stack
+    for r in range(g.meta["rounds"]):
+        clients, weights = _round_inputs(g, r)
+        if r == 1:  # one refused attempt of round 1 first
+            def refuse(*a, **k):
+                if k.get("v_out") is not None:
+                    raise ValueError("refused launch")
+                return real(*a, **k)
+
+            monkeypatch.setattr(aggregator, "reduce_stack", refuse)
+            with pytest.raises(SystemExit):  # client/config data errors take server_exception
+                s.server(upload(clients, weights), r)
+            monkeypatch.setattr(aggregator, "reduce_stack", real)
+        got = s.server(upload(clients, weights), r)["w_glob"]
+        assert_dict_bitwise(got, g.output(f"w{r}"), f"{name} w{r}")
+        assert_dict_bitwise(s.server_opt.v_t(s.engine.last_plan), g.output(f"v{r}"), f"{name} v{r}")
+
+
 @pytest.mark.parametrize("name", ROUND_CASES)
 def test_client_side_update_matches_reference(name, cuda):
     """AVGM.mean_momentum / OPT.adaptive_opt on the GPU (the reference's client_receive math)."""

@@ -2,7 +2,7 @@
 pipeline model behind bench.py's stripe choice, and the plans it produces."""
 import pytest
 
-from flearn_amd.dist import ALIGN, ShardPlan, StripeModel, plan_stripes
+from flearn_amd.dist import ALIGN, ShardPlan, StripeModel, plan_shards, plan_stripes
 
 
 def test_makespan_two_stage_pipeline():
@@ -59,3 +59,51 @@ def test_from_widths_layout():
         ShardPlan.from_widths(1000, 4, 0, (64, 100))
     with pytest.raises(ValueError):
         ShardPlan.from_widths(10_000, 4, 0, (64, 64))
+
+
+def test_makespan_with_replicated_tail():
+    m = StripeModel(a_r=0.0, b_r=1.0, a_g=0.0, b_g=2.0)
+    # stripe 0 reduced at 64, gathered 64..192; the tail's reduce (64..128) hides under it
+    assert m.makespan((64,), rep=64) == (192.0, 128.0, 64.0)
+    # a long tail: the step ends with the reduce, nothing exposed
+    assert m.makespan((64,), rep=256) == (320.0, 320.0, 0.0)
+
+
+@pytest.mark.parametrize("n_cols", [44_426, 11_699_112, 25_610_152])
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_plan_shards_covers_exactly(n_cols, world):
+    for model in (StripeModel.assumed(100, world), StripeModel.assumed(1000, world),
+                  StripeModel(10e-6, 100 * 4 / 7e12, 0.0, 0.0)):
+        widths, rep = plan_shards(n_cols, world, model)
+        plan = ShardPlan.from_widths(n_cols, world, world - 1, widths, rep=rep)
+        if rep:
+            assert plan.full_cols == n_cols and world * sum(widths) + rep == n_cols
+        else:
+            assert plan.padded >= n_cols
+        t = model.makespan(widths, rep)[0]
+        w0 = plan_stripes(-(-n_cols // world), model)
+        assert t <= model.makespan(w0)[0] + 1e-15  # never worse than the padded plan
+
+
+def test_plan_shards_replicates_only_when_the_gather_dominates():
+    p = 25_610_152  # NS
+    # G = 2, one xGMI link: the gather of half the model takes longer than the reduce of it
+    widths, rep = plan_shards(p, 2, StripeModel.assumed(100, 2))
+    assert rep > 0.05 * p
+    m = StripeModel.assumed(100, 2)
+    assert m.makespan(widths, rep)[0] < 0.85 * m.makespan(plan_stripes(-(-p // 2), m))[0]
+    # reduce-bound (1000 clients) or no collective: no replicated work beyond the alignment tail
+    for m in (StripeModel.assumed(1000, 8), StripeModel(10e-6, 100 * 4 / 7e12, 0.0, 0.0)):
+        assert plan_shards(11_699_112, 8, m)[1] < 8 * ALIGN
+
+
+def test_replicated_tail_layout():
+    plan = ShardPlan.from_widths(4 * 192 + 100, 4, 2, (128, 64), rep=100)
+    assert plan.local_cols == 292 and plan.local_stripes == 192 and plan.full_cols == 868
+    assert plan.segments() == [(0, 256, 128), (128, 4 * 128 + 128, 64), (192, 768, 100)]
+    assert plan.local_to_global(191) == 4 * 128 + 128 + 63 and plan.local_to_global(192) == 768
+    assert plan.local_to_global(291) == 867
+    with pytest.raises(IndexError):
+        plan.local_to_global(292)
+    with pytest.raises(ValueError):  # the stripes must end exactly where the tail starts
+        ShardPlan.from_widths(4 * 192 + 100, 4, 0, (128, 128), rep=100)

@@ -19,7 +19,7 @@ from pathlib import Path
 REPO = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(REPO))
 
-from flearn_amd.dist import ALIGN, StripeModel, plan_stripes  # noqa: E402
+from flearn_amd.dist import ALIGN, StripeModel, plan_shards, plan_stripes  # noqa: E402
 
 # config -> (clients, fp32 params, 1-GPU step of the final profile pass in s, algorithmic bytes/col)
 CONFIGS = {
@@ -34,7 +34,7 @@ def one_gpu_step(cfg: str) -> float:
     return d["ms_per_step"] / 1e3
 
 
-def project(cfg: str, g: int, link_bs: float, launch_s=10e-6, collective_s=30e-6):
+def project(cfg: str, g: int, link_bs: float, launch_s=10e-6, collective_s=30e-6, tail=True):
     n, p = CONFIGS[cfg]
     t1 = one_gpu_step(cfg)
     local = -(-p // g)
@@ -42,25 +42,33 @@ def project(cfg: str, g: int, link_bs: float, launch_s=10e-6, collective_s=30e-6
     b_r = t1 / p  # the 1-GPU per-column cost (fused state traffic included)
     b_g = (g - 1) * 4.0 / ((g - 1) * link_bs) if g > 1 else 0.0
     m = StripeModel(launch_s, b_r, collective_s if g > 1 else 0.0, b_g)
-    widths = plan_stripes(local, m) if g > 1 else (local,)
-    step, red, exposed = m.makespan(widths)
+    if g == 1:
+        widths, rep = (local,), 0
+    elif tail:
+        widths, rep = plan_shards(p, g, m)
+    else:
+        widths, rep = plan_stripes(local, m), 0
+    step, red, exposed = m.makespan(widths, rep)
     return {"config": cfg, "gpus": g, "link_GBs": link_bs / 1e9, "ingress_GBs": (g - 1) * link_bs / 1e9,
-            "stripes": len(widths), "step_ms": round(step * 1e3, 3), "reduce_ms": round(red * 1e3, 3),
-            "exposed_gather_ms": round(exposed * 1e3, 3), "speedup": round(t1 / step, 2)}
+            "stripes": len(widths), "replicated_frac": round(rep / p, 3), "step_ms": round(step * 1e3, 3),
+            "reduce_ms": round(red * 1e3, 3), "exposed_gather_ms": round(exposed * 1e3, 3),
+            "speedup": round(t1 / step, 2)}
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--link-gbs", default="50,64")
     ap.add_argument("--json", action="store_true")
+    ap.add_argument("--no-tail", action="store_true", help="stripes only (no replicated tail)")
     a = ap.parse_args()
-    rows = [project(c, g, float(l) * 1e9) for l in a.link_gbs.split(",") for c in CONFIGS for g in (2, 4, 8)]
+    rows = [project(c, g, float(l) * 1e9, tail=not a.no_tail)
+            for l in a.link_gbs.split(",") for c in CONFIGS for g in (2, 4, 8)]
     if a.json:
         print(json.dumps(rows, indent=1))
         return
     for r in rows:
         print(f"{r['link_GBs']:>5.0f} GB/s/link  {r['config']:>3}  G={r['gpus']}  ingress {r['ingress_GBs']:>4.0f} GB/s  "
-              f"{r['stripes']} stripes  step {r['step_ms']:.3f} ms  (reduce {r['reduce_ms']:.3f}, exposed gather "
+              f"{r['stripes']} stripes  tail {r['replicated_frac']:.3f}  step {r['step_ms']:.3f} ms  (reduce {r['reduce_ms']:.3f}, exposed gather "
               f"{r['exposed_gather_ms']:.3f})  {r['speedup']:.2f}x")
 
 
