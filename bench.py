@@ -59,7 +59,7 @@ from flearn_amd import _native as na  # noqa: E402
 from flearn_amd import aggregator as agg  # noqa: E402
 from flearn_amd import launch, layouts  # noqa: E402
 from flearn_amd.dist import (ALIGN, PingPong, ShardedReducer, ShardPlan, StripeModel,  # noqa: E402
-                             all_gather_into, hip_reduce_fn, plan_shards)
+                             all_gather_into, hip_reduce_fn, shard_candidates)
 
 METRIC = "device-resident GiB/s, FedAVG N-client weighted tensor reduce; %HBM peak"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
@@ -248,15 +248,33 @@ def run_job(cfg, layout, n, args, world, rank, dev, g_eff):
             probe.reduce_only()
         model, cal = calibrate(probe, world, dev)
         probe.release()
-        widths, rep = plan_shards(p_real, g_eff, model)
+        cands = shard_candidates(p_real, g_eff, model)
+        widths, rep = cands[0]
+        trials = []
+        if world > 1 and len(cands) > 1:
+            # the model's plan and its neighbours, each timed for a few steps on this job (real
+            # collectives; max over ranks, so every rank picks the same plan)
+            for w_c, r_c in cands:
+                tj = Job(cfg, layout, n, ShardPlan.from_widths(p_real, g_eff, rank, w_c, rep=r_c), dev, world,
+                         args.reorder)
+                for _ in range(2):
+                    tj.red.step()
+                t = _max_over_ranks((_event_time(tj.red.step, 5),), world, dev)[0]
+                tj.release()
+                trials.append({"stripe_widths": list(w_c), "replicated_cols": r_c, "predicted_ms":
+                               round(model.makespan(w_c, r_c)[0] * 1e3, 4), "measured_ms": round(t * 1e3, 4)})
+            widths, rep = cands[min(range(len(cands)), key=lambda i: trials[i]["measured_ms"])]
         plan = ShardPlan.from_widths(p_real, g_eff, rank, widths, rep=rep)
         pred, red_s, exposed = model.makespan(plan.widths, plan.rep)
-        info.update(stripe_choice="model (flearn_amd.dist.plan_shards: stripes + replicated tail), coefficients "
-                                  "fitted on this job",
+        info.update(stripe_choice=("model (flearn_amd.dist.plan_shards: stripes + replicated tail), coefficients "
+                                   "fitted on this job" + ("; the fastest of the model's plan and its neighbours "
+                                                           "over 5 measured steps each" if trials else "")),
                     model={"a_r_us": round(model.a_r * 1e6, 3), "b_r_ns_per_col": round(model.b_r * 1e9, 5),
                            "a_g_us": round(model.a_g * 1e6, 3), "b_g_ns_per_col": round(model.b_g * 1e9, 5)},
                     calibration=cal, predicted_ms=round(pred * 1e3, 4),
                     predicted_exposed_gather_ms=round(exposed * 1e3, 4))
+        if trials:
+            info["plan_trials"] = trials
     info["stripe_widths"] = list(plan.widths)
     # columns every rank reduces itself (no gather): redundant work, counted once in `value`
     info["replicated_cols"] = plan.rep

@@ -160,6 +160,32 @@ def plan_shards(n_cols: int, world: int, model: StripeModel, max_stripes: int = 
     return best[0], best[1]
 
 
+def shard_candidates(n_cols: int, world: int, model: StripeModel, max_stripes: int = 8) -> list:
+    """The plans a measured trial chooses among (bench.py times each for a few steps on the
+    running job): plan_shards' best, the best plan with no replicated tail, and the best with
+    half and with 1.5x the best's tail — the model ignores that RCCL's kernels and the reduce
+    share CUs and HBM bandwidth, so its overlap is the optimistic end and the measured step picks."""
+    best = plan_shards(n_cols, world, model, max_stripes)
+    out = [best]
+    if world < 2:
+        return out
+
+    def with_tail(rep_target):
+        units = int(n_cols - rep_target) // (world * ALIGN)
+        rep = n_cols - world * units * ALIGN
+        if units < 1 or rep <= 0:
+            return None
+        return plan_stripes(units * ALIGN, model, max_stripes, rep=rep), rep
+
+    cands = [(plan_stripes(-(-max(n_cols, 1) // world), model, max_stripes), 0)]
+    if best[1] >= 4 * world * ALIGN:
+        cands += [with_tail(best[1] // 2), with_tail(min(int(best[1] * 1.5), int(n_cols * 0.75)))]
+    for c in cands:
+        if c is not None and c not in out:
+            out.append(c)
+    return out
+
+
 @dataclass(frozen=True)
 class ShardPlan:
     n_cols: int  # real global columns (parameters)

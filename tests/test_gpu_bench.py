@@ -44,5 +44,9 @@ def test_bench_two_ranks_rehearsal(config, cuda):
     if mg["replicated_cols"]:
         assert sum(mg["stripe_widths"]) * 2 + mg["replicated_cols"] == d["config"]["params"]
     assert mg["per_rank_reduce_ms"] > 0 and mg["exposed_gather_ms"] >= 0
+    # the plan is the fastest of the measured candidates
+    trials = mg["plan_trials"]
+    best = min(trials, key=lambda t: t["measured_ms"])
+    assert (best["stripe_widths"], best["replicated_cols"]) == (mg["stripe_widths"], mg["replicated_cols"])
     assert d["weak"]["clients"] == 200 and d["weak"]["value"] > 0
     assert d["roofline"]["bound"] == "hbm" and d["roofline"]["frac"] > 0

@@ -2,7 +2,7 @@
 pipeline model behind bench.py's stripe choice, and the plans it produces."""
 import pytest
 
-from flearn_amd.dist import ALIGN, ShardPlan, StripeModel, plan_shards, plan_stripes
+from flearn_amd.dist import ALIGN, ShardPlan, StripeModel, plan_shards, plan_stripes, shard_candidates
 
 
 def test_makespan_two_stage_pipeline():
@@ -107,3 +107,17 @@ def test_replicated_tail_layout():
         plan.local_to_global(292)
     with pytest.raises(ValueError):  # the stripes must end exactly where the tail starts
         ShardPlan.from_widths(4 * 192 + 100, 4, 0, (128, 128), rep=100)
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_shard_candidates_for_the_measured_trial(world):
+    p = 25_610_152
+    m = StripeModel.assumed(100, world)
+    c = shard_candidates(p, world, m)
+    assert c[0] == plan_shards(p, world, m)  # the model's choice first
+    assert any(rep == 0 for _, rep in c)  # the plan without replicated work is always tried
+    assert len(set((tuple(w), r) for w, r in c)) == len(c)  # distinct
+    for w, rep in c:
+        plan = ShardPlan.from_widths(p, world, 0, w, rep=rep)
+        assert plan.full_cols >= p
+    assert shard_candidates(p, 1, m) == [plan_shards(p, 1, m)]
