@@ -153,3 +153,26 @@ def test_strategies_shards_outputs_and_codec(c, strat, shards, out, http, cuda):
             w = w.astype(np.float32)
         assert g.shape == w.shape and g.dtype == w.dtype, (k, g.dtype, w.dtype)
         assert np.array_equal(g.reshape(-1).view(np.uint8), w.reshape(-1).view(np.uint8)), (k, strat, shards, out, http)
+
+
+@settings(max_examples=int(os.environ.get("FA_PROP_EXAMPLES", "40")) // 2, deadline=None,
+          suppress_health_check=list(HealthCheck))
+@given(cs=st.lists(case(), min_size=2, max_size=4), order=st.lists(st.integers(0, 3), min_size=3, max_size=8))
+def test_one_server_many_rounds(cs, order, cuda):
+    """ONE server across rounds whose layouts, client counts and weights change and come back
+    (cached plans, small-round records, pinned stagings and zero-copy buffers reused and
+    switched between), with fresh values every round: every round bit-equal to the oracle."""
+    s = AVG()
+    for r, i in enumerate(order):
+        lay, n, wkind, seed = cs[i % len(cs)]
+        rng = np.random.default_rng(seed + 7919 * r)  # new values each round, same layout
+        clients = [{k: (rng.integers(-1000, 1000, size=shape).astype(np.int64) if dt == np.int64
+                        else rng.standard_normal(shape).astype(dt)) for k, shape, dt in lay} for _ in range(n)]
+        weights = {"pyfloat": [float(x) for x in rng.uniform(0.1, 3.0, n)],
+                   "pyint": [int(x) for x in rng.integers(1, 600, n)],
+                   "np32": [np.float32(x) for x in rng.uniform(0.1, 3.0, n)],
+                   "np64": [np.float64(x) for x in rng.uniform(0.1, 3.0, n)],
+                   "ones": [1.0] * n}[wkind]
+        want = oracle.server_ensemble(weights, [{k: v.copy() for k, v in cl.items()} for cl in clients])
+        got = s.server([{"agg_weight": w, "params": cl} for w, cl in zip(weights, clients)], r)["w_glob"]
+        assert_dict_bitwise(got, want, f"round {r}: {lay} n={n} {wkind}")
