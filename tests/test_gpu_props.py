@@ -176,3 +176,44 @@ def test_one_server_many_rounds(cs, order, cuda):
         want = oracle.server_ensemble(weights, [{k: v.copy() for k, v in cl.items()} for cl in clients])
         got = s.server([{"agg_weight": w, "params": cl} for w, cl in zip(weights, clients)], r)["w_glob"]
         assert_dict_bitwise(got, want, f"round {r}: {lay} n={n} {wkind}")
+
+
+@settings(max_examples=int(os.environ.get("FA_PROP_EXAMPLES", "40")) // 2, deadline=None,
+          suppress_health_check=list(HealthCheck))
+@given(c=case(), op=st.sampled_from(["avgm", "adagrad", "yogi", "adam"]), init=st.booleans(),
+       shards=st.integers(1, 2))
+def test_server_side_optimizer_rounds_on_random_layouts(c, op, init, shards, cuda):
+    """Server-fused FedAVGM / FedOPT (BASELINE configs 3 and 5) on random fp32 layouts, 3 rounds:
+    round r = the reference's mean of fresh uploads, then the reference's update with w_local =
+    the previous global model in fp32 (avgm.py:19-36, opt.py:23-65) — the first round adopts the
+    mean when no previous model was given — composed from the oracle's restatements, bit for bit,
+    with the double-buffered state in HBM (and split over column shards)."""
+    from flearn_amd import AVGM, OPT
+
+    lay, n, wkind, seed = c
+    lay = [(k, shape, np.float32) for k, shape, _ in lay]  # the fused step covers the fp32 bucket
+    rng = np.random.default_rng(seed)
+    s = AVGM(server_side=True) if op == "avgm" else OPT(server_side=True, method=op)
+    s.devices = [cuda] * shards
+    prev = None
+    if init:
+        prev = {k: rng.standard_normal(shape).astype(np.float32) for k, shape, _ in lay}
+        s.server_opt.init_global(prev)
+    v = None
+    for r in range(3):
+        clients = [{k: rng.standard_normal(shape).astype(np.float32) for k, shape, _ in lay} for _ in range(n)]
+        weights = {"pyfloat": [float(x) for x in rng.uniform(0.1, 3.0, n)],
+                   "pyint": [int(x) for x in rng.integers(1, 600, n)],
+                   "np32": [np.float32(x) for x in rng.uniform(0.1, 3.0, n)],
+                   "np64": [np.float64(x) for x in rng.uniform(0.1, 3.0, n)],
+                   "ones": [1.0] * n}[wkind]
+        g = oracle.server_ensemble(weights, [{k: a.copy() for k, a in cl.items()} for cl in clients])
+        if prev is None:  # first round, no previous model: the mean, state adopted
+            want = g
+        elif op == "avgm":
+            want, v = oracle.mean_momentum(prev, g, v, 0.9)
+        else:
+            want, v = oracle.adaptive_opt(prev, g, v, op)
+        prev = {k: np.asarray(want[k]).astype(np.float32) for k in want}
+        got = s.server([{"agg_weight": w, "params": cl} for w, cl in zip(weights, clients)], r)["w_glob"]
+        assert_dict_bitwise(got, want, f"round {r} {op} {lay} n={n} {wkind} init={init}")
