@@ -443,7 +443,10 @@ def main():
                                    if job.plan.rep else "") + ")"
                                 + (f"; EMULATED: rank 0's reduce of a {emu}-GPU job on one GPU, no gather"
                                    if emu else "")),
-                "hbm_peak_frac_of_value": round(value * GIB / 1e9 / HBM_PEAK_GBS, 4),
+                # `value` against the HBM peak of the GPUs that produced it (N x 8 TB/s; at N > 1
+                # the step includes the all-gather, so this is the job's, not a kernel's, fraction)
+                "hbm_peak_frac_of_value": round(value * GIB / 1e9 / (HBM_PEAK_GBS * (world if not emu else 1)), 4),
+                "hbm_peak_gbs_all_gpus": HBM_PEAK_GBS * (world if not emu else 1),
                 "wall_s_timed_region": round(wall, 4),
             },
             "roofline": roofline,
