@@ -8,6 +8,7 @@ runs one fa_opt_apply launch, with the reference's operation order and precision
 from __future__ import annotations
 
 import concurrent.futures
+import ctypes
 
 import numpy as np
 import torch
@@ -39,14 +40,14 @@ class _DictPack:
     fa_py_pack_rows (csrc/fa_pyhost.c), in byte-balanced parts run on the pool; False when a
     value is not a C-contiguous array of the expected dtype (the caller then copies in Python)."""
 
-    def __init__(self, lay, dtype, dst_ptr):
+    def __init__(self, lay, dtype, dst_ptr, part_bytes=_PART_BYTES):
         self.fn = na.load_pyhost().fa_py_pack_rows
         item, fmt = np.dtype(dtype).itemsize, _FMT[np.dtype(dtype)]
         parts, cur, size = [], [], 0
         for k, _s, o, n in lay:
             cur.append((k, n, o))
             size += n * item
-            if size >= _PART_BYTES:
+            if size >= part_bytes:
                 parts.append(cur)
                 cur, size = [], 0
         if cur:
@@ -63,16 +64,26 @@ class _DictPack:
             desc[6 * m:7 * m] = np.array([o for _, _, o in part], dtype=np.int64) * item
             self.parts.append((tuple(k for k, _, _ in part), desc))
 
-    def __call__(self, d: dict) -> bool:
+    def tasks(self, d: dict):
+        """The pack as pool tasks (one per part); each returns 0 on success."""
         if type(d) is not dict:
             d = dict(d)
         clients = [d]
-        return all(rc == 0 for rc in _run([
-            (lambda keys=keys, desc=desc: self.fn(clients, keys, len(keys), desc.ctypes.data, 0, 1))
-            for keys, desc in self.parts]))
+        return [(lambda keys=keys, desc=desc: self.fn(clients, keys, len(keys), desc.ctypes.data, 0, 1))
+                for keys, desc in self.parts]
+
+    def __call__(self, d: dict) -> bool:
+        return all(rc == 0 for rc in _run(self.tasks(d)))
 
 
 class DeviceUpdater:
+    #: zero-copy, chunked: the update kernel reads w_local / w_glob from the pinned staging and
+    #: writes the result into pinned memory over PCIe, one chunk of keys at a time, while the
+    #: pool packs the next chunk and copies finished chunks out (False: pack everything, two H2D
+    #: copies, one launch, one D2H; tools/bench_client_update.py --ab times both)
+    zero_copy = True
+    chunk_bytes = 32 << 20  # w_glob bytes per zero-copy chunk
+
     def __init__(self, op: str, device=None, beta=0.9, eta=1e-1, tau=1e-9, beta2=0.99):
         self.op = na.OP_BY_NAME[op]
         self.device = device
@@ -174,6 +185,8 @@ class DeviceUpdater:
             self.v = torch.zeros(total, dtype=tdt, device=dev)  # np.zeros_like(delta) on first use
             self._stage = None
         st = self._staging(lay, total, tdt, dev)
+        if self.zero_copy:
+            return self._device_step_zc(w_local, glob, local, lay, total, tdt, dev, **override)
         lh, gh, oh, pack_l, pack_g = st
         with torch.cuda.device(dev):
             # local -> pinned -> device, then the global model while the local one is in flight
@@ -198,6 +211,75 @@ class DeviceUpdater:
         fresh = np.empty(total, dtype=src.dtype)
         step = 1 << 22
         _run([(lambda a=a: np.copyto(fresh[a : a + step], src[a : a + step])) for a in range(0, total, step)])
+        for k, s, o, n in lay:  # replaced per key, like the reference (avgm.py:34-35, opt.py:62-63)
+            w_local[k] = fresh[o : o + n].reshape(s)
+
+    def _chunks(self, lay, total, tdt):
+        """[(first, end, pack_local, pack_glob)]: runs of whole keys of about chunk_bytes of w_glob,
+        in layout order, with their own pack tables into the shared staging (cached per layout)."""
+        if getattr(self, "_chunk_plan", None) is not None and self._chunk_plan[0] is self._stage:
+            return self._chunk_plan[1]
+        lh, gh = self._stage[0], self._stage[1]
+        gdt = np.float64 if tdt == torch.float64 else np.float32
+        item = np.dtype(gdt).itemsize
+        groups, cur, size = [], [], 0
+        for e in lay:
+            cur.append(e)
+            size += e[3] * item
+            if size >= self.chunk_bytes:
+                groups.append(cur)
+                cur, size = [], 0
+        if cur:
+            groups.append(cur)
+        out = []
+        for j, g in enumerate(groups):
+            first = g[0][2] if j else 0
+            end = groups[j + 1][0][2] if j + 1 < len(groups) else total
+            out.append((first, end, _DictPack(g, np.float32, lh.data_ptr(), 4 << 20),
+                        _DictPack(g, gdt, gh.data_ptr(), 4 << 20), g))
+        self._chunk_plan = (self._stage, out)
+        return out
+
+    def _device_step_zc(self, w_local, glob, local, lay, total, tdt, dev, **override):
+        from ..aggregator import _epilogue
+
+        lh, gh, oh = self._stage[0], self._stage[1], self._stage[2]
+        L = na.lib()
+        prec = na.PREC_F64 if tdt == torch.float64 else na.PREC_F32
+        p = dict(self.params, **override)
+        src = oh.numpy()
+        fresh = np.empty(total, dtype=src.dtype)
+        with torch.cuda.device(dev):
+            stream = torch.cuda.current_stream(dev)
+            sh = stream.cuda_stream
+            events = []
+            for first, end, pack_l, pack_g, g in self._chunks(lay, total, tdt):
+                tl, tg = pack_l.tasks(local), pack_g.tasks(glob)
+                rc = _run(tl + tg)
+                if any(rc[: len(tl)]):  # a value the native pack refuses: copy in Python
+                    for k, s, o, n in g:
+                        lh.numpy()[o : o + n] = local[k].reshape(-1)
+                if any(rc[len(tl) :]):
+                    for k, s, o, n in g:
+                        gh.numpy()[o : o + n] = glob[k].reshape(-1)
+                n = end - first
+                epi = _epilogue(self.op, lh[first:end], self.v[first:end], p["beta"], p["eta"], p["tau"], p["beta2"])
+                out = oh[first:end].data_ptr()
+                na.check(L.fa_opt_apply(prec, ctypes.byref(epi), lh[first:end].data_ptr(), gh[first:end].data_ptr(), n,
+                                        None if prec == na.PREC_F64 else out, out if prec == na.PREC_F64 else None, sh),
+                         "fa_opt_apply")
+                ev = torch.cuda.Event()
+                ev.record(stream)
+                events.append((ev, first, end))
+            # finished chunks leave the pinned result while later chunks are still on the GPU
+            futs = []
+            step = 1 << 22
+            for ev, first, end in events:
+                ev.synchronize()
+                futs += [_pool().submit(lambda a=a, b=min(a + step, end): np.copyto(fresh[a:b], src[a:b]))
+                         for a in range(first, end, step)]
+            for f in futs:
+                f.result()
         for k, s, o, n in lay:  # replaced per key, like the reference (avgm.py:34-35, opt.py:62-63)
             w_local[k] = fresh[o : o + n].reshape(s)
 

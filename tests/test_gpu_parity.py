@@ -961,11 +961,19 @@ def test_host_pack_mixed_upload_kinds(shards, cuda):
         assert_dict_bitwise(got, want, f"mixed x{shards}")
 
 
+@pytest.mark.parametrize("mode", ["copy-engine", "zero-copy", "zero-copy-1MiB-chunks"])
 @pytest.mark.parametrize("op", ["avgm", "adagrad", "yogi"])
-def test_client_side_update_large_and_fallback_values(op, cuda):
+def test_client_side_update_large_and_fallback_values(op, mode, cuda, monkeypatch):
     """The client update on a model above the copy-part size (parallel native packs) and with
     values the byte copy hands back to Python (a Fortran-order local array, a strided global
-    view, a 0-d entry): bit-exact against the oracle over 3 rounds, state included."""
+    view, a 0-d entry): bit-exact against the oracle over 3 rounds, state included — with two H2D
+    copies and one launch, and zero-copy in one or in many chunks (the kernel reading the pinned
+    staging over PCIe chunk by chunk while the next chunk is packed)."""
+    from flearn_amd.strategy._update import DeviceUpdater
+
+    monkeypatch.setattr(DeviceUpdater, "zero_copy", mode != "copy-engine")
+    if mode == "zero-copy-1MiB-chunks":
+        monkeypatch.setattr(DeviceUpdater, "chunk_bytes", 1 << 20)
     rng = np.random.default_rng(21)
     shapes = {"a": (1024, 3000), "b": (3000,), "c": (700, 900), "d": (), "e": (5, 7)}
     prev = {k: rng.standard_normal(sh).astype(np.float32) for k, sh in shapes.items()}

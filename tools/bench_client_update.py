@@ -44,7 +44,16 @@ def main():
     ap.add_argument("--rounds", type=int, default=4)
     ap.add_argument("--ref-rounds", type=int, default=2)
     ap.add_argument("--no-counters", action="store_true", help="drop the BN num_batches_tracked keys")
+    ap.add_argument("--ab", action="store_true",
+                    help="DeviceUpdater copy-engine vs zero-copy chunked, alternating, outputs compared")
+    ap.add_argument("--zero-copy", type=int, default=None, help="DeviceUpdater.zero_copy (default: the class default)")
     a = ap.parse_args()
+    if a.zero_copy is not None:
+        from flearn_amd.strategy._update import DeviceUpdater
+
+        DeviceUpdater.zero_copy = bool(a.zero_copy)
+    if a.ab:
+        return ab(a)
     lay = layouts.get(a.layout)
     w_local0 = model(lay, 1, np.float32, not a.no_counters)
     globs = [model(lay, 10 + r, np.float64, not a.no_counters) for r in range(a.rounds)]
@@ -72,7 +81,42 @@ def main():
         res[method] = {"flearn_amd_s": round(med, 4), "first_call_s": round(ts[0], 4),
                        "reference_s": round(float(np.median(rs[1:] if len(rs) > 1 else rs)), 4),
                        "speedup": round(float(np.median(rs[1:] if len(rs) > 1 else rs)) / med, 1)}
+    from flearn_amd.strategy._update import DeviceUpdater
+
+    res["zero_copy"] = DeviceUpdater.zero_copy
     res["note"] = "host arrays in and out (PCIe-inclusive); reference = its numpy ops on 1 core; median after round 0"
+    print(json.dumps(res))
+
+
+def ab(a):
+    from flearn_amd.strategy._update import DeviceUpdater
+
+    lay = layouts.get(a.layout)
+    w_local0 = model(lay, 1, np.float32, not a.no_counters)
+    globs = [model(lay, 10 + r, np.float64, not a.no_counters) for r in range(a.rounds)]
+    res = {"layout": a.layout}
+    for method in ("avgm", "adagrad"):
+        # one strategy object per mode (its pinned staging persists), called alternately
+        objs = {zc: (flearn_amd.AVGM() if method == "avgm" else flearn_amd.OPT()) for zc in (False, True)}
+        times, outs = {False: [], True: []}, {False: [], True: []}
+        for rep in range(3):
+            for r in range(a.rounds):
+                for zc in (False, True):
+                    DeviceUpdater.zero_copy = zc
+                    s = objs[zc]
+                    wl = dict(w_local0)
+                    t0 = time.perf_counter()
+                    out = s.mean_momentum(wl, globs[r], 0.9) if method == "avgm" else s.adaptive_opt(wl, globs[r], "adagrad")
+                    dt = time.perf_counter() - t0
+                    if rep or r:
+                        times[zc].append(dt)
+                    if rep == 0:
+                        outs[zc].append({k: np.array(v, copy=True) for k, v in out.items()})
+        same = all(np.array_equal(np.asarray(x[k]), np.asarray(y[k])) and np.asarray(x[k]).dtype == np.asarray(y[k]).dtype
+                   for x, y in zip(outs[False], outs[True]) for k in x)
+        res[method] = {"copy_engine_s": round(float(np.median(times[False])), 4),
+                       "zero_copy_s": round(float(np.median(times[True])), 4), "bit_equal": same}
+    DeviceUpdater.zero_copy = True
     print(json.dumps(res))
 
 
