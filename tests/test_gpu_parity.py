@@ -1108,3 +1108,56 @@ def test_small_round_fast_path_reuses_its_record_safely(zero_copy, cuda, monkeyp
         rec = s.engine.last_plan.memo.get(("small_round", id(s.engine.packer), str(s.engine.device), "reference",
                                            zero_copy))
         assert rec, "the small-round record was not built"
+
+
+@pytest.mark.parametrize("wkind", ["pyfloat", "np64", "np32"])
+@pytest.mark.parametrize("n,p,dev", [(3, 4099, False), (41, 4099, False), (3, 4_500_001, False),
+                                     (5, 4_500_001, True)])
+def test_special_values_match_reference(wkind, n, p, dev, cuda):
+    """IEEE corner cases through the whole server path, against the oracle: fp32 subnormal inputs
+    and products (no flush to zero), signed zeros (-0 sums stay -0), infinities, input NaNs, and
+    inf - inf.  Bit-exact everywhere except the bits of NaNs the arithmetic creates (inf - inf):
+    x86 SSE makes the negative default NaN, the GPU the positive canonical one — there only the
+    NaN positions must agree."""
+    rng = np.random.default_rng(n)
+    tiny = np.float32(1.4e-45)  # the smallest fp32 subnormal
+    clients = []
+    for i in range(n):
+        x = rng.standard_normal(p).astype(np.float32)
+        if p > 260_000:  # the corner cases again at a piece boundary, mid-window and at the end
+            for o in (262_144 - 100, p // 2 + 3, p - 300):
+                x[o : o + 64] = tiny * (i + 1)
+                x[o + 64 : o + 128] = -0.0
+                x[o + 128] = np.inf if i == 0 else (-np.inf if i == n - 1 else 1.0)
+        x[0:64] = tiny * (i + 1)                                  # subnormal inputs, subnormal sums
+        x[64:128] = np.float32(1.1754942e-38) * rng.uniform(-1, 1, 64).astype(np.float32)  # around FLT_MIN
+        x[128:192] = -0.0                                           # -0 + -0 ... = -0
+        x[192:256] = 0.0 if i % 2 else -0.0                         # +0 / -0 mixed
+        x[256] = np.inf                                             # +inf stays +inf
+        x[257] = np.inf if i == 0 else (-np.inf if i == n - 1 else 1.0)  # inf - inf: a created NaN
+        x[258] = np.float32("nan") if i == 1 else 2.0               # an input NaN propagates
+        x[259] = np.float32(3.4e38)                                 # overflow to inf in the sum
+        clients.append({"w": x, "b": x[:7].copy()})
+    weights = {"pyfloat": [float(x) for x in rng.uniform(0.1, 3.0, n)],
+               "np64": [np.float64(x) for x in rng.uniform(0.1, 3.0, n)],
+               "np32": [np.float32(x) for x in rng.uniform(0.1, 3.0, n)]}[wkind]
+    want = oracle.server_ensemble(weights, [{k: v.copy() for k, v in c.items()} for c in clients])
+    if dev:  # device-resident uploads: the row-pointer kernel reads them in place
+        if wkind != "pyfloat":
+            pytest.skip("torch uploads follow torch's promotion")
+        import torch
+
+        ups = [{"agg_weight": w, "params": {k: torch.from_numpy(v).to(cuda) for k, v in c.items()}}
+               for w, c in zip(weights, clients)]
+        got = {k: v.cpu().numpy() if hasattr(v, "cpu") else v for k, v in AVG().server(ups, 0)["w_glob"].items()}
+    else:
+        got = AVG().server(upload(clients, weights), 0)["w_glob"]
+    for k in want:
+        g, w = np.asarray(got[k]), np.asarray(want[k])
+        assert g.dtype == w.dtype and g.shape == w.shape, k
+        gn, wn = np.isnan(g), np.isnan(w)
+        assert np.array_equal(gn, wn), (k, np.nonzero(gn != wn))
+        assert g[~gn].tobytes() == w[~wn].tobytes(), (k, wkind, np.nonzero(g[~gn].view(np.uint8) != w[~wn].view(np.uint8)))
+        if k == "w":
+            assert np.all(np.signbit(g[128:192])) and np.isposinf(g[256]) and np.isnan(g[257]) and np.isnan(g[258])
+            assert np.any(g[0:64] != 0)  # subnormal results were not flushed
