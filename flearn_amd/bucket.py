@@ -202,9 +202,21 @@ def make_plan(agg_weight_lst, w_local_lst, key_lst=None) -> BucketPlan:
         raise IndexError("list index out of range")  # reference: agg_weight_lst[0] (strategy.py:123)
     if len(agg_weight_lst) != len(w_local_lst):
         raise ValueError("agg_weight_lst and w_local_lst differ in length")
-    keys = select_keys(w_local_lst, key_lst)
-    sig0 = _raw_signature(w_local_lst[0], keys)
-    if sig0 is not None and _same_signature_native(w_local_lst, keys, sig0):
+    keys = sig0 = slow = None
+    if key_lst is None and len(w_local_lst) > 1:
+        # the usual round: client 0's keys, verified natively in every client together with their
+        # metadata — a client missing one of them makes the native check give up (the general
+        # intersection below then runs), so passing it proves the intersection is client 0's keys
+        k0 = list(w_local_lst[0].keys())
+        s0 = _raw_signature(w_local_lst[0], k0)
+        if s0 is not None and _same_signature_native(w_local_lst, k0, s0):
+            keys, sig0, slow = k0, s0, []
+    if keys is None:
+        keys = select_keys(w_local_lst, key_lst)
+        sig0 = _raw_signature(w_local_lst[0], keys)
+    if slow is not None:
+        pass
+    elif sig0 is not None and _same_signature_native(w_local_lst, keys, sig0):
         slow = []
     else:
         slow = [n for n in range(1, len(w_local_lst))
