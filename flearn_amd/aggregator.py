@@ -702,15 +702,30 @@ class Aggregator:
             else:
                 stack = torch.empty((n, g.stride), dtype=tdt, device=dev)
                 dout = torch.empty(g.stride, dtype=odt, device=dev)
+            split = None
             if kind == KIND_F32:
                 fn = L.fa_reduce_f32
                 args = (stack.data_ptr(), g.stride, n, nm.mode, w.data_ptr(), float(nm.denom), 0, g.stride, None,
                         None if f64 else dout.data_ptr(), dout.data_ptr() if f64 else None)
+                if zc and n >= 4 and nm.mode in (na.MODE_W32_DIV64, na.MODE_W32_DIV32):
+                    # two launches, so the second half is packed while the first is summed: rows
+                    # [0, h) into their fp32 sum (W = 1: the epilogue returns the sum itself),
+                    # written over row h-1, then rows [h-1, n) with weight fl32(1.0) on that row —
+                    # fl32(1 * acc) = acc, so the chain of adds is the single launch's, bit for bit
+                    h = n // 2
+                    row = g.stride * 4
+                    w_b = torch.cat([torch.ones(1, dtype=torch.float32, device=dev), w[h:]])
+                    part = host.data_ptr() + (h - 1) * row
+                    args_a = (host.data_ptr(), g.stride, h, na.MODE_W32_DIV32, w.data_ptr(), 1.0, 0, g.stride, None,
+                              part, None)
+                    args_b = (part, g.stride, n - h + 1, nm.mode, w_b.data_ptr(), float(nm.denom), 0, g.stride, None,
+                              None if f64 else dout.data_ptr(), dout.data_ptr() if f64 else None)
+                    split = (h, args_a, args_b, w_b)
             else:
                 fn = L.fa_reduce_f64 if kind == KIND_F64 else L.fa_reduce_i64
                 args = (stack.data_ptr(), g.stride, n, w.data_ptr(), float(nm.denom), 0, g.stride, dout.data_ptr())
             out = [(s.key, s.offset, s.numel, s.shape) for s in g.segments]
-            kinds.append((nat, host, stack, w, dout, hout, hout.numpy(), fn, args, out))
+            kinds.append((nat, host, stack, w, dout, hout, hout.numpy(), fn, args, out, split))
         g32 = plan.groups.get(KIND_F32)
         wsig = (tuple((s.key, s.shape, s.offset) for s in g32.segments) + (g32.stride,)) if g32 is not None else None
         rec = plan.memo[key] = (tuple(kinds), na.load_pyhost().fa_py_pack_rows, wsig)
@@ -734,13 +749,23 @@ class Aggregator:
 
             if wire_row(lst[0], wsig) is not None:  # decoded by the wire codec into pinned rows of
                 return None                          # this layout: the general path DMAs them as is
-        for nat, *_ in kinds:
-            if pack(lst, nat.keys, len(nat.keys), nat.ptr, 0, len(lst)) != 0:
+        n = len(lst)
+        for nat, *rest in kinds:  # every bucket packed whole, except the split one's second half
+            split = rest[-1]
+            if pack(lst, nat.keys, len(nat.keys), nat.ptr, 0, split[0] if split else n) != 0:
                 return None
         dev = self.device
         stream = torch.cuda.current_stream(dev)
         sh = stream.cuda_stream
-        for nat, host, stack, w, dout, hout, hnp, fn, args, out in kinds:
+        for nat, host, stack, w, dout, hout, hnp, fn, args, out, split in kinds:
+            if split is not None:  # zero-copy in two launches: the second half packed meanwhile
+                h, args_a, args_b, _ = split
+                na.check(fn(*args_a, sh), fn.__name__)
+                if pack(lst, nat.keys, len(nat.keys), nat.ptr, h, n) != 0:
+                    stream.synchronize()  # the first launch must be done with the staging
+                    return None
+                na.check(fn(*args_b, sh), fn.__name__)
+                continue
             if stack is host:  # zero-copy record
                 na.check(fn(*args, sh), fn.__name__)
                 continue
@@ -749,7 +774,7 @@ class Aggregator:
             hout.copy_(dout, non_blocking=True)
         stream.synchronize()  # also: the staging may be rewritten by the next call
         parts = {}
-        for nat, host, stack, w, dout, hout, hnp, fn, args, out in kinds:
+        for nat, host, stack, w, dout, hout, hnp, fn, args, out, split in kinds:
             fresh = hnp.copy()
             for k, off, m, shape in out:
                 a = fresh[off : off + m].reshape(shape)

@@ -1098,9 +1098,12 @@ def test_small_round_fast_path_reuses_its_record_safely(zero_copy, cuda, monkeyp
     for r in range(6):
         flat = oracle.fill_uniform(10, p, seed=40 + r)
         clients = [layouts.synthetic_state_dict(layout, flat[i]) for i in range(10)]
-        if r == 2:  # a Fortran-ordered copy: same shape and dtype, not C-contiguous
-            k = next(k for k, v in clients[3].items() if v.ndim == 2)
-            clients[3][k] = np.asfortranarray(clients[3][k])
+        if r in (2, 4):  # a Fortran-ordered copy: same shape and dtype, not C-contiguous — in the
+            # first half of the clients, and (round 4) in the second half, which the zero-copy
+            # record packs only after its first launch is queued
+            c = 3 if r == 2 else 7
+            k = next(k for k, v in clients[c].items() if v.ndim == 2)
+            clients[c][k] = np.asfortranarray(clients[c][k])
         weights = [1.0 + 0.5 * i for i in range(10)]
         got = s.server(upload(clients, weights), r)["w_glob"]
         want = oracle.server_ensemble(weights, [{k: v.copy() for k, v in c.items()} for c in clients])
