@@ -47,11 +47,14 @@ def main():
     ap.add_argument("--ab", action="store_true",
                     help="DeviceUpdater copy-engine vs zero-copy chunked, alternating, outputs compared")
     ap.add_argument("--zero-copy", type=int, default=None, help="DeviceUpdater.zero_copy (default: the class default)")
+    ap.add_argument("--chunk-mb", type=float, default=None, help="DeviceUpdater.chunk_bytes in MiB")
     a = ap.parse_args()
-    if a.zero_copy is not None:
-        from flearn_amd.strategy._update import DeviceUpdater
+    from flearn_amd.strategy._update import DeviceUpdater
 
+    if a.zero_copy is not None:
         DeviceUpdater.zero_copy = bool(a.zero_copy)
+    if a.chunk_mb is not None:
+        DeviceUpdater.chunk_bytes = int(a.chunk_mb * (1 << 20))
     if a.ab:
         return ab(a)
     lay = layouts.get(a.layout)
@@ -84,6 +87,7 @@ def main():
     from flearn_amd.strategy._update import DeviceUpdater
 
     res["zero_copy"] = DeviceUpdater.zero_copy
+    res["chunk_bytes"] = DeviceUpdater.chunk_bytes
     res["note"] = "host arrays in and out (PCIe-inclusive); reference = its numpy ops on 1 core; median after round 0"
     print(json.dumps(res))
 
