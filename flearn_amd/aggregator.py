@@ -755,6 +755,17 @@ class Aggregator:
             if pack(lst, nat.keys, len(nat.keys), nat.ptr, 0, split[0] if split else n) != 0:
                 return None
         dev = self.device
+        if dev.index is not None and dev.index != torch.cuda.current_device():
+            with torch.cuda.device(dev):  # launches go to dev's stream from dev's context
+                parts = self._small_launch(kinds, pack, lst, n, dev)
+        else:
+            parts = self._small_launch(kinds, pack, lst, n, dev)
+        return None if parts is None else {k: parts[k] for k in plan.keys}
+
+    def _small_launch(self, kinds, pack, lst, n, dev):
+        """The queued part of _small_round: launches (and copies) on dev's current stream, one
+        synchronisation, the results as {key: value}; None when the split bucket's second half
+        cannot be packed natively (nothing left running)."""
         stream = torch.cuda.current_stream(dev)
         sh = stream.cuda_stream
         for nat, host, stack, w, dout, hout, hnp, fn, args, out, split in kinds:
@@ -779,7 +790,7 @@ class Aggregator:
             for k, off, m, shape in out:
                 a = fresh[off : off + m].reshape(shape)
                 parts[k] = a.dtype.type(a[()]) if shape == () else a
-        return {k: parts[k] for k in plan.keys}
+        return parts
 
     def _gather_columns(self, plan: BucketPlan, parts):
         """Column-sharded group: every rank's reduced columns -> the whole f32 bucket on every
