@@ -325,10 +325,37 @@ __device__ __forceinline__ typename vec4<T>::type buf_load_tquad(__amdgpu_buffer
   }
 }
 
-template <typename T>
+// XL (whole-line f64 stores): the wave's 64 consecutive f64 quads (2 KiB) are regrouped through
+// LDS so that each of the two store instructions writes 1 KiB contiguous (eight whole 128-B
+// lines) instead of every other 16 B of the 2 KiB (DESIGN.md §4 finding 22).  Callers run it
+// wave-convergent with q = (the wave's first quad) + lane (finish_piece's slots).  The product
+// enables it where it does not make the kernel spill (rowmajor_group); FA_EPI_STORE64_LDS=1
+// forces it everywhere (tuning builds).
+#ifndef FA_EPI_STORE64_LDS
+#define FA_EPI_STORE64_LDS 0
+#endif
+template <typename T, bool XL = false>
 __device__ __forceinline__ void buf_store_tquad(__amdgpu_buffer_rsrc_t r, int q, typename vec4<T>::type v) {
   if constexpr (sizeof(T) == 4) {
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, q * 16, 0, FA_EPI_STORE_AUX);
+  } else if constexpr (XL || FA_EPI_STORE64_LDS != 0) {
+    typedef double d2 __attribute__((ext_vector_type(2)));
+    __shared__ d2 xch[8][128];  // 2 KiB per wave, up to 8 waves per block
+    const int lane = (int)threadIdx.x & 63;
+    d2* s = xch[(int)threadIdx.x >> 6];
+    s[2 * lane] = d2{v[0], v[1]};
+    s[2 * lane + 1] = d2{v[2], v[3]};
+    // lane l reads what lanes l/2 and 32 + l/2 wrote: a cross-lane dependency the compiler does
+    // not see, so pin the order (one wave's LDS operations complete in order)
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    __builtin_amdgcn_wave_barrier();
+    const d2 a = s[lane], b = s[64 + lane];
+    const int base = (q - lane) * 32;  // the wave's first byte
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, a), r, base + lane * 16, 0, FA_EPI_STORE64_AUX);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, b), r, base + 1024 + lane * 16, 0,
+                                           FA_EPI_STORE64_AUX);
+    __builtin_amdgcn_wave_barrier();  // the next slot's writes come after these reads
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
   } else {
     typedef double d2 __attribute__((ext_vector_type(2)));
     const d2 lo = {v[0], v[1]}, hi = {v[2], v[3]};
@@ -408,26 +435,26 @@ __device__ __forceinline__ void epi_compute(const Epi<T>& e, const typename vec4
 // store quad q's updated state and results.  GUARD = false: the result stores are issued
 // unconditionally (a null out32 / out64 has an empty descriptor range, so they are dropped) and
 // the quad is one basic block.
-template <typename T, int OP, bool GUARD = true>
+template <typename T, int OP, bool GUARD = true, bool XL = false>
 __device__ __forceinline__ void epi_store(const Epi<T>& e, const EpiRsrc<T, OP>& r, int q,
                                           const typename vec4<float>::type l, const typename vec4<T>::type vv,
                                           const typename vec4<T>::type w) {
   if constexpr (OP == FA_OP_DYN) buf_store_tquad<float>(r.rl, q, l);
-  if constexpr (OP != FA_OP_MEAN) buf_store_tquad<T>(r.rvo, q, vv);
+  if constexpr (OP != FA_OP_MEAN) buf_store_tquad<T, XL>(r.rvo, q, vv);
   if (!GUARD || e.out32) buf_store_tquad<float>(r.r32, q, typename vec4<float>::type{(float)w[0], (float)w[1], (float)w[2], (float)w[3]});
-  if (!GUARD || e.out64) buf_store_tquad<double>(r.r64, q, typename vec4<double>::type{(double)w[0], (double)w[1], (double)w[2], (double)w[3]});
+  if (!GUARD || e.out64) buf_store_tquad<double, XL>(r.r64, q, typename vec4<double>::type{(double)w[0], (double)w[1], (double)w[2], (double)w[3]});
 }
 
-template <typename T, int OP, typename A, bool GUARD = true>
+template <typename T, int OP, typename A, bool GUARD = true, bool XL = false>
 __device__ __forceinline__ void epi_quad(const Epi<T>& e, const EpiRsrc<T, OP>& r, int q,
                                          const typename vec4<A>::type a, typename vec4<float>::type l,
                                          typename vec4<T>::type vv) {
   typename vec4<T>::type w;
   epi_compute<T, OP, A>(e, a, l, vv, w);
-  epi_store<T, OP, GUARD>(e, r, q, l, vv, w);
+  epi_store<T, OP, GUARD, XL>(e, r, q, l, vv, w);
 }
 
-template <typename T, int OP, typename A, int V, int STEP, int B>
+template <typename T, int OP, typename A, int V, int STEP, int B, bool XL = false>
 __device__ __forceinline__ void finish_piece(const Epi<T>& e, int64_t qbase, int cols,
                                              const typename vec4<A>::type (&acc)[V]) {
   static_assert(V % B == 0, "batch must divide the slots");
@@ -440,7 +467,8 @@ __device__ __forceinline__ void finish_piece(const Epi<T>& e, int64_t qbase, int
 #pragma unroll
     for (int b = 0; b < B; ++b) epi_load<T, OP>(r, (int)threadIdx.x + (b0 + b) * STEP, l[b], vv[b]);
 #pragma unroll
-    for (int b = 0; b < B; ++b) epi_quad<T, OP, A>(e, r, (int)threadIdx.x + (b0 + b) * STEP, acc[b0 + b], l[b], vv[b]);
+    for (int b = 0; b < B; ++b)
+      epi_quad<T, OP, A, true, XL>(e, r, (int)threadIdx.x + (b0 + b) * STEP, acc[b0 + b], l[b], vv[b]);
   }
 }
 
@@ -1202,7 +1230,7 @@ __global__ __launch_bounds__(64 * W) void reduce_kernel_narrow(const float* __re
 
 // One group of a row-major block: KG of the block's pieces (slots g0 .. g0+KG-1, interleaved
 // over the grid as in reduce_kernel_rows), all rows swept once, then the group epilogue.
-template <class P, typename T, int OP, int V, int D, int W, int KG, bool NT, int EPIB, bool TR>
+template <class P, typename T, int OP, int V, int D, int W, int KG, bool NT, int EPIB, bool TR, int XLM = -1>
 __device__ __forceinline__ void rowmajor_group(const char* __restrict__ base, int64_t row_bytes, int n,
                                                const typename P::w_t* __restrict__ w, int64_t g0, int64_t k,
                                                int64_t pc, int64_t pieces, int64_t nquads, int64_t ncols,
@@ -1291,8 +1319,12 @@ __device__ __forceinline__ void rowmajor_group(const char* __restrict__ base, in
       }
     }
   } else {
+    // whole-line f64 state / result stores where they cost no spills: the fused ops at KG <= 3
+    // (at KG = 4 the LDS regrouping pushes the kernel past 256 + 256 registers; finding 22)
+    // (XLM: -1 this rule, 0 / 1 forced off / on by the tuner)
+    constexpr bool XL = XLM >= 0 ? XLM == 1 : (sizeof(T) == 8 && OP != FA_OP_MEAN && KG <= 3);
 #pragma unroll
-    for (int j = 0; j < KG; ++j) finish_piece<T, OP, A, V, 64 * W, EPIB>(e, qb[j], (int)(bytes[j] / 4), acc[j]);
+    for (int j = 0; j < KG; ++j) finish_piece<T, OP, A, V, 64 * W, EPIB, XL>(e, qb[j], (int)(bytes[j] / 4), acc[j]);
   }
   if constexpr (TR) {
     if (threadIdx.x == 0 && gi < 7) e.trace[blockIdx.x * 16 + 2 + 2 * gi] = wall_clock64();
@@ -1310,7 +1342,7 @@ __device__ __forceinline__ void rowmajor_group(const char* __restrict__ base, in
 // TR (tools/tune_reduce.hip set "timeline"): wave 0 of every block stamps the 100-MHz wall clock
 // at its start and at each group's sweep end and epilogue end into e.trace[block * 16 + slot].
 template <class P, typename T, int OP, int V, int D, int W, int KG, bool NT, int EPIB = (V >= 2 ? 2 : V),
-          bool TR = false>
+          bool TR = false, int XLM = -1>
 __global__ __launch_bounds__(64 * W) void reduce_kernel_rowmajor(const float* __restrict__ stack,
                                                                  int64_t stride, int n,
                                                                  const typename P::w_t* __restrict__ w,
@@ -1328,7 +1360,7 @@ __global__ __launch_bounds__(64 * W) void reduce_kernel_rowmajor(const float* __
     if (threadIdx.x == 0) e.trace[blockIdx.x * 16] = wall_clock64();
   }
 #define FA_RM_GROUP(KGX, G0, GI) \
-  rowmajor_group<P, T, OP, V, D, W, KGX, NT, EPIB, TR>(base, row_bytes, n, w, G0, k, pc, pieces, nquads, ncols, GI, e)
+  rowmajor_group<P, T, OP, V, D, W, KGX, NT, EPIB, TR, XLM>(base, row_bytes, n, w, G0, k, pc, pieces, nquads, ncols, GI, e)
   int gi = 0;
   for (int64_t g0 = 0; g0 < k; g0 += KG) FA_RM_GROUP(KG, g0, gi++);
 #undef FA_RM_GROUP

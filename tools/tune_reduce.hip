@@ -672,6 +672,21 @@ Variant make_narrow_lb(const float* stack, int64_t stride, int n, const float* w
           true, {}};
 }
 
+template <int V, int D, int W, int KG, int OP, typename T, int EPIB, int XLM>
+Variant make_rowmajor_xl(const float* stack, int64_t stride, int n, const float* w, int64_t ncols, Epi<T> e,
+                         double bytes, int64_t grid) {
+  const int64_t chunks = ((ncols + 3) / 4 + 63) / 64;
+  if (grid > chunks) grid = chunks;
+  char name[96];
+  snprintf(name, sizeof name, "rowmajor V%d W%d KG%d g%lld epib%d xl%d", V, W, KG, (long long)grid, EPIB, XLM);
+  return {name, bytes,
+          [=] {
+            hipLaunchKernelGGL((reduce_kernel_rowmajor<AccF32, T, OP, V, D, W, KG, true, EPIB, false, XLM>),
+                               dim3((unsigned)grid), dim3(64 * W), 0, 0, stack, stride, n, w, (int64_t)0, ncols, e);
+          },
+          true, {}};
+}
+
 template <int V, int D, int W, int KG, int OP, typename T, int EPIB = (V >= 2 ? 2 : V)>
 Variant make_rowmajor(const float* stack, int64_t stride, int n, const float* w, int64_t ncols, Epi<T> e,
                       double bytes, int64_t grid) {
@@ -998,6 +1013,25 @@ int main(int argc, char** argv) {
   vs.push_back(op == FA_OP_AVGM      ? make_narrow_lb<LB, D, FA_OP_AVGM, double>(stack, stride, n, w, ncols, e, bytes)   \
                : op == FA_OP_ADAGRAD ? make_narrow_lb<LB, D, FA_OP_ADAGRAD, double>(stack, stride, n, w, ncols, e, bytes) \
                                      : make_narrow_lb<LB, D, FA_OP_MEAN, double>(stack, stride, n, w, ncols, e, bytes))
+#define RMXL(KG, EB, XLM)                                                                                      \
+  vs.push_back(op == FA_OP_AVGM      ? make_rowmajor_xl<16, 1, 4, KG, FA_OP_AVGM, double, EB, XLM>(stack, stride, n, w, ncols, e, bytes, 192)   \
+               : op == FA_OP_ADAGRAD ? make_rowmajor_xl<16, 1, 4, KG, FA_OP_ADAGRAD, double, EB, XLM>(stack, stride, n, w, ncols, e, bytes, 192) \
+                                     : make_rowmajor_xl<16, 1, 4, KG, FA_OP_MEAN, double, EB, XLM>(stack, stride, n, w, ncols, e, bytes, 192))
+  if (!strcmp(set, "xl")) {  // whole-line f64 stores (LDS regrouping) off / on, the product geometry, each twice
+    const int64_t chunks = ((ncols + 3) / 4 + 63) / 64;
+    const int64_t k = (chunks + 192 * 64 - 1) / (192 * 64);
+    if (k % 3 == 0) {
+      RMXL(3, 4, 0);
+      RMXL(3, 4, 1);
+      RMXL(3, 4, 0);
+      RMXL(3, 4, 1);
+    } else {
+      RMXL(4, 4, 0);
+      RMXL(4, 4, 1);
+      RMXL(4, 4, 0);
+      RMXL(4, 4, 1);
+    }
+  }
   if (!strcmp(set, "nlb")) {  // narrow strips per wave (LB bytes per lane) vs the product's narrow kernel
     NARROW(40, 1);
     NARROW(32, 1);
