@@ -1017,6 +1017,27 @@ int main(int argc, char** argv) {
   vs.push_back(op == FA_OP_AVGM      ? make_rowmajor_xl<16, 1, 4, KG, FA_OP_AVGM, double, EB, XLM>(stack, stride, n, w, ncols, e, bytes, 192)   \
                : op == FA_OP_ADAGRAD ? make_rowmajor_xl<16, 1, 4, KG, FA_OP_ADAGRAD, double, EB, XLM>(stack, stride, n, w, ncols, e, bytes, 192) \
                                      : make_rowmajor_xl<16, 1, 4, KG, FA_OP_MEAN, double, EB, XLM>(stack, stride, n, w, ncols, e, bytes, 192))
+#define RMXLG(KG, EB, XLM, G)                                                                                      \
+  vs.push_back(op == FA_OP_AVGM      ? make_rowmajor_xl<16, 1, 4, KG, FA_OP_AVGM, double, EB, XLM>(stack, stride, n, w, ncols, e, bytes, G)   \
+               : op == FA_OP_ADAGRAD ? make_rowmajor_xl<16, 1, 4, KG, FA_OP_ADAGRAD, double, EB, XLM>(stack, stride, n, w, ncols, e, bytes, G) \
+                                     : make_rowmajor_xl<16, 1, 4, KG, FA_OP_MEAN, double, EB, XLM>(stack, stride, n, w, ncols, e, bytes, G))
+  if (!strcmp(set, "xlg")) {  // KG = 4 shapes: the product (KG 4, no XL) vs KG 3 with XL on a grid whose k splits in 3s
+    const int64_t chunks = ((ncols + 3) / 4 + 63) / 64;
+    int64_t g3 = 192;
+    for (int64_t gg = 184; gg <= 216; ++gg) {
+      const int64_t kk = (chunks + gg * 64 - 1) / (gg * 64);
+      if (kk % 3 == 0) { g3 = gg; break; }
+    }
+    printf("# KG 3 grid %lld\n", (long long)g3);
+    for (int rep = 0; rep < 2; ++rep) {
+      RMXL(4, 4, 0);
+      if (g3 == 192) { RMXLG(3, 4, 1, 192); RMXLG(3, 4, 0, 192); }
+      else if (g3 == 196) { RMXLG(3, 4, 1, 196); RMXLG(3, 4, 0, 196); }
+      else if (g3 == 200) { RMXLG(3, 4, 1, 200); RMXLG(3, 4, 0, 200); }
+      else if (g3 == 204) { RMXLG(3, 4, 1, 204); RMXLG(3, 4, 0, 204); }
+      else { RMXLG(3, 4, 1, 208); RMXLG(3, 4, 0, 208); }
+    }
+  }
   if (!strcmp(set, "xl")) {  // whole-line f64 stores (LDS regrouping) off / on, the product geometry, each twice
     const int64_t chunks = ((ncols + 3) / 4 + 63) / 64;
     const int64_t k = (chunks + 192 * 64 - 1) / (192 * 64);
