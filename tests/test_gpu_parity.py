@@ -287,9 +287,14 @@ def test_row_pipeline_deep_window_offsets(cuda):
         assert torch.equal(part, full[c0 : c0 + width]), c0
 
 
-@pytest.mark.parametrize("op", ["avgm", "adagrad"])
-def test_fused_epilogue_big_tiles(op, cuda):
-    n, p = 4, 8388608 + 5
+@pytest.mark.parametrize("dbuf", [False, True])
+@pytest.mark.parametrize("p", [5_000_003, 8388608 + 5, 18_000_007])
+@pytest.mark.parametrize("op", ["avgm", "adagrad", "yogi", "adam"])
+def test_fused_epilogue_big_tiles(op, p, dbuf, cuda):
+    """Fused f64 epilogues on row-major geometries of 2, 3 and 6 pieces per block (KG 2 / 3,
+    8 waves x 8 KiB and 4 waves x 16 KiB steps: the instances whose f64 stores are regrouped into
+    whole lines, DESIGN §4 finding 22), in place and double-buffered (v_out), against the C oracle."""
+    n = 4
     stride = -(-p // 64) * 64
     x = _device_stack(n, stride, seed=21)
     w = np.ones(n, np.float32)
@@ -299,12 +304,13 @@ def test_fused_epilogue_big_tiles(op, cuda):
     v = torch.full((p,), 0.25, dtype=torch.float64, device=cuda)
     v_h = v.cpu().numpy().copy()
     out64 = torch.empty(p, dtype=torch.float64, device=cuda)
+    v_out = torch.empty_like(v) if dbuf else None
     agg.reduce_stack(x, torch.from_numpy(w).to(cuda), na.MODE_W32_DIV64, float(n), n_cols=p, out64=out64,
-                     op=na.OP_BY_NAME[op], prev=prev[0], v=v)
+                     op=na.OP_BY_NAME[op], prev=prev[0], v=v, v_out=v_out)
     g = oracle.c_reduce(oracle.MODE_W32_DIV64, x[:, :p].cpu().numpy(), w, float(n))
     want = oracle.c_update(op, g, prev_h, v_h)
     assert bitwise_equal(out64.cpu().numpy(), want)
-    assert bitwise_equal(v.cpu().numpy(), v_h)
+    assert bitwise_equal((v_out if dbuf else v).cpu().numpy(), v_h)
 
 
 @pytest.mark.parametrize("col_begin", [0, 4, 64, 1000, 4096])
