@@ -57,11 +57,13 @@ sys.path.insert(0, str(REPO))
 
 from flearn_amd import _native as na  # noqa: E402
 from flearn_amd import aggregator as agg  # noqa: E402
-from flearn_amd import launch, layouts  # noqa: E402
+from flearn_amd import dist as fa_dist  # noqa: E402
+from flearn_amd import launch, layouts, verify  # noqa: E402
 from flearn_amd.dist import (ALIGN, PingPong, ShardedReducer, ShardPlan, StripeModel,  # noqa: E402
                              all_gather_into, hip_reduce_fn, shard_candidates)
 
 METRIC = "device-resident GiB/s, FedAVG N-client weighted tensor reduce; %HBM peak"
+UPLOAD_SEED, PREV_SEED = 2024, 1  # synthetic client uploads / previous global model
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
 GIB = 1024.0**3
 
@@ -155,20 +157,29 @@ class Job:
             + (f" + replicated tail {plan.rep}" if plan.rep else ""))
         self.stack = torch.empty((n, stride), dtype=torch.float32, device=dev)
         for lo, g0, width in plan.segments():
-            agg.fill_uniform(self.stack[:, lo:], seed=2024, row_begin=0, col_begin=g0, n_cols=width)
+            agg.fill_uniform(self.stack[:, lo:], seed=UPLOAD_SEED, row_begin=0, col_begin=g0, n_cols=width)
         self.weights = torch.ones(n, dtype=torch.float32, device=dev)  # Python 1.0 -> fl32(1.0)
-        denom = float(np.sum([1.0] * n))  # np.sum(agg_weight_lst), strategy.py:127
+        self.denom = float(np.sum([1.0] * n))  # np.sum(agg_weight_lst), strategy.py:127
+        self.reorder = reorder
         epi, state = {}, None
         if cfg["op"] != "mean":
             prev = torch.empty((1, stride), dtype=torch.float32, device=dev)
-            for lo, g0, width in plan.segments():
-                agg.fill_uniform(prev[:, lo:], seed=1, col_begin=g0, n_cols=width)
             # the fused step reads (prev, v_t) and writes the new global model and v_t into a
             # second pair, swapped every step — as the product's ServerOptimizer does
             state = PingPong(prev[0], torch.zeros(stride, dtype=torch.float64, device=dev))
+            self.reset_state(state)
             epi = dict(op=na.OP_BY_NAME[cfg["op"]], state=state)
-        self.fn = hip_reduce_fn(self.stack, self.weights, na.MODE_W32_DIV64, denom, reorder=reorder, **epi)
+        self.fn = hip_reduce_fn(self.stack, self.weights, na.MODE_W32_DIV64, self.denom, reorder=reorder, **epi)
         self.red = ShardedReducer(plan, self.fn, dev, gather=world > 1, state=state)
+
+    def reset_state(self, state=None):
+        """The fused optimizers' initial state: prev = the seed-1 synthetic model on this rank's
+        columns, v_t = 0 (np.zeros_like on first use, avgm.py:27 / opt.py:35)."""
+        st = state if state is not None else self.red.state
+        st.cur = 0
+        for lo, g0, width in self.plan.segments():
+            agg.fill_uniform(st.prev[0][lo:], seed=PREV_SEED, col_begin=g0, n_cols=width)
+        st.v[0].zero_()
 
     def release(self):
         self.stack = self.red = self.fn = None
@@ -306,6 +317,167 @@ def run_job(cfg, layout, n, args, world, rank, dev, g_eff):
     return job, step_s, wall, info
 
 
+def verify_job(job, cfg, world, dev) -> dict:
+    """After the timed region: prove the reassembled global model right (flearn_amd.verify).
+    Windows on every slice start / rank boundary / replicated-tail edge (>= 64) are regenerated
+    for all N clients and reduced UNSHARDED with the same kernel; the bucket the sharded step
+    returned (RCCL all-gather at N > 1) must match bit for bit, on every rank.  Fused configs
+    restart from the initial state and check the second step's model and every rank's own v_t
+    slices.  No oracle: the product kernel against itself."""
+    op = cfg["op"]
+    n, plan = job.n, job.plan
+    fused = op != "mean"
+    if fused:
+        job.reset_state()
+        job.red.step()
+    full = job.red.step()
+    torch.cuda.synchronize(dev)
+    state = job.red.state.v[job.red.state.cur] if fused else None
+    width = 4096
+    x = torch.empty((n, width), dtype=torch.float32, device=dev)
+    prev = torch.empty(width, dtype=torch.float32, device=dev)
+    v0 = torch.zeros(width, dtype=torch.float64, device=dev)
+    w1, v1, w2, v2 = (torch.empty(width, dtype=dt, device=dev) for dt in
+                      (torch.float32, torch.float64, torch.float32, torch.float64))
+    kw = dict(op=na.OP_BY_NAME[op]) if fused else {}
+
+    def expect(g0, w):
+        agg.fill_uniform(x, seed=UPLOAD_SEED, col_begin=g0, n_cols=w)
+        if not fused:
+            agg.reduce_stack(x, job.weights, na.MODE_W32_DIV64, job.denom, n_cols=w, out32=w2)
+            return w2, None
+        agg.fill_uniform(prev, seed=PREV_SEED, col_begin=g0, n_cols=w)
+        agg.reduce_stack(x, job.weights, na.MODE_W32_DIV64, job.denom, n_cols=w, out32=w1, prev=prev, v=v0,
+                         v_out=v1, **kw)
+        agg.reduce_stack(x, job.weights, na.MODE_W32_DIV64, job.denom, n_cols=w, out32=w2, prev=w1, v=v1,
+                         v_out=v2, **kw)
+        return w2, v2
+
+    compare = None
+    if job.reorder:  # the split-N order is not the list order: its documented bound instead
+        def compare(a, b):
+            a64, b64 = a.double(), b.double()
+            return bool(torch.linalg.vector_norm(a64 - b64) <= 1e-6 * torch.linalg.vector_norm(b64))
+    res = verify.check_step(plan, full, expect, state=state, width=width, compare=compare)
+    res["comparison"] = "<= 1e-6 normwise (--reorder)" if job.reorder else "bitwise"
+    res["what"] = ("the returned global bucket vs the unsharded same-kernel reduce of regenerated inputs, on "
+                   "windows at every stripe/rank slice boundary and replicated-tail edge"
+                   + (" (2nd step from the initial state; v_t on every rank's own slice edges)" if fused else ""))
+    return res
+
+
+def gather_probe(job, world, dev, reps: int = 5) -> dict:
+    """All-gather rate of this job's local width (RCCL over xGMI at N > 1), outside the timed
+    region: every GPU receives (world-1) slices, one over each peer link (one xGMI link per peer
+    on an MI355X node)."""
+    cols = job.plan.local_cols
+    src = job.red.local_out[:cols]
+    full = torch.empty(world * cols, dtype=torch.float32, device=dev)
+    for _ in range(2):
+        all_gather_into(full, src)
+    torch.cuda.synchronize(dev)
+    dist.barrier()
+    t = _max_over_ranks((_event_time(lambda: all_gather_into(full, src), reps),), world, dev)[0]
+    per_link = cols * 4 / t / 1e9
+    return {"cols_per_rank": cols, "us": round(t * 1e6, 2), "ingress_gbs_per_gpu": round(per_link * (world - 1), 2),
+            "per_link_gbs": round(per_link, 2)}
+
+
+def rccl_version() -> str | None:
+    try:
+        v = torch.cuda.nccl.version()
+        return ".".join(str(x) for x in v) if isinstance(v, tuple) else str(v)
+    except Exception:  # noqa: BLE001 - a build without RCCL: nothing to report
+        return None
+
+
+def loopback_multi_gpu(devices, rounds: int = 5, config: str = "c2") -> dict:
+    """flearn's in-process server on an N-GPU node: Communicator.run collects every upload in ONE
+    process (Communicator.py:127-141) and Server.ensemble calls strategy.server once
+    (Server.py:126-142), so the drop-in there is AVG(devices=[cuda:0..N-1]) — each GPU packs and
+    reduces its column share of the host uploads through its own PCIe link.  Times C2 loopback
+    (100 x ResNet-18 host numpy uploads with BN counters) for output="reference" (host float64
+    dict, the reference's types) and output="device" (tensors on cuda:0, peer copies over xGMI),
+    checks each result bit for bit against the one-device call on the same uploads, and reports
+    the per-GPU H2D rate of the pack phase."""
+    import flearn_amd
+
+    cfg = CONFIGS[config]
+    layout = layouts.get(cfg["layout"])
+    n, p = cfg["clients"], layouts.fp32_elems(layout)
+    d0 = devices[0]
+    x = torch.empty((n, p), dtype=torch.float32, device=d0)
+    agg.fill_uniform(x, seed=UPLOAD_SEED)
+    host = x.cpu().numpy()
+    del x
+    torch.cuda.empty_cache()
+    uploads = [{"agg_weight": 1.0, "params": layouts.synthetic_state_dict(layout, host[i], counter=100 + i)}
+               for i in range(n)]
+
+    def sync():
+        for d in set(devices):
+            torch.cuda.synchronize(d)
+
+    def host_of(v):
+        if isinstance(v, torch.Tensor):
+            return v.detach().cpu().numpy()
+        return np.asarray(v)
+
+    out = {"config": config, "clients": n, "params": p, "devices": [str(d) for d in devices],
+           "upload_bytes": int(host.nbytes)}
+    for output in ("reference", "device"):
+        one = flearn_amd.AVG(output=output, devices=[d0])
+        want = {k: host_of(v) for k, v in one.server(uploads, 0)["w_glob"].items()}
+        one = None
+        s = flearn_amd.AVG(output=output, devices=list(devices))
+        eng = s.engine
+        orig = eng.packer.pack
+        pack_t, ingest = [], {}
+
+        def pack(plan, w, orig=orig, pack_t=pack_t, ingest=ingest):
+            t0 = time.perf_counter()
+            stacks = orig(plan, w)
+            sync()
+            pack_t.append(time.perf_counter() - t0)
+            for parts in stacks.values():
+                for sh, st in parts:
+                    if isinstance(st, torch.Tensor):
+                        ingest[sh.index] = ingest.get(sh.index, 0) + n * sh.width * st.element_size()
+            return stacks
+
+        eng.packer.pack = pack
+        times, got = [], None
+        for r in range(rounds + 2):
+            t0 = time.perf_counter()
+            res = s.server(uploads, r)["w_glob"]
+            sync()
+            dt = time.perf_counter() - t0
+            if r >= 2:
+                times.append(dt)
+            if r == 0:
+                got = res
+        ok = set(got) == set(want) and all(
+            host_of(got[k]).dtype == want[k].dtype and host_of(got[k]).shape == want[k].shape
+            and host_of(got[k]).tobytes() == want[k].tobytes() for k in want)
+        calls = rounds + 2
+        per_dev = {i: b / calls for i, b in ingest.items()}
+        pk = float(np.median(pack_t[2:])) if len(pack_t) > 2 else float(np.median(pack_t))
+        out[output] = {
+            "round_ms": round(float(np.median(times)) * 1e3, 3),
+            "pack_h2d_ms": round(pk * 1e3, 3),
+            "h2d_gbs_per_gpu": [round(b / pk / 1e9, 2) for _, b in sorted(per_dev.items())],
+            "h2d_gbs_total": round(sum(per_dev.values()) / pk / 1e9, 2),
+            "verified": bool(ok),
+        }
+        eng.packer.pack = orig
+        s = eng = None
+        torch.cuda.empty_cache()
+    out["verified"] = all(out[o]["verified"] for o in ("reference", "device"))
+    out["what"] = ("AVG(devices=[...]).server(host uploads) per round (pack+H2D per GPU, reduce, D2H or device "
+                   "assembly), median of the rounds after 2 warm-up calls; bit-compared with the 1-device call")
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -325,6 +497,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--reorder", action="store_true",
                     help="allow the split-N kernel (deterministic, <= 1e-6 normwise, not bit-exact)")
+    ap.add_argument("--no-verify", action="store_true", help="skip the post-run check of the reassembled model")
+    ap.add_argument("--no-loopback", action="store_true",
+                    help="N>1: skip the single-process AVG(devices=[...]) loopback measurement")
     args = ap.parse_args()
 
     # one process per GPU: with no launcher env, --gpus N > 1 starts the N ranks here, BEFORE any
@@ -351,6 +526,16 @@ def main():
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group(backend)
+    if os.environ.get("FLEARN_BENCH_INJECT") == "gather_offset":
+        # rehearsal of a mis-gathering collective (tests/test_gpu_bench.py): every stripe's
+        # gathered range lands ALIGN columns late — the self-check must catch it and fail the run
+        real_gather = fa_dist.all_gather_into
+
+        def late_gather(dst, src, group=None, async_op=False):
+            real_gather(dst, src, group=group, async_op=False)
+            dst.copy_(torch.roll(dst, ALIGN))
+
+        fa_dist.all_gather_into = late_gather
 
     cfg = CONFIGS[args.config]
     layout = layouts.get(cfg["layout"])
@@ -361,7 +546,8 @@ def main():
     main_n = strong_n if args.scaling == "strong" else weak_n
 
     job, step_s, wall, info = run_job(cfg, layout, main_n, args, world, rank, dev, g_eff)
-    cols = job.plan.local_cols
+    plan = job.plan
+    cols = plan.local_cols
     job_bytes = algorithmic_bytes(main_n, p_real, cfg["op"])
     if emu:  # rank 0's columns only
         job_bytes = algorithmic_bytes(main_n, cols, cfg["op"])
@@ -389,6 +575,23 @@ def main():
     if traffic_src:
         roofline["traffic_source"] = traffic_src
 
+    check = None
+    if not args.no_verify:
+        log(f"[rank {rank}] verifying the reassembled model ...")
+        check = verify_job(job, cfg, world, dev)
+        if rank == 0:
+            log(f"[rank 0] verified={check['verified']} windows={check['windows']} "
+                f"mismatched={check['mismatched_windows']}")
+    if world > 1:
+        info["world_size"] = dist.get_world_size()
+        info["backend"] = dist.get_backend()
+        info["rccl_version"] = rccl_version() if backend == "nccl" else None
+        info["allgather_probe"] = gather_probe(job, world, dev)
+        cal = info.get("calibration")
+        if cal and cal.get("measured_gather"):
+            c_cols, g_us = cal["width_cols"][0], cal["gather_us"][0]
+            info["calibrated_per_link_gbs"] = round(c_cols * 4 / (g_us * 1e-6) / 1e9, 2) if g_us > 0 else None
+
     cpu = None
     if rank == 0 and g_eff == 1 and not args.no_cpu_baseline:
         sample = args.cpu_sample or min(main_n, 100)
@@ -409,6 +612,20 @@ def main():
             **oinfo,
         }
         ojob.release()
+
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    loop = None
+    if world > 1 and rank == 0 and not args.no_loopback:
+        # the single-process multi-GPU drop-in (flearn's Communicator collects every upload in one
+        # process): rank 0 alone, after the process group is gone, drives every GPU of the node
+        ndev = max(torch.cuda.device_count(), 1)
+        devices = [torch.device("cuda", i % ndev) for i in range(world)]
+        job.release()
+        job = None
+        log(f"[rank 0] loopback AVG(devices={[str(d) for d in devices]}) ...")
+        loop = loopback_multi_gpu(devices)
 
     if rank == 0:
         weak_main = args.scaling == "weak" and g_eff > 1
@@ -436,11 +653,11 @@ def main():
                 "order": ("split-N allowed (fixed-order tree of client splits, <= 1e-6 normwise)" if args.reorder
                           else "reference client order (bit-exact)"),
                 "parallelism": ("single GPU" if g_eff == 1 else
-                                f"element-range shards x{g_eff} + RCCL all-gather ({job.plan.stripes} stripes"
-                                + (f", widths {'/'.join(str(x) for x in job.plan.widths)}" if job.plan.stripes > 1
+                                f"element-range shards x{g_eff} + RCCL all-gather ({plan.stripes} stripes"
+                                + (f", widths {'/'.join(str(x) for x in plan.widths)}" if plan.stripes > 1
                                    else "")
-                                + (f"; the last {job.plan.rep} columns reduced by every rank, not gathered"
-                                   if job.plan.rep else "") + ")"
+                                + (f"; the last {plan.rep} columns reduced by every rank, not gathered"
+                                   if plan.rep else "") + ")"
                                 + (f"; EMULATED: rank 0's reduce of a {emu}-GPU job on one GPU, no gather"
                                    if emu else "")),
                 # `value` against the HBM peak of the GPUs that produced it (N x 8 TB/s; at N > 1
@@ -451,17 +668,24 @@ def main():
             },
             "roofline": roofline,
             "cpu_baseline": cpu,
+            "verify": check,
         }
         if g_eff > 1:
             line["multi_gpu"] = info
             if world > 1 and backend != "nccl":
                 line["multi_gpu"]["backend"] = f"{backend} (rehearsal: host-staged gather, not xGMI)"
+            if check is not None:
+                line["multi_gpu"]["verified"] = check["verified"]
+                line["multi_gpu"]["verified_windows"] = check["windows"]
             if other is not None:
                 line[other["scaling"]] = other
+        if loop is not None:
+            line["loopback_multi_gpu"] = loop
         print(json.dumps(line), flush=True)
-    if world > 1:
-        dist.barrier()
-        dist.destroy_process_group()
+    failed = (check is not None and not check["verified"]) or (loop is not None and not loop["verified"])
+    if failed:
+        log(f"[rank {rank}] SELF-CHECK FAILED: the reassembled global model differs from the unsharded reduce")
+        sys.exit(verify.EXIT_MISMATCH)
 
 
 if __name__ == "__main__":

@@ -48,6 +48,7 @@ def build_pyhost(force: bool = False, verbose: bool = False) -> Path:
 
 TORCHMETA_SOURCE = HERE / "csrc" / "fa_torchmeta.cpp"  # tensor-metadata walks (ctypes.PyDLL), not C ABI
 TORCHMETA_OUT = HERE / "lib" / "libfa_torchmeta.so"
+TORCHMETA_STAMP = HERE / "lib" / "libfa_torchmeta.stamp"  # sidecar: the stamp the .so was built with
 
 
 def torch_stamp() -> str:
@@ -83,8 +84,12 @@ def build_torchmeta(force: bool = False, verbose: bool = False):
 
     stamp = torch_stamp()
     newest = max(TORCHMETA_SOURCE.stat().st_mtime, Path(__file__).stat().st_mtime)
+    # the up-to-date check reads the sidecar stamp file, never the library itself: dlopening the
+    # old .so here would leave glibc's handle cached in this process, and a later load of the
+    # rebuilt file would get the stale one back (load_torchmeta then reads the old stamp)
+    side = TORCHMETA_STAMP
     if (TORCHMETA_OUT.exists() and not force and TORCHMETA_OUT.stat().st_mtime >= newest
-            and read_torchmeta_stamp() == stamp):
+            and side.exists() and side.read_text() == stamp):
         return TORCHMETA_OUT
     TORCHMETA_OUT.parent.mkdir(parents=True, exist_ok=True)
     tmp = TORCHMETA_OUT.with_suffix(".so.tmp")
@@ -102,9 +107,11 @@ def build_torchmeta(force: bool = False, verbose: bool = False):
     except (subprocess.CalledProcessError, OSError) as e:
         print(f"[flearn_amd] libfa_torchmeta.so not built ({e}); device uploads use the Python metadata path")
         TORCHMETA_OUT.unlink(missing_ok=True)
+        side.unlink(missing_ok=True)
         tmp.unlink(missing_ok=True)
         return None
     tmp.replace(TORCHMETA_OUT)
+    side.write_text(stamp)
     return TORCHMETA_OUT
 
 

@@ -46,7 +46,13 @@ def _epilogue(op: int, prev, v, beta=0.9, eta=1e-1, tau=1e-9, beta2=0.99, h=None
     return na.Epilogue(op, 0, _ptr(prev), _ptr(v), beta, eta, tau, beta2, _ptr(h), alpha, float(n_dyn), _ptr(v_out))
 
 
-def _check_v_out(v_out, v, ncols):
+def _byte_range(t: torch.Tensor, ncols: int):
+    return t.data_ptr(), t.data_ptr() + ncols * t.element_size()
+
+
+def _check_v_out(v_out, v, ncols, others=()):
+    """v_out (the updated v / theta) must not share a byte with v, nor with the other operands
+    the epilogue reads (prev, h): the kernel's stores would race its loads."""
     if v_out is None:
         return
     _check_cuda(v_out, "v_out", v.dtype)
@@ -54,6 +60,13 @@ def _check_v_out(v_out, v, ncols):
         raise ValueError("v_out too small or not contiguous")
     if v_out.data_ptr() == v.data_ptr():
         raise ValueError("v_out must be None (in place) or another buffer")
+    o0, o1 = _byte_range(v_out, ncols)
+    for name, t in (("v", v),) + tuple(others):
+        if t is None or ncols == 0:
+            continue
+        a0, a1 = _byte_range(t, ncols)
+        if o0 < a1 and a0 < o1:
+            raise ValueError(f"v_out overlaps {name}")
 
 
 # ---------------------------------------------------------------------------------------------
@@ -129,7 +142,7 @@ def reduce_stack(
         _check_cuda(v, "theta", vdt)
         if h.numel() < ncols or v.numel() < ncols:
             raise ValueError("h / theta too small")
-        _check_v_out(v_out, v, ncols)
+        _check_v_out(v_out, v, ncols, (("h", h),))
         epi = _epilogue(op, None, v, h=h, alpha=alpha, n_dyn=n, v_out=v_out)
     elif op != na.OP_MEAN:
         vdt = torch.float32 if mode == na.MODE_W32_DIV32 else torch.float64
@@ -137,7 +150,7 @@ def reduce_stack(
         _check_cuda(v, "v", vdt)
         if prev.numel() < ncols or v.numel() < ncols:
             raise ValueError("prev / v too small")
-        _check_v_out(v_out, v, ncols)
+        _check_v_out(v_out, v, ncols, (("prev", prev),))
         epi = _epilogue(op, prev, v, beta, eta, tau, beta2, v_out=v_out)
     if rows:
         pieces, npieces, grid = stack.piece_table(op)

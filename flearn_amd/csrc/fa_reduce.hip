@@ -323,8 +323,16 @@ int dispatch_op(int op, const typename P::x_t* stack, int64_t stride, int n, con
 
 bool aligned_to(const void* p, size_t a) { return ((uintptr_t)p % a) == 0; }
 
+// [a, a + bytes) and [b, b + bytes) share a byte
+bool overlaps(const void* a, const void* b, size_t bytes) {
+  const uintptr_t x = (uintptr_t)a, y = (uintptr_t)b;
+  return x < y + bytes && y < x + bytes;
+}
+
+// ncols: the columns the launch touches (0: unknown — only the exact-alias check applies)
 template <typename T>
-int make_epi(const fa_epilogue* in, double denom, int n_reduced, float* out32, double* out64, Epi<T>* e) {
+int make_epi(const fa_epilogue* in, double denom, int n_reduced, float* out32, double* out64, Epi<T>* e,
+             int64_t ncols = 0) {
   e->denom = (T)denom;
   e->prev = nullptr;
   e->v = nullptr;
@@ -341,7 +349,8 @@ int make_epi(const fa_epilogue* in, double denom, int n_reduced, float* out32, d
   e->v = static_cast<T*>(in->v);
   if (in->v_out) {
     if (!aligned_to(in->v_out, 4 * sizeof(T))) return fail(FA_ERR_ALIGN, "v_out must be 4-element aligned");
-    if (in->v_out == in->v) return fail(FA_ERR_ARG, "v_out must be NULL (in place) or another array");
+    if (in->v_out == in->v || (ncols > 0 && overlaps(in->v_out, in->v, (size_t)ncols * sizeof(T))))
+      return fail(FA_ERR_ARG, "v_out must be NULL (in place) or an array not overlapping v");
     e->v_out = static_cast<T*>(in->v_out);
   }
   if (in->op == FA_OP_DYN) {
@@ -419,19 +428,19 @@ int fa_reduce_f32(const float* stack, int64_t row_stride, int32_t n_clients, int
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (mode == FA_MODE_W32_DIV64) {
     Epi<double> e;
-    if ((rc = make_epi<double>(epi, denom, n_clients, out32, out64, &e))) return rc;
+    if ((rc = make_epi<double>(epi, denom, n_clients, out32, out64, &e, n_cols))) return rc;
     return dispatch_op<AccF32, double>(op, stack, row_stride, n_clients, weights, col_begin, n_cols,
                                        e, s);
   }
   if (mode == FA_MODE_W32_DIV32) {
     Epi<float> e;
-    if ((rc = make_epi<float>(epi, denom, n_clients, out32, out64, &e))) return rc;
+    if ((rc = make_epi<float>(epi, denom, n_clients, out32, out64, &e, n_cols))) return rc;
     return dispatch_op<AccF32, float>(op, stack, row_stride, n_clients, weights, col_begin, n_cols,
                                       e, s);
   }
   if (mode == FA_MODE_W64) {
     Epi<double> e;
-    if ((rc = make_epi<double>(epi, denom, n_clients, out32, out64, &e))) return rc;
+    if ((rc = make_epi<double>(epi, denom, n_clients, out32, out64, &e, n_cols))) return rc;
     return dispatch_op<AccF32W64, double>(op, stack, row_stride, n_clients, weights, col_begin,
                                           n_cols, e, s);
   }
@@ -451,17 +460,17 @@ int fa_reduce_f32_splitn(const float* stack, int64_t row_stride, int32_t n_clien
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (mode == FA_MODE_W32_DIV64) {
     Epi<double> e;
-    if ((rc = make_epi<double>(epi, denom, n_clients, out32, out64, &e))) return rc;
+    if ((rc = make_epi<double>(epi, denom, n_clients, out32, out64, &e, n_cols))) return rc;
     return dispatch_splitn<AccF32, double>(op, stack, row_stride, n_clients, weights, col_begin, n_cols, e, s);
   }
   if (mode == FA_MODE_W32_DIV32) {
     Epi<float> e;
-    if ((rc = make_epi<float>(epi, denom, n_clients, out32, out64, &e))) return rc;
+    if ((rc = make_epi<float>(epi, denom, n_clients, out32, out64, &e, n_cols))) return rc;
     return dispatch_splitn<AccF32, float>(op, stack, row_stride, n_clients, weights, col_begin, n_cols, e, s);
   }
   if (mode == FA_MODE_W64) {
     Epi<double> e;
-    if ((rc = make_epi<double>(epi, denom, n_clients, out32, out64, &e))) return rc;
+    if ((rc = make_epi<double>(epi, denom, n_clients, out32, out64, &e, n_cols))) return rc;
     return dispatch_splitn<AccF32W64, double>(op, stack, row_stride, n_clients, weights, col_begin, n_cols, e, s);
   }
   return fail(FA_ERR_ARG, "unknown reduce mode");
@@ -516,7 +525,7 @@ int fa_opt_apply(int32_t prec, const fa_epilogue* epi, const float* local, const
                      static_cast<const T*>(glob), n, e)
   if (prec == FA_PREC_F64) {
     Epi<double> e;
-    if ((rc = make_epi<double>(&local_epi, 1.0, 1, out32, out64, &e))) return rc;
+    if ((rc = make_epi<double>(&local_epi, 1.0, 1, out32, out64, &e, n))) return rc;
     switch (epi->op) {
       case FA_OP_AVGM: FA_APPLY(double, FA_OP_AVGM); break;
       case FA_OP_ADAGRAD: FA_APPLY(double, FA_OP_ADAGRAD); break;
@@ -526,7 +535,7 @@ int fa_opt_apply(int32_t prec, const fa_epilogue* epi, const float* local, const
     }
   } else if (prec == FA_PREC_F32) {
     Epi<float> e;
-    if ((rc = make_epi<float>(&local_epi, 1.0, 1, out32, out64, &e))) return rc;
+    if ((rc = make_epi<float>(&local_epi, 1.0, 1, out32, out64, &e, n))) return rc;
     switch (epi->op) {
       case FA_OP_AVGM: FA_APPLY(float, FA_OP_AVGM); break;
       case FA_OP_ADAGRAD: FA_APPLY(float, FA_OP_ADAGRAD); break;

@@ -9,6 +9,8 @@ from __future__ import annotations
 
 import concurrent.futures
 import ctypes
+import os
+import time
 
 import numpy as np
 import torch
@@ -24,7 +26,13 @@ _POOL = None
 def _pool() -> concurrent.futures.ThreadPoolExecutor:
     global _POOL
     if _POOL is None:
-        _POOL = concurrent.futures.ThreadPoolExecutor(8, thread_name_prefix="fa-update")
+        # the pack is host-memory copies (the GIL released): as many threads as the process may
+        # use, up to 16 (the GPU box's CPU share per GPU)
+        try:
+            cpus = len(os.sched_getaffinity(0))
+        except (AttributeError, OSError):
+            cpus = os.cpu_count() or 8
+        _POOL = concurrent.futures.ThreadPoolExecutor(max(4, min(16, cpus)), thread_name_prefix="fa-update")
     return _POOL
 
 
@@ -78,11 +86,16 @@ class _DictPack:
 
 class DeviceUpdater:
     #: zero-copy, chunked: the update kernel reads w_local / w_glob from the pinned staging and
-    #: writes the result into pinned memory over PCIe, one chunk of keys at a time, while the
-    #: pool packs the next chunk and copies finished chunks out (False: pack everything, two H2D
-    #: copies, one launch, one D2H; tools/bench_client_update.py --ab times both)
+    #: writes the result straight into a fresh pinned buffer over PCIe, one chunk of keys at a
+    #: time, while the pool packs the next chunk; the new w_local values are views of that buffer
+    #: (no copy-out).  False: pack everything, two H2D copies, one launch, one D2H, a host copy
+    #: out; tools/bench_client_update.py --ab times both
     zero_copy = True
-    chunk_bytes = 32 << 20  # w_glob bytes per zero-copy chunk
+    chunk_bytes = 32 << 20  # w_glob bytes per zero-copy chunk (the middle ones)
+    first_chunk_bytes = 4 << 20  # the first chunks grow from this (x2 each) so the GPU starts early
+    last_chunk_bytes = 8 << 20  # ... and the last ones shrink towards this: a short exposed tail
+    #: a list to receive per-call phase times (tools/bench_client_update.py --phases), or None
+    trace = None
 
     def __init__(self, op: str, device=None, beta=0.9, eta=1e-1, tau=1e-9, beta2=0.99):
         self.op = na.OP_BY_NAME[op]
@@ -90,6 +103,7 @@ class DeviceUpdater:
         self.params = dict(beta=beta, eta=eta, tau=tau, beta2=beta2)
         self.layout = None  # [(key, shape, offset, numel)]
         self.v = None
+        self._v_next = None  # the zero-copy path's second v_t buffer (double-buffered: all or nothing)
         self.v_host = {}  # v_t of the keys computed on the host (integer buffers, scalars)
         self._stage = None  # pinned staging of the current layout (local, global, result)
 
@@ -105,7 +119,7 @@ class DeviceUpdater:
     def reset(self):
         """Forget v_t (device and host keys): the next call starts from zeros, as a fresh
         strategy object would."""
-        self.layout, self.v, self._stage, self.v_host = None, None, None, {}
+        self.layout, self.v, self._v_next, self._stage, self.v_host = None, None, None, None, {}
 
     def state(self):
         """v_t as the reference exposes it: {key: ndarray}."""
@@ -183,11 +197,15 @@ class DeviceUpdater:
         if self.v is None:
             self.layout = lay
             self.v = torch.zeros(total, dtype=tdt, device=dev)  # np.zeros_like(delta) on first use
+            self._v_next = None
             self._stage = None
         st = self._staging(lay, total, tdt, dev)
         if self.zero_copy:
             return self._device_step_zc(w_local, glob, local, lay, total, tdt, dev, **override)
         lh, gh, oh, pack_l, pack_g = st
+        if oh is None:  # staging made for the zero-copy path: the copy-engine path needs a result buffer
+            oh = torch.empty(total, dtype=tdt, pin_memory=True)
+            self._stage = (lh, gh, oh, pack_l, pack_g)
         with torch.cuda.device(dev):
             # local -> pinned -> device, then the global model while the local one is in flight
             if not pack_l(local):
@@ -222,11 +240,26 @@ class DeviceUpdater:
         lh, gh = self._stage[0], self._stage[1]
         gdt = np.float64 if tdt == torch.float64 else np.float32
         item = np.dtype(gdt).itemsize
+        # target sizes: first_chunk_bytes doubling up to chunk_bytes, then chunk_bytes, and the
+        # last ones halving down to last_chunk_bytes (the exposed ends of the pipeline: the first
+        # chunk's pack before the GPU starts, the last chunk's kernel after the pack is done)
+        total_b = sum(e[3] for e in lay) * item
+        head, b = [], max(1, int(self.first_chunk_bytes))
+        while b < self.chunk_bytes and sum(head) + b < total_b:
+            head.append(b)
+            b *= 2
+        tail, b = [], max(1, int(self.last_chunk_bytes))
+        while b < self.chunk_bytes and sum(head) + sum(tail) + b < total_b:
+            tail.append(b)
+            b *= 2
+        tail.reverse()
+        mid = max(0, total_b - sum(head) - sum(tail))
+        targets = head + [self.chunk_bytes] * max(1, -(-mid // max(1, self.chunk_bytes))) + tail
         groups, cur, size = [], [], 0
         for e in lay:
             cur.append(e)
             size += e[3] * item
-            if size >= self.chunk_bytes:
+            if size >= targets[min(len(groups), len(targets) - 1)]:
                 groups.append(cur)
                 cur, size = [], 0
         if cur:
@@ -241,45 +274,55 @@ class DeviceUpdater:
         return out
 
     def _device_step_zc(self, w_local, glob, local, lay, total, tdt, dev, **override):
+        """All or nothing: v_t advances into the second buffer, which becomes v_t only after
+        every chunk ran; on any error the queued chunks are waited for (they read the staging
+        the next call repacks) and v_t, the staging and w_local are as before the call."""
         from ..aggregator import _epilogue
 
-        lh, gh, oh = self._stage[0], self._stage[1], self._stage[2]
+        lh, gh = self._stage[0], self._stage[1]
         L = na.lib()
         prec = na.PREC_F64 if tdt == torch.float64 else na.PREC_F32
         p = dict(self.params, **override)
-        src = oh.numpy()
-        fresh = np.empty(total, dtype=src.dtype)
+        if self._v_next is None or self._v_next.shape != self.v.shape or self._v_next.dtype != self.v.dtype:
+            self._v_next = torch.empty_like(self.v)
+        v_in, v_out = self.v, self._v_next
+        # the new w_local lives in a fresh pinned buffer the kernel writes over PCIe; the values
+        # handed out are views of it (torch's host caching allocator recycles it once they die)
+        res = torch.empty(total, dtype=tdt, pin_memory=True)
+        tr = [] if self.trace is not None else None
+        t0 = time.perf_counter()
         with torch.cuda.device(dev):
             stream = torch.cuda.current_stream(dev)
             sh = stream.cuda_stream
-            events = []
-            for first, end, pack_l, pack_g, g in self._chunks(lay, total, tdt):
-                tl, tg = pack_l.tasks(local), pack_g.tasks(glob)
-                rc = _run(tl + tg)
-                if any(rc[: len(tl)]):  # a value the native pack refuses: copy in Python
-                    for k, s, o, n in g:
-                        lh.numpy()[o : o + n] = local[k].reshape(-1)
-                if any(rc[len(tl) :]):
-                    for k, s, o, n in g:
-                        gh.numpy()[o : o + n] = glob[k].reshape(-1)
-                n = end - first
-                epi = _epilogue(self.op, lh[first:end], self.v[first:end], p["beta"], p["eta"], p["tau"], p["beta2"])
-                out = oh[first:end].data_ptr()
-                na.check(L.fa_opt_apply(prec, ctypes.byref(epi), lh[first:end].data_ptr(), gh[first:end].data_ptr(), n,
-                                        None if prec == na.PREC_F64 else out, out if prec == na.PREC_F64 else None, sh),
-                         "fa_opt_apply")
-                ev = torch.cuda.Event()
-                ev.record(stream)
-                events.append((ev, first, end))
-            # finished chunks leave the pinned result while later chunks are still on the GPU
-            futs = []
-            step = 1 << 22
-            for ev, first, end in events:
-                ev.synchronize()
-                futs += [_pool().submit(lambda a=a, b=min(a + step, end): np.copyto(fresh[a:b], src[a:b]))
-                         for a in range(first, end, step)]
-            for f in futs:
-                f.result()
+            try:
+                for first, end, pack_l, pack_g, g in self._chunks(lay, total, tdt):
+                    tp = time.perf_counter()
+                    tl, tg = pack_l.tasks(local), pack_g.tasks(glob)
+                    rc = _run(tl + tg)
+                    if any(rc[: len(tl)]):  # a value the native pack refuses: copy in Python
+                        for k, s, o, n in g:
+                            lh.numpy()[o : o + n] = local[k].reshape(-1)
+                    if any(rc[len(tl) :]):
+                        for k, s, o, n in g:
+                            gh.numpy()[o : o + n] = glob[k].reshape(-1)
+                    n = end - first
+                    epi = _epilogue(self.op, lh[first:end], v_in[first:end], p["beta"], p["eta"], p["tau"], p["beta2"],
+                                    v_out=v_out[first:end])
+                    out = res[first:end].data_ptr()
+                    na.check(L.fa_opt_apply(prec, ctypes.byref(epi), lh[first:end].data_ptr(), gh[first:end].data_ptr(),
+                                            n, None if prec == na.PREC_F64 else out,
+                                            out if prec == na.PREC_F64 else None, sh), "fa_opt_apply")
+                    if tr is not None:
+                        tr.append((end - first, tp - t0, time.perf_counter() - t0))
+            except BaseException:
+                stream.synchronize()  # no queued chunk may still read the staging or write `res`
+                raise
+            ts = time.perf_counter()
+            stream.synchronize()
+        self.v, self._v_next = v_out, v_in
+        if tr is not None:
+            self.trace.append({"chunks": tr, "launched_s": ts - t0, "done_s": time.perf_counter() - t0})
+        fresh = res.numpy()
         for k, s, o, n in lay:  # replaced per key, like the reference (avgm.py:34-35, opt.py:62-63)
             w_local[k] = fresh[o : o + n].reshape(s)
 
@@ -289,7 +332,7 @@ class DeviceUpdater:
         if getattr(self, "_stage", None) is None:
             lh = torch.zeros(total, dtype=torch.float32, pin_memory=True)
             gh = torch.zeros(total, dtype=tdt, pin_memory=True)
-            oh = torch.empty(total, dtype=tdt, pin_memory=True)
+            oh = None if self.zero_copy else torch.empty(total, dtype=tdt, pin_memory=True)
             gdt = np.float64 if tdt == torch.float64 else np.float32
             self._stage = (lh, gh, oh, _DictPack(lay, np.float32, lh.data_ptr()), _DictPack(lay, gdt, gh.data_ptr()))
         return self._stage

@@ -27,11 +27,18 @@ import torch.distributed as _dist
 
 from .._native import NativeError, NativeUnavailable
 
-#: exceptions that mean "the device or the environment failed", re-raised as they are; every
-#: other exception (NotImplementedError for unsupported client data included) takes the
-#: reference's server_exception -> SystemExit route
+#: exceptions that mean "the device or the environment failed", re-raised as they are (they are
+#: RuntimeErrors; listed so that the NotImplementedError subclass test below cannot catch them)
 _DEVICE_ERRORS = (NativeUnavailable, NativeError, torch.OutOfMemoryError, torch.AcceleratorError,
                   _dist.DistError)
+#: what bad client data raises — numpy's errors on the reference's arithmetic (shape/dtype/key
+#: mismatches, an empty list), the engine's own validation (bucket.py / semantics.py) and the
+#: deliberate refusals of unsupported client data (NotImplementedError): these take the
+#: reference's server_exception -> SystemExit route (avg.py:28-31).  Everything else — a plain
+#: RuntimeError from a gloo/c10d collective (timeout, dead peer), a device-placement error,
+#: OSError, ... — is a device or environment failure and propagates unchanged.
+_CLIENT_DATA_ERRORS = (ValueError, TypeError, LookupError, AttributeError, ArithmeticError,
+                       NotImplementedError, SystemError)
 
 
 class BaseEncrypt:
@@ -112,7 +119,7 @@ class Strategy(ABC):
             # errors, a failed collective: a device or environment problem, not bad client data —
             # never turned into the "check that the client model parameters are valid" exit
             raise
-        except Exception as e:  # the reference's convention (avg.py:28-31) for what numpy would raise
+        except _CLIENT_DATA_ERRORS as e:  # the reference's convention (avg.py:28-31)
             self.server_exception(e)
 
     @abstractmethod

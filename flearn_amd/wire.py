@@ -246,7 +246,9 @@ def restricted_loads(data) -> object:
 # pinned rows handed out by decode (weakly tracked, verified by address before reuse)
 # ---------------------------------------------------------------------------------------------
 _ROWS: dict[int, tuple] = {}
-_ROWS_LOCK = threading.Lock()
+# re-entrant: a row's weakref callback (_drop_entry) may run from the garbage collector while
+# this thread already holds the lock
+_ROWS_LOCK = threading.RLock()
 
 
 class _RowArray(np.ndarray):
@@ -259,11 +261,47 @@ def _register(params: dict, row_np: _RowArray, layout: tuple, staged=None):
     # the exact array objects handed out, weakly: wire_row then checks identity (an array that was
     # replaced is a different object; an array cannot move, so identity pins its address too)
     refs = tuple(weakref.ref(params[k]) for k, _, _ in layout[:-1])
+    key = id(params)
     with _ROWS_LOCK:
         if len(_ROWS) > 4096:
-            for k in [k for k, ent in _ROWS.items() if ent[0]() is None]:
+            for k in [k for k, ent in _ROWS.items() if not _entry_alive(ent)]:
                 del _ROWS[k]
-        _ROWS[id(params)] = (weakref.ref(row_np), layout, staged, refs)
+        # the entry goes when its row dies (a params dict cannot be weakly referenced, so a dict
+        # freed while its arrays live on leaves the entry behind: _live_entry drops it on lookup)
+        _ROWS[key] = (weakref.ref(row_np, lambda r, k=key: _drop_entry(k, r)), layout, staged, refs)
+
+
+def _entry_alive(ent) -> bool:
+    return ent[0]() is not None and all(r() is not None for r in ent[3])
+
+
+def _drop_entry(key: int, row_ref) -> None:
+    with _ROWS_LOCK:
+        ent = _ROWS.get(key)
+        if ent is not None and ent[0] is row_ref:
+            del _ROWS[key]
+
+
+def _live_entry(params: dict):
+    """The registry entry of this exact params dict, or None.  An entry is trusted only while its
+    row and every array it handed out are alive AND are the ones the dict holds now: a dict at a
+    reused id() (an earlier upload's dict freed, a new one allocated at the same address) never
+    matches, and its stale entry is dropped here."""
+    key = id(params)
+    with _ROWS_LOCK:
+        ent = _ROWS.get(key)
+        if ent is None:
+            return None
+        if not _entry_alive(ent):
+            del _ROWS[key]
+            return None
+    for (k, _shape, _off), ref in zip(ent[1][:-1], ent[3]):
+        if params.get(k) is not ref():
+            with _ROWS_LOCK:
+                if _ROWS.get(key) is ent:
+                    del _ROWS[key]
+            return None
+    return ent
 
 
 class _DeviceStage:
@@ -340,7 +378,7 @@ def wire_device_stack(params_list, layout: tuple, device):
     """The staged device stack [N, stride] of these decoded uploads when every one was staged,
     in list order, into slots 0..N-1 of the same round on `device` and still holds the decoder's
     arrays — else None (the caller then DMAs the pinned rows or packs)."""
-    ents = [_ROWS.get(id(p)) for p in params_list]
+    ents = [_live_entry(p) for p in params_list]
     stages = {e[2][0] for e in ents if e is not None and e[2] is not None}
     ok = bool(ents) and len(stages) == 1 and all(e is not None and e[2] is not None for e in ents)
     if ok:
@@ -359,17 +397,11 @@ def wire_device_stack(params_list, layout: tuple, device):
 def wire_row(params: dict, layout: tuple):
     """The pinned row behind a decoded upload's params when its fp32 arrays are still the
     decoder's views laid out as `layout` ((key, shape, offset), ..., stride) — else None."""
-    ent = _ROWS.get(id(params))
-    if ent is None:
+    ent = _live_entry(params)
+    if ent is None or ent[1] != layout:
         return None
     row_np = ent[0]()
-    if row_np is None or ent[1] != layout:
-        return None
-    for (key, _shape, _off), ref in zip(layout[:-1], ent[3]):
-        a = params.get(key)
-        if a is None or a is not ref():
-            return None
-    return row_np._fa_tensor
+    return None if row_np is None else row_np._fa_tensor
 
 
 # ---------------------------------------------------------------------------------------------

@@ -114,6 +114,18 @@ def test_unknown_mode_and_op(L):
     assert rc == header_define("FA_ERR_ARG")
 
 
+def test_v_out_overlapping_v_is_refused(L):
+    """v_out may not share a byte with v over the launch's columns (a shifted view would race the
+    epilogue's loads); the exact alias was refused already."""
+    for shift in (0, 4, 8 * 4):  # f64 elements: same address, half a quad later, 4 quads later
+        epi = na.Epilogue(na.OP_AVGM, 0, FAKE, FAKE, 0.9, 0.1, 1e-9, 0.99, None, 0, 0, FAKE + 8 * shift)
+        rc = L.fa_reduce_f32(FAKE, 4096, 2, 0, FAKE, 1.0, 0, 1024, ctypes.byref(epi), FAKE, None, None)
+        assert rc == header_define("FA_ERR_ARG") and b"overlap" in L.fa_last_error() or shift == 0, shift
+        assert rc == header_define("FA_ERR_ARG")
+        rc = L.fa_opt_apply(na.PREC_F64, ctypes.byref(epi), FAKE, FAKE, 1024, None, FAKE, None)
+        assert rc == header_define("FA_ERR_ARG")
+
+
 def test_empty_window_is_a_no_op(L):
     assert L.fa_reduce_f32(FAKE, 64, 2, 0, FAKE, 1.0, 0, 0, None, FAKE, None, None) == 0
     assert L.fa_reduce_f64(FAKE, 64, 2, FAKE, 1.0, 0, 0, FAKE, None) == 0

@@ -23,14 +23,20 @@ def _free_port():
         return s.getsockname()[1]
 
 
+def _rehearse(config, extra=(), inject=None):
+    env = dict(os.environ, FLEARN_BENCH_BACKEND="gloo", MASTER_ADDR="127.0.0.1", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    if inject:
+        env["FLEARN_BENCH_INJECT"] = inject
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", str(REPO / "bench.py"), "--gpus", "2",
+           "--steps", "3", "--warmup", "1", "--config", config, *extra]
+    return subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=280, cwd=str(REPO))
+
+
 @pytest.mark.timeout(300)
 @pytest.mark.parametrize("config", ["c2", "c3"])
 def test_bench_two_ranks_rehearsal(config, cuda):
-    env = dict(os.environ, FLEARN_BENCH_BACKEND="gloo", MASTER_ADDR="127.0.0.1", HSA_ENABLE_IPC_MODE_LEGACY="0")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
-           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", str(REPO / "bench.py"), "--gpus", "2",
-           "--steps", "3", "--warmup", "1", "--config", config]
-    p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=280, cwd=str(REPO))
+    p = _rehearse(config)
     assert p.returncode == 0, p.stderr[-4000:]
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, p.stdout  # rank 0 prints one line
@@ -50,3 +56,41 @@ def test_bench_two_ranks_rehearsal(config, cuda):
     assert (best["stripe_widths"], best["replicated_cols"]) == (mg["stripe_widths"], mg["replicated_cols"])
     assert d["weak"]["clients"] == 200 and d["weak"]["value"] > 0
     assert d["roofline"]["bound"] == "hbm" and d["roofline"]["frac"] > 0
+    # the reassembled model was checked bit for bit on >= 64 boundary windows, on both ranks
+    v = d["verify"]
+    assert v["verified"] is True and v["windows"] >= 64 and v["ranks_checked"] == 2 and v["comparison"] == "bitwise"
+    assert v["mismatched_windows"] == 0 and (v["state_windows"] > 0) == (config == "c3")
+    assert mg["verified"] is True and mg["verified_windows"] == v["windows"]
+    assert mg["world_size"] == 2 and mg["backend"].startswith("gloo") and mg["allgather_probe"]["per_link_gbs"] > 0
+    assert mg["calibrated_per_link_gbs"] > 0
+    # the single-process multi-GPU drop-in, rehearsed as devices=[cuda:0, cuda:0]
+    lb = d["loopback_multi_gpu"]
+    assert lb["verified"] is True and lb["devices"] == ["cuda:0", "cuda:0"] and lb["clients"] == 100
+    for o in ("reference", "device"):
+        assert lb[o]["verified"] is True and lb[o]["round_ms"] > 0 and lb[o]["pack_h2d_ms"] > 0
+        assert len(lb[o]["h2d_gbs_per_gpu"]) == 2 and min(lb[o]["h2d_gbs_per_gpu"]) > 0
+
+
+@pytest.mark.timeout(300)
+def test_bench_fails_on_a_misplaced_gather(cuda):
+    """FLEARN_BENCH_INJECT=gather_offset: every gathered slice lands ALIGN columns late; the
+    self-check must flag it in the line and the run must exit non-zero (EXIT_MISMATCH)."""
+    from flearn_amd import verify
+
+    p = _rehearse("c2", ("--no-weak", "--no-loopback", "--stripes", "2"), inject="gather_offset")
+    assert p.returncode != 0, p.stdout[-2000:]
+    assert "SELF-CHECK FAILED" in p.stderr
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d["verify"]["verified"] is False and d["verify"]["mismatched_windows"] > 0
+    assert verify.EXIT_MISMATCH == 3
+
+
+def test_single_gpu_line_is_verified(cuda):
+    """The default N=1 line checks its own output too (one launch, no gather)."""
+    p = subprocess.run([sys.executable, str(REPO / "bench.py"), "--steps", "3", "--warmup", "1", "--config", "c3",
+                        "--no-cpu-baseline"], capture_output=True, text=True, timeout=280, cwd=str(REPO))
+    assert p.returncode == 0, p.stderr[-3000:]
+    d = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][0])
+    assert d["verify"]["verified"] is True and d["verify"]["windows"] >= 64 and d["verify"]["state_windows"] >= 2

@@ -1003,6 +1003,53 @@ def test_client_side_update_large_and_fallback_values(op, mode, cuda, monkeypatc
             prev["c"] = np.asfortranarray(prev["c"])
 
 
+@pytest.mark.parametrize("op", ["avgm", "adagrad"])
+def test_client_side_update_failure_mid_call_changes_nothing(op, cuda, monkeypatch):
+    """a zero-copy chunked update that fails on a later chunk (chunks before it already
+    queued) must leave v_t and w_local as they were — v_t is double-buffered and swapped only
+    after every chunk ran, and the queued chunks are waited for before the error propagates — so
+    retrying the round gives the reference's result."""
+    from flearn_amd import aggregator
+    from flearn_amd.strategy._update import DeviceUpdater
+
+    monkeypatch.setattr(DeviceUpdater, "zero_copy", True)
+    monkeypatch.setattr(DeviceUpdater, "chunk_bytes", 1 << 20)
+    rng = np.random.default_rng(5)
+    shapes = {"a": (512, 1024), "b": (3000,), "c": (300, 700), "d": (4096,)}
+    prev = {k: rng.standard_normal(sh).astype(np.float32) for k, sh in shapes.items()}
+    s = AVGM() if op == "avgm" else OPT()
+    v = None
+    real = aggregator._epilogue
+    for r in range(3):
+        glob = {k: rng.standard_normal(sh) for k, sh in shapes.items()}
+        if r == 1:
+            calls = {"n": 0}
+
+            def failing(*a, **k):
+                calls["n"] += 1
+                if calls["n"] == 3:
+                    raise ValueError("refused chunk")
+                return real(*a, **k)
+
+            monkeypatch.setattr(aggregator, "_epilogue", failing)
+            wl = dict(prev)
+            with pytest.raises(ValueError, match="refused chunk"):
+                s.mean_momentum(wl, glob, 0.9) if op == "avgm" else s.adaptive_opt(wl, glob, op)
+            assert calls["n"] == 3 and all(wl[k] is prev[k] for k in prev)
+            monkeypatch.setattr(aggregator, "_epilogue", real)
+            if v is not None:
+                assert_dict_bitwise(s.v_t, v, f"{op} v after the failed call")
+        if op == "avgm":
+            want, v = oracle.mean_momentum(prev, glob, v, 0.9)
+            got = s.mean_momentum(dict(prev), glob, 0.9)
+        else:
+            want, v = oracle.adaptive_opt(prev, glob, v, op)
+            got = s.adaptive_opt(dict(prev), glob, op)
+        assert_dict_bitwise(got, want, f"{op} w{r}")
+        assert_dict_bitwise(s.v_t, v, f"{op} v{r}")
+        prev = {k: np.asarray(got[k]).astype(np.float32) for k in shapes}
+
+
 @pytest.mark.parametrize("op", ["avgm", "adagrad", "adam"])
 def test_client_side_update_bn_model(op, cuda):
     """A BatchNorm model: the server's w_glob holds np.float64 scalars for the int64

@@ -183,6 +183,34 @@ def test_product_path_fails_loudly_without_gpu():
         flearn_amd.AVG().server(ups, 0)
 
 
+@pytest.mark.parametrize("exc,exits", [
+    (ValueError("shape mismatch"), True), (TypeError("dtype"), True), (KeyError("w"), True),
+    (IndexError("list index out of range"), True), (NotImplementedError("sparse uploads"), True),
+    (RuntimeError("[gloo/transport/tcp/pair.cc] Connection closed by peer"), False),
+    (RuntimeError("Expected all tensors to be on the same device"), False),
+    (torch.distributed.DistBackendError("Watchdog caught collective operation timeout"), False),
+    (na.NativeError("hipErrorLaunchFailure"), False), (OSError("pinned alloc"), False),
+])
+def test_only_client_data_errors_take_server_exception(exc, exits):
+    """avg.py:28-31 turns what numpy would raise on bad uploads into SystemExit; a failed
+    collective of a group= round (a plain RuntimeError from gloo/c10d), a device-placement error
+    or a HIP failure is not bad client data and must propagate unchanged."""
+    class Engine:
+        def ensemble(self, *a, **k):
+            raise exc
+
+    s = flearn_amd.AVG()
+    s._engine = Engine()
+    ups = [{"agg_weight": 1.0, "params": {"w": np.ones(4, np.float32)}}]
+    if exits:
+        with pytest.raises(SystemExit):
+            s.server(ups, 0)
+    else:
+        with pytest.raises(type(exc)) as info:
+            s.server(ups, 0)
+        assert info.value is exc
+
+
 def test_product_never_imports_the_oracle():
     code = "import sys, flearn_amd, flearn_amd.aggregator, flearn_amd.dist; print('oracle' in sys.modules)"
     out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True,

@@ -1,5 +1,7 @@
 """Host: the tensor-metadata walks (csrc/fa_torchmeta.cpp) agree with the Python comparisons they
 replace (bucket._raw_signature / Packer.row_table), and fall back instead of raising."""
+from pathlib import Path
+
 import numpy as np
 import pytest
 import torch
@@ -89,10 +91,11 @@ def test_sparse_and_storage_less_values_fall_back(L):
 
 
 @pytest.mark.gpu
-def test_sparse_device_value_falls_back(L):
+@pytest.mark.gpu
+def test_sparse_device_value_falls_back(L, cuda):
     """A sparse CUDA tensor passes the dtype and device checks: the layout check must refuse it
     before is_contiguous() (which throws for sparse tensors) is reached."""
-    dev = torch.device("cuda", 0)
+    dev = cuda
     cs = [{k: v.to(dev) for k, v in c.items()} for c in _clients()]
     keys = ("a.weight", "a.bias")
     ptrs = np.zeros((2, len(cs)), np.int64)
@@ -101,3 +104,18 @@ def test_sparse_device_value_falls_back(L):
     assert L.fa_tm_tensor_ptrs(cs, keys, dts, 0, ptrs.ctypes.data, keep) == 0
     cs[3]["a.bias"] = torch.zeros(3, device=dev).to_sparse()
     assert L.fa_tm_tensor_ptrs(cs, keys, dts, 0, ptrs.ctypes.data, keep) == 1
+
+
+def test_up_to_date_check_never_loads_the_library():
+    """build_torchmeta decides "up to date" from the sidecar stamp file: the building process
+    must not dlopen the old library (glibc would hand that cached handle to the later load of the
+    rebuilt file, and load_torchmeta would read the stale stamp)."""
+    import subprocess
+    import sys
+
+    code = ("from flearn_amd import _build; _build.build_torchmeta(); "
+            "print(any('libfa_torchmeta' in l for l in open('/proc/self/maps')))")
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True,
+                         cwd=str(Path(__file__).resolve().parent.parent))
+    assert out.returncode == 0, out.stderr
+    assert out.stdout.strip().splitlines()[-1] == "False"

@@ -332,7 +332,54 @@ def test_repeated_key_in_pickled_params_decodes_like_pickle():
     assert list(want["params"]) == ["wq"] and want["params"]["wq"].shape == (500,)
     got = wire.Encrypt(fast_min_chars=0).decode(base64.b64encode(raw).decode())
     same(got, want)
-    assert id(got["params"]) not in wire._ROWS  # not handed to the engine as a pinned row
+    assert wire._live_entry(got["params"]) is None  # not handed to the engine as a pinned row
+
+
+def test_reused_dict_id_never_finds_a_stale_row():
+    """A decoded upload's params dict is freed while its arrays live on; a new dict allocated at
+    the same id() must not be taken for it (the registry is keyed by id(), dicts cannot be weakly
+    referenced): the stale entry is dropped on lookup, and a row that dies takes its entry along."""
+    import gc
+
+    rng = np.random.default_rng(5)
+    obj = {"agg_weight": 1.0, "params": {"a": rng.random(700, dtype=np.float32),
+                                         "b": rng.random(300, dtype=np.float32)}}
+    text = base64.b64encode(pickle.dumps(obj)).decode()
+    got = wire.Encrypt(fast_min_chars=0).decode(text)
+    params = got["params"]
+    ent = wire._live_entry(params)
+    if ent is None:
+        pytest.skip("decode did not register a pinned row here (no pinned memory)")
+    layout = ent[1]
+    assert wire.wire_row(params, layout) is not None
+    keep = params["a"]  # keeps the row alive after the dict is gone
+    key = id(params)
+    del got, params, ent
+    gc.collect()
+    # force id reuse: allocate dicts until one lands at the freed address (CPython reuses it)
+    fresh = None
+    pool = []
+    for _ in range(20000):
+        d = {"a": np.zeros(700, np.float32), "b": np.zeros(300, np.float32)}
+        if id(d) == key:
+            fresh = d
+            break
+        pool.append(d)
+    if fresh is None:
+        # no reuse happened: inject one by hand through the same lookup the engine uses
+        fresh = {"a": np.zeros(700, np.float32)}
+        with wire._ROWS_LOCK:
+            wire._ROWS[id(fresh)] = wire._ROWS.pop(key)
+    assert wire.wire_row(fresh, layout) is None
+    assert wire._live_entry(fresh) is None and id(fresh) not in wire._ROWS
+    # an entry whose row dies is removed by the row's weakref callback
+    got2 = wire.Encrypt(fast_min_chars=0).decode(text)
+    k2 = id(got2["params"])
+    if wire._live_entry(got2["params"]) is not None:
+        del got2
+        gc.collect()
+        assert k2 not in wire._ROWS
+    del keep, pool
 
 
 def test_in_place_str_fill_is_probed(monkeypatch):

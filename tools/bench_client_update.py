@@ -48,8 +48,18 @@ def main():
                     help="DeviceUpdater copy-engine vs zero-copy chunked, alternating, outputs compared")
     ap.add_argument("--zero-copy", type=int, default=None, help="DeviceUpdater.zero_copy (default: the class default)")
     ap.add_argument("--chunk-mb", type=float, default=None, help="DeviceUpdater.chunk_bytes in MiB")
+    ap.add_argument("--first-mb", type=float, default=None, help="DeviceUpdater.first_chunk_bytes in MiB")
+    ap.add_argument("--last-mb", type=float, default=None, help="DeviceUpdater.last_chunk_bytes in MiB")
+    ap.add_argument("--phases", action="store_true", help="record the zero-copy pipeline's per-chunk times")
     a = ap.parse_args()
     from flearn_amd.strategy._update import DeviceUpdater
+
+    if a.first_mb is not None:
+        DeviceUpdater.first_chunk_bytes = int(a.first_mb * (1 << 20))
+    if a.last_mb is not None:
+        DeviceUpdater.last_chunk_bytes = int(a.last_mb * (1 << 20))
+    if a.phases:
+        DeviceUpdater.trace = []
 
     if a.zero_copy is not None:
         DeviceUpdater.zero_copy = bool(a.zero_copy)
@@ -81,6 +91,13 @@ def main():
             ref(wl, globs[r])
             rs.append(time.perf_counter() - t0)
         med = float(np.median(ts[1:]))
+        if a.phases and DeviceUpdater.trace:
+            last = DeviceUpdater.trace[-1]
+            res[f"{method}_phases"] = {
+                "launched_ms": round(last["launched_s"] * 1e3, 3), "done_ms": round(last["done_s"] * 1e3, 3),
+                "chunks": [[n, round(t0 * 1e3, 3), round(t1 * 1e3, 3)] for n, t0, t1 in last["chunks"]],
+                "note": "per chunk: [elements, pack start ms, launch queued ms]"}
+            DeviceUpdater.trace.clear()
         res[method] = {"flearn_amd_s": round(med, 4), "first_call_s": round(ts[0], 4),
                        "reference_s": round(float(np.median(rs[1:] if len(rs) > 1 else rs)), 4),
                        "speedup": round(float(np.median(rs[1:] if len(rs) > 1 else rs)) / med, 1)}
@@ -88,6 +105,8 @@ def main():
 
     res["zero_copy"] = DeviceUpdater.zero_copy
     res["chunk_bytes"] = DeviceUpdater.chunk_bytes
+    res["first_chunk_bytes"] = DeviceUpdater.first_chunk_bytes
+    res["last_chunk_bytes"] = DeviceUpdater.last_chunk_bytes
     res["note"] = "host arrays in and out (PCIe-inclusive); reference = its numpy ops on 1 core; median after round 0"
     print(json.dumps(res))
 
