@@ -228,6 +228,17 @@ def apply_dyn(glob, h, theta, n_clients: int, alpha: float = 0.01, *, out32=None
     na.check(rc, "fa_opt_apply")
 
 
+def set_reduce_grid(grid: int) -> int:
+    """Blocks of the fp32 stack reduce, process-wide (fa_set_reduce_grid): 0 = the library's
+    choice; fewer leave CUs to kernels running beside the reduce (RCCL's gather in the multi-GPU
+    pipeline).  Returns the previous setting.  Results never depend on it."""
+    L = na.load()
+    rc = L.fa_set_reduce_grid(int(grid))
+    if rc < 0:
+        na.check(rc, "fa_set_reduce_grid")
+    return rc
+
+
 def fill_uniform(dst: torch.Tensor, seed: int, row_begin: int = 0, col_begin: int = 0,
                  n_cols: int | None = None) -> None:
     """Synthetic client data on device: dst[r, c] = U(-1,1) hash of (seed, row_begin+r,

@@ -14,6 +14,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <atomic>
 #include <string>
 #include <vector>
 
@@ -161,17 +162,44 @@ bool rowmajor_geometry(int64_t chunks, int cus, int64_t target, int64_t* grid, i
   return false;
 }
 
+// fa_set_reduce_grid: 0 = the geometry below chooses the grid
+std::atomic<int> g_reduce_grid{0};
+
+// KG for a forced grid: the group size in {4, 3, 2} that wastes the fewest group slots
+int kg_for(int64_t k) {
+  int best = 4;
+  int64_t waste = (k + 3) / 4 * 4 - k;
+  for (int c : {3, 2}) {
+    const int64_t wc = (k + c - 1) / c * c - k;
+    if (wc < waste) {
+      waste = wc;
+      best = c;
+    }
+  }
+  return best;
+}
+
 template <class P, typename T, int OP>
 int launch_reduce(const typename P::x_t* stack, int64_t stride, int n, const void* w, int64_t col0,
                   int64_t ncols, const Epi<T>& e, hipStream_t s) {
   const typename P::w_t* wt = static_cast<const typename P::w_t*>(w);
   const int cus = device_cus();
   const int64_t chunks = ((ncols + 3) / 4 + 63) / 64;  // 1-KiB row pieces
+  const int forced = g_reduce_grid.load(std::memory_order_relaxed);
   if constexpr (sizeof(typename P::x_t) == 4) {
     if constexpr (sizeof(typename P::acc_t) == 4) {  // fp32 sums (every flearn weight type but f64)
       int64_t g = 0;
       int kg = 0;
-      if (chunks > (int64_t)cus * kPieceChunks &&
+      if (forced > 0 && chunks > (int64_t)forced * kPieceChunks) {
+        g = forced;
+        kg = kg_for((chunks + g * kPieceChunks - 1) / (g * kPieceChunks));
+        switch (kg) {
+          case 2: return launch_rowmajor<P, T, OP, 2>(stack, stride, n, wt, col0, ncols, e, g, s);
+          case 3: return launch_rowmajor<P, T, OP, 3>(stack, stride, n, wt, col0, ncols, e, g, s);
+          default: return launch_rowmajor<P, T, OP, 4>(stack, stride, n, wt, col0, ncols, e, g, s);
+        }
+      }
+      if (forced <= 0 && chunks > (int64_t)cus * kPieceChunks &&
           rowmajor_geometry(chunks, cus, (int64_t)(cus * kRowsBlocksPerCU + 0.5), &g, &kg)) {
         switch (kg) {
           case 2: return launch_rowmajor<P, T, OP, 2>(stack, stride, n, wt, col0, ncols, e, g, s);
@@ -180,10 +208,10 @@ int launch_reduce(const typename P::x_t* stack, int64_t stride, int n, const voi
         }
       }
     }
-    int64_t grid = (int64_t)(cus * kRowsBlocksPerCU + 0.5);
+    int64_t grid = forced > 0 ? forced : (int64_t)(cus * kRowsBlocksPerCU + 0.5);
     // a window just wider than one round of full pieces: a few more blocks (up to one per CU)
     // instead of a second, nearly empty round
-    if (chunks > grid * kPieceChunks && chunks <= (int64_t)cus * kPieceChunks)
+    if (forced <= 0 && chunks > grid * kPieceChunks && chunks <= (int64_t)cus * kPieceChunks)
       grid = (chunks + kPieceChunks - 1) / kPieceChunks;
     if (grid < 1) grid = 1;
     if (grid > chunks) grid = chunks;
@@ -684,6 +712,11 @@ int fa_gather_rows_f64(double* stack, int64_t row_stride, int32_t n_clients, con
     if (int rc = launch_check()) return rc;
   }
   return FA_OK;
+}
+
+int fa_set_reduce_grid(int32_t grid) {
+  if (grid < 0) return fail(FA_ERR_ARG, "grid must be >= 0");
+  return g_reduce_grid.exchange(grid);
 }
 
 int fa_fill_uniform_f32(float* dst, int64_t row_stride, int32_t n_rows, int64_t n_cols,

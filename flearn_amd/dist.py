@@ -65,12 +65,18 @@ def all_gather_into(dst: torch.Tensor, src: torch.Tensor, group=None, async_op: 
 class StripeModel:
     """Per-stripe cost model of one rank (seconds; widths in columns per rank).
     reduce(S) = a_r + b_r*S on the compute stream; gather(S) = a_g + b_g*S on the collective's
-    stream (a stripe of S columns per rank is an all-gather of world*S columns)."""
+    stream (a stripe of S columns per rank is an all-gather of world*S columns).
+    Contention: a reduce that runs beside a gather streams (1 + c_r) times slower, a gather that
+    runs beside a reduce (1 + c_g) times slower — they share the CUs and the HBM.  Measured on one
+    MI355X with a copy kernel standing in for the gather (tools/overlap_probe.py, DESIGN.md §6);
+    0 = the optimistic model (perfect overlap)."""
 
     a_r: float
     b_r: float
     a_g: float
     b_g: float
+    c_r: float = 0.0
+    c_g: float = 0.0
 
     @staticmethod
     def assumed(n_clients: int, world: int, hbm_bytes_s: float = 7.0e12, link_bytes_s: float = 50e9,
@@ -84,25 +90,35 @@ class StripeModel:
                            max(world - 1, 0) * 4.0 / ingress)
 
     @staticmethod
-    def fit(w_big: int, w_small: int, r_big: float, r_small: float, g_big: float, g_small: float) -> "StripeModel":
-        """Coefficients from two widths' measured reduce and gather times (non-negative)."""
+    def fit(w_big: int, w_small: int, r_big: float, r_small: float, g_big: float, g_small: float,
+            c_r: float = 0.0, c_g: float = 0.0) -> "StripeModel":
+        """Coefficients from two widths' measured reduce and gather times (non-negative), plus
+        the contention terms (measured separately)."""
         def line(tb, ts):
             b = max((tb - ts) / max(w_big - w_small, 1), 0.0)
             return max(ts - b * w_small, 0.0), b
 
         a_r, b_r = line(r_big, r_small)
         a_g, b_g = line(g_big, g_small)
-        return StripeModel(a_r, b_r, a_g, b_g)
+        return StripeModel(a_r, b_r, a_g, b_g, max(c_r, 0.0), max(c_g, 0.0))
+
+    def with_contention(self, c_r: float, c_g: float) -> "StripeModel":
+        return StripeModel(self.a_r, self.b_r, self.a_g, self.b_g, max(c_r, 0.0), max(c_g, 0.0))
 
     def makespan(self, widths, rep: int = 0) -> tuple:
         """(step time, reduce-stream busy time, exposed gather time) of a stripe plan; `rep`
-        replicated columns are reduced after the stripes, with no gather."""
+        replicated columns are reduced after the stripes, with no gather.  Every stripe's reduce
+        but the first runs beside the previous stripe's gather, and every gather but one that
+        finds the reduce stream idle runs beside a reduce: those streaming terms carry the
+        contention factors (1 + c_r) and (1 + c_g)."""
         t_red = t_gat = 0.0
-        for w in widths:
-            t_red += self.a_r + self.b_r * w
-            t_gat = max(t_red, t_gat) + self.a_g + self.b_g * w
+        last = len(widths) - 1
+        for c, w in enumerate(widths):
+            t_red += self.a_r + self.b_r * w * (1.0 + (self.c_r if c > 0 else 0.0))
+            busy_after = c < last or rep > 0  # a reduce (next stripe or the tail) runs beside it
+            t_gat = max(t_red, t_gat) + self.a_g + self.b_g * w * (1.0 + (self.c_g if busy_after else 0.0))
         if rep:
-            t_red += self.a_r + self.b_r * rep
+            t_red += self.a_r + self.b_r * rep * (1.0 + (self.c_r if widths else 0.0))
         step = max(t_gat, t_red)
         return step, t_red, step - t_red
 

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define FA_ABI_VERSION 6
+#define FA_ABI_VERSION 7
 
 /* return codes */
 #define FA_OK 0
@@ -207,6 +207,16 @@ int fa_gather_rows_f64(double* stack, int64_t row_stride, int32_t n_clients, con
  * regenerates any element.  Not a reference interface.                                        */
 int fa_fill_uniform_f32(float* dst, int64_t row_stride, int32_t n_rows, int64_t n_cols,
                         uint64_t seed, int64_t row_begin, int64_t col_global_begin, void* stream);
+
+/* Process-wide grid of the fp32 stack reduce (fa_reduce_f32 / _splitn's fallback): the number
+ * of blocks the row-pipelined kernels are launched with.  0 (the default) = the library's own
+ * choice (~0.75 blocks per CU, one block per CU at most: DESIGN.md section 4).  A smaller grid
+ * leaves CUs free for kernels that run beside the reduce — RCCL's all-gather of the previous
+ * stripe in the multi-GPU pipeline (flearn_amd.dist; DESIGN.md section 6 measures the
+ * contention).  Results do not depend on the grid (every column is still summed in client
+ * order).  Returns the previous value; grid < 0 -> FA_ERR_ARG.  No reference counterpart: a
+ * scheduling knob of this engine (the reference has one CPU thread).                         */
+int fa_set_reduce_grid(int32_t grid);
 
 /* ---- wire codec (HOST functions: every pointer below is host memory) -------------------------
  * flearn's HTTP mode ships uploads and global models as base64(pickle.dumps(obj))

@@ -232,3 +232,12 @@ def test_rows_entry_points_validate(L):
     assert L.fa_gather_rows_f64(FAKE, -1, 2, FAKE, FAKE, 1, None) == err
     assert L.fa_gather_rows_f64(None, 64, 2, FAKE, FAKE, 1, None) == err
     assert L.fa_gather_rows_f64(FAKE, 64, 2, FAKE, FAKE, 0, None) == 0
+
+
+def test_reduce_grid_knob(L):
+    """fa_set_reduce_grid: process-wide, returns the previous value, refuses negatives."""
+    assert L.fa_set_reduce_grid(0) == 0
+    assert L.fa_set_reduce_grid(160) == 0
+    assert L.fa_set_reduce_grid(224) == 160
+    assert L.fa_set_reduce_grid(-1) == header_define("FA_ERR_ARG")
+    assert L.fa_set_reduce_grid(0) == 224

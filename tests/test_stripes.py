@@ -121,3 +121,25 @@ def test_shard_candidates_for_the_measured_trial(world):
         plan = ShardPlan.from_widths(p, world, 0, w, rep=rep)
         assert plan.full_cols >= p
     assert shard_candidates(p, 1, m) == [plan_shards(p, 1, m)]
+
+
+def test_makespan_contention_terms():
+    """c_r / c_g: reduces that run beside a gather (every stripe after the first, and the tail)
+    and gathers that run beside a reduce (all but a last gather with nothing after it) stream
+    slower; zero contention is the old model exactly."""
+    base = StripeModel(a_r=0.0, b_r=1.0, a_g=0.0, b_g=0.25)
+    assert base.with_contention(0.0, 0.0).makespan((192, 64)) == base.makespan((192, 64))
+    m = base.with_contention(0.5, 1.0)
+    # reduce 0: 192; reduce 1 (beside gather 0): 64*1.5 = 96 -> 288
+    # gather 0 (beside reduce 1): 48*2 = 96, 192..288; gather 1 (nothing after it): 16, 288..304
+    assert m.makespan((192, 64)) == (304.0, 288.0, 16.0)
+    # a replicated tail runs beside the last gather: both carry the terms
+    t, red, exp = m.makespan((64,), rep=64)
+    assert red == 64 + 64 * 1.5 and t == max(64 + 16 * 2.0, red)
+    # one stripe, no tail: nothing overlaps
+    assert m.makespan((256,)) == base.makespan((256,))
+    # contention never makes a plan faster, and a fitted model carries it
+    for w in ((64,), (128, 64), (64, 64, 64)):
+        assert m.makespan(w)[0] >= base.makespan(w)[0]
+    f = StripeModel.fit(8000, 1000, 10 + 8000 * 2, 10 + 1000 * 2, 30 + 8000 * 5, 30 + 1000 * 5, c_r=0.1, c_g=-1)
+    assert (f.c_r, f.c_g) == (0.1, 0.0)

@@ -138,7 +138,13 @@ def ab(a):
         same = all(np.array_equal(np.asarray(x[k]), np.asarray(y[k])) and np.asarray(x[k]).dtype == np.asarray(y[k]).dtype
                    for x, y in zip(outs[False], outs[True]) for k in x)
         res[method] = {"copy_engine_s": round(float(np.median(times[False])), 4),
-                       "zero_copy_s": round(float(np.median(times[True])), 4), "bit_equal": same}
+                       "zero_copy_s": round(float(np.median(times[True])), 4), "bit_equal": same,
+                       "zero_copy_all_s": [round(t, 4) for t in times[True]],
+                       "copy_engine_all_s": [round(t, 4) for t in times[False]]}
+        if DeviceUpdater.trace:
+            res[method]["zero_copy_launched_done_ms"] = [
+                [round(t["launched_s"] * 1e3, 2), round(t["done_s"] * 1e3, 2)] for t in DeviceUpdater.trace]
+            DeviceUpdater.trace.clear()
     DeviceUpdater.zero_copy = True
     print(json.dumps(res))
 

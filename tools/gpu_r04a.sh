@@ -9,4 +9,5 @@ timeout -k 10 180 python3 -c "import sys; sys.path.insert(0, '$R'); import __gra
 timeout -k 10 300 python3 $R/bench.py > $O/bench.json 2> $O/bench.err
 timeout -k 10 300 python3 $R/tools/bench_client_update.py --phases --rounds 6 > $O/client_update.json 2> $O/client_update.err
 timeout -k 10 300 python3 $R/tools/bench_client_update.py --ab --rounds 4 > $O/client_update_ab.json 2> $O/client_update_ab.err
+timeout -k 10 300 python3 $R/tools/overlap_probe.py > $O/overlap.json 2> $O/overlap.err
 echo done

@@ -1,0 +1,50 @@
+// probe_copy.hip — stand-in for RCCL's all-gather traffic on ONE GPU (tools/overlap_probe.py):
+// a grid-stride 16-B copy on a chosen number of blocks, launched on its own stream beside the
+// aggregation reduce, so the reduce's slowdown from sharing CUs and HBM with a concurrent
+// collective can be measured without a second GPU.  Not product code.
+//   hipcc --offload-arch=gfx950 -O3 -fPIC -shared tools/probe_copy.hip -o tools/libprobe_copy.so
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+__global__ __launch_bounds__(256) void probe_copy16(uint4* __restrict__ dst, const uint4* __restrict__ src,
+                                                    int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) dst[i] = src[i];
+}
+
+extern "C" int probe_copy(void* dst, const void* src, int64_t n16, int32_t blocks, void* stream) {
+  if (!dst || !src || n16 <= 0 || blocks <= 0) return -1;
+  hipLaunchKernelGGL(probe_copy16, dim3((unsigned)blocks), dim3(256), 0, static_cast<hipStream_t>(stream),
+                     static_cast<uint4*>(dst), static_cast<const uint4*>(src), n16);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+// the same copy over one small buffer `reps` times (L2-resident: CU and cache traffic, no HBM)
+__global__ __launch_bounds__(256) void probe_copy16_rep(uint4* __restrict__ dst, const uint4* __restrict__ src,
+                                                        int64_t n, int reps) {
+  for (int r = 0; r < reps; ++r)
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+      uint4 v = src[i];
+      v.x += (unsigned)r;
+      dst[i] = v;
+    }
+}
+
+// ALU only: a dependent FMA chain per lane, one store per lane at the end (no memory traffic)
+__global__ __launch_bounds__(256) void probe_spin_k(float* __restrict__ out, int iters) {
+  float a = (float)threadIdx.x * 1e-3f, b = 1.0000001f, c = 1e-7f;
+  for (int i = 0; i < iters; ++i) a = __builtin_fmaf(a, b, c);
+  out[(int64_t)blockIdx.x * 256 + threadIdx.x] = a;
+}
+
+extern "C" int probe_copy_rep(void* dst, const void* src, int64_t n16, int32_t blocks, int32_t reps, void* stream) {
+  if (!dst || !src || n16 <= 0 || blocks <= 0 || reps <= 0) return -1;
+  hipLaunchKernelGGL(probe_copy16_rep, dim3((unsigned)blocks), dim3(256), 0, static_cast<hipStream_t>(stream),
+                     static_cast<uint4*>(dst), static_cast<const uint4*>(src), n16, reps);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+extern "C" int probe_spin(float* out, int32_t blocks, int32_t iters, void* stream) {
+  if (!out || blocks <= 0 || iters <= 0) return -1;
+  hipLaunchKernelGGL(probe_spin_k, dim3((unsigned)blocks), dim3(256), 0, static_cast<hipStream_t>(stream), out, iters);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}

@@ -34,7 +34,27 @@ def one_gpu_step(cfg: str) -> float:
     return d["ms_per_step"] / 1e3
 
 
-def project(cfg: str, g: int, link_bs: float, launch_s=10e-6, collective_s=30e-6, tail=True):
+OVERLAP = REPO / "profiles" / "r04" / "overlap" / "overlap.json"
+
+
+def contention(ingress_bs: float, path=OVERLAP):
+    """(c_r, c_g, the stand-in used) for a gather bringing `ingress_bs` into each GPU: from the
+    one-GPU overlap probe (tools/overlap_probe.py) at the library's default reduce grid, the
+    smallest copy stand-in whose local HBM traffic (2 x its copy rate: read + write) is at least
+    the gather's (2 x ingress: the received bytes written, the rank's own slice read once per
+    peer) — the next measured point above, or the largest."""
+    d = json.loads(Path(path).read_text())
+    row = next(r for r in d["rows"] if r["grid"] == "default")
+    pts = sorted(((v["copy_alone_gbs"] * 1e9, v["reduce_slowdown"] - 1.0, v["copy_slowdown"] - 1.0, k)
+                  for k, v in row["with"].items() if k != "dma"))
+    for rate, c_r, c_g, k in pts:
+        if rate >= ingress_bs:
+            return c_r, c_g, f"copy on {k} blocks ({rate / 1e9:.0f} GB/s)"
+    rate, c_r, c_g, k = pts[-1]
+    return c_r, c_g, f"copy on {k} blocks ({rate / 1e9:.0f} GB/s)"
+
+
+def project(cfg: str, g: int, link_bs: float, launch_s=10e-6, collective_s=30e-6, tail=True, contended=False):
     n, p = CONFIGS[cfg]
     t1 = one_gpu_step(cfg)
     local = -(-p // g)
@@ -42,6 +62,10 @@ def project(cfg: str, g: int, link_bs: float, launch_s=10e-6, collective_s=30e-6
     b_r = t1 / p  # the 1-GPU per-column cost (fused state traffic included)
     b_g = (g - 1) * 4.0 / ((g - 1) * link_bs) if g > 1 else 0.0
     m = StripeModel(launch_s, b_r, collective_s if g > 1 else 0.0, b_g)
+    stand_in = None
+    if contended and g > 1:
+        c_r, c_g, stand_in = contention((g - 1) * link_bs)
+        m = m.with_contention(c_r, c_g)
     if g == 1:
         widths, rep = (local,), 0
     elif tail:
@@ -52,7 +76,7 @@ def project(cfg: str, g: int, link_bs: float, launch_s=10e-6, collective_s=30e-6
     return {"config": cfg, "gpus": g, "link_GBs": link_bs / 1e9, "ingress_GBs": (g - 1) * link_bs / 1e9,
             "stripes": len(widths), "replicated_frac": round(rep / p, 3), "step_ms": round(step * 1e3, 3),
             "reduce_ms": round(red * 1e3, 3), "exposed_gather_ms": round(exposed * 1e3, 3),
-            "speedup": round(t1 / step, 2)}
+            "speedup": round(t1 / step, 2), "c_r": round(m.c_r, 3), "c_g": round(m.c_g, 3), "stand_in": stand_in}
 
 
 def main():
@@ -60,8 +84,10 @@ def main():
     ap.add_argument("--link-gbs", default="50,64")
     ap.add_argument("--json", action="store_true")
     ap.add_argument("--no-tail", action="store_true", help="stripes only (no replicated tail)")
+    ap.add_argument("--contended", action="store_true",
+                    help="reduce / gather slowed by the measured one-GPU contention (profiles/r04/overlap)")
     a = ap.parse_args()
-    rows = [project(c, g, float(l) * 1e9, tail=not a.no_tail)
+    rows = [project(c, g, float(l) * 1e9, tail=not a.no_tail, contended=a.contended)
             for l in a.link_gbs.split(",") for c in CONFIGS for g in (2, 4, 8)]
     if a.json:
         print(json.dumps(rows, indent=1))
@@ -69,7 +95,7 @@ def main():
     for r in rows:
         print(f"{r['link_GBs']:>5.0f} GB/s/link  {r['config']:>3}  G={r['gpus']}  ingress {r['ingress_GBs']:>4.0f} GB/s  "
               f"{r['stripes']} stripes  tail {r['replicated_frac']:.3f}  step {r['step_ms']:.3f} ms  (reduce {r['reduce_ms']:.3f}, exposed gather "
-              f"{r['exposed_gather_ms']:.3f})  {r['speedup']:.2f}x")
+              f"{r['exposed_gather_ms']:.3f})  {r['speedup']:.2f}x  c_r {r['c_r']} c_g {r['c_g']}")
 
 
 if __name__ == "__main__":
