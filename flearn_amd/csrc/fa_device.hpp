@@ -341,8 +341,13 @@ __device__ __forceinline__ void buf_store_tquad(__amdgpu_buffer_rsrc_t r, int q,
   } else if constexpr (XL || FA_EPI_STORE64_LDS != 0) {
     typedef double d2 __attribute__((ext_vector_type(2)));
     __shared__ d2 xch[8][128];  // 2 KiB per wave, up to 8 waves per block
-    const int lane = (int)threadIdx.x & 63;
-    d2* s = xch[(int)threadIdx.x >> 6];
+    // the thread index made opaque HERE: otherwise the lane-dependent LDS and store addresses
+    // are hoisted out of the group sweep and held in VGPRs through it (KG = 4: the sweep is at
+    // 256 + 256 registers already, and those few more spilled it to scratch)
+    int tid = (int)threadIdx.x;
+    asm volatile("" : "+v"(tid));
+    const int lane = tid & 63;
+    d2* s = xch[tid >> 6];
     s[2 * lane] = d2{v[0], v[1]};
     s[2 * lane + 1] = d2{v[2], v[3]};
     // lane l reads what lanes l/2 and 32 + l/2 wrote: a cross-lane dependency the compiler does
@@ -945,8 +950,14 @@ __global__ __launch_bounds__(64 * W) void reduce_kernel_splitn(const float* __re
 // TR (tools/tune_rows.hip): wave 0 of every block stamps the 100-MHz wall clock at each claim it
 // starts (e.trace[block * 32 + 1 + c], c < 30) and at its exit (slot 0), claim count in slot 31.
 // DS: steps in flight (1, or any divisor of KG: step s = (i, j) lives in slot j % DS).
+// PFA > 0 (tuning, tools/tune_rows.hip): translation prefetch — after each refill every wave also
+// loads ONE dword (all lanes the same address) of the step PFA steps past the next one, so the
+// page translation of that upload row is resolved before its 64-KiB step is issued (the
+// row-pointer kernel takes 2.4x the UTCL1 translation misses of the stack kernel on per-tensor
+// allocations: profiles/r04/rows_pmc/).  The dword is consumed one row later (xor into a sink
+// kept alive by an empty asm), when it has long arrived.
 template <class P, typename T, int OP, int V, int W, int KG, int DN, bool NT, bool TR = false, int DS = 1,
-          bool SG = false>
+          bool SG = false, int PFA = 0>
 __global__ __launch_bounds__(64 * W) void reduce_kernel_segrows_rm(const float* const* __restrict__ rows, int n,
                                                                    const typename P::w_t* __restrict__ w,
                                                                    const fa_piece* __restrict__ pieces,
@@ -1002,17 +1013,26 @@ __global__ __launch_bounds__(64 * W) void reduce_kernel_segrows_rm(const float* 
       static_assert(KG % DS == 0, "steps in flight must divide the group");
       AV acc[KG][V];
       XV x[DS][V];
+      uint32_t pf[KG > 0 ? KG : 1];
+      uint32_t sink = 0;
+#pragma unroll
+      for (int j = 0; j < KG; ++j) pf[j] = 0;
 #pragma unroll
       for (int d = 0; d < DS; ++d) FA_SRM_LOAD(FA_SRM_PTR(d / KG, d % KG), d % KG, d);
       const char* pn = FA_SRM_PTR(DS / KG, DS % KG);  // the pointer of the next step to load
       // after consuming step (i, j): refill its slot with step (i, j) + DS, then fetch the pointer
       // of the step after that one
-#define FA_SRM_REFILL(i, j)                                           \
-  __builtin_amdgcn_sched_barrier(0);                                  \
-  if ((i) + ((j) + DS) / KG < n) {                                    \
-    FA_SRM_LOAD(pn, ((j) + DS) % KG, (j) % DS);                       \
-    pn = FA_SRM_PTR((i) + ((j) + DS + 1) / KG, ((j) + DS + 1) % KG); \
-  }                                                                   \
+#define FA_SRM_REFILL(i, j)                                                                          \
+  __builtin_amdgcn_sched_barrier(0);                                                                 \
+  if ((i) + ((j) + DS) / KG < n) {                                                                   \
+    FA_SRM_LOAD(pn, ((j) + DS) % KG, (j) % DS);                                                      \
+    pn = FA_SRM_PTR((i) + ((j) + DS + 1) / KG, ((j) + DS + 1) % KG);                                \
+    if constexpr (PFA > 0) {                                                                         \
+      sink ^= pf[j];                                                                                 \
+      pf[j] = __builtin_amdgcn_raw_buffer_load_b32(                                                  \
+          row_rsrc(FA_SRM_PTR((i) + ((j) + DS + 1 + PFA) / KG, ((j) + DS + 1 + PFA) % KG), 4u), 0, 0, 0); \
+    }                                                                                                \
+  }                                                                                                  \
   __builtin_amdgcn_sched_barrier(0);
       {  // row 0: the products initialise the sums (peeled: a select between the first product
          // and the running sum kept both alive for every slot and spilled KG >= 3)
@@ -1038,6 +1058,11 @@ __global__ __launch_bounds__(64 * W) void reduce_kernel_segrows_rm(const float* 
 #undef FA_SRM_REFILL
 #undef FA_SRM_LOAD
 #undef FA_SRM_PTR
+      if constexpr (PFA > 0) {
+#pragma unroll
+        for (int j = 0; j < KG; ++j) sink ^= pf[j];
+        asm volatile("" ::"v"(sink));
+      }
 #pragma unroll
       for (int j = 0; j < KG; ++j) finish_piece<T, OP, A, V, 64 * W, (V >= 2 ? 2 : V)>(e, col[j] / 4, cols[j], acc[j]);
     } else {
@@ -1321,10 +1346,35 @@ __device__ __forceinline__ void rowmajor_group(const char* __restrict__ base, in
   } else {
     // whole-line f64 state / result stores where they cost no spills: the fused ops at KG <= 3
     // (at KG = 4 the LDS regrouping pushes the kernel past 256 + 256 registers; finding 22)
-    // (XLM: -1 this rule, 0 / 1 forced off / on by the tuner)
-    constexpr bool XL = XLM >= 0 ? XLM == 1 : (sizeof(T) == 8 && OP != FA_OP_MEAN && KG <= 3);
+    // (XLM: -1 this rule, 0 / 1 forced off / on by the tuner; 2: on, with the last KG/2 pieces'
+    // sums parked in LDS while the first ones finish, so the regrouping has registers to use)
+    constexpr bool XL = XLM >= 0 ? XLM >= 1 : (sizeof(T) == 8 && OP != FA_OP_MEAN && KG <= 3);
+    if constexpr (XLM == 2 && KG >= 2) {
+      constexpr int KP = KG / 2;  // pieces parked
+      // lane-private slots, [piece][slot][thread]: consecutive lanes, consecutive 16 B (no bank
+      // conflicts); a wave reads only what its own lanes wrote, in program order (no barrier)
+      __shared__ AV park[KP][V][64 * W];
 #pragma unroll
-    for (int j = 0; j < KG; ++j) finish_piece<T, OP, A, V, 64 * W, EPIB, XL>(e, qb[j], (int)(bytes[j] / 4), acc[j]);
+      for (int j = 0; j < KP; ++j)
+#pragma unroll
+        for (int v = 0; v < V; ++v) park[j][v][threadIdx.x] = acc[KG - KP + j][v];
+      // the compiler must not forward the stored values (that would keep them in registers)
+      __atomic_signal_fence(__ATOMIC_SEQ_CST);
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int j = 0; j < KG - KP; ++j) finish_piece<T, OP, A, V, 64 * W, EPIB, XL>(e, qb[j], (int)(bytes[j] / 4), acc[j]);
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int j = 0; j < KP; ++j) {
+        AV a2[V];
+#pragma unroll
+        for (int v = 0; v < V; ++v) a2[v] = park[j][v][threadIdx.x];
+        finish_piece<T, OP, A, V, 64 * W, EPIB, XL>(e, qb[KG - KP + j], (int)(bytes[KG - KP + j] / 4), a2);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < KG; ++j) finish_piece<T, OP, A, V, 64 * W, EPIB, XL>(e, qb[j], (int)(bytes[j] / 4), acc[j]);
+    }
   }
   if constexpr (TR) {
     if (threadIdx.x == 0 && gi < 7) e.trace[blockIdx.x * 16 + 2 + 2 * gi] = wall_clock64();

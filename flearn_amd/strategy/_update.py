@@ -9,6 +9,7 @@ from __future__ import annotations
 
 import concurrent.futures
 import ctypes
+import math
 import os
 import time
 
@@ -91,7 +92,13 @@ class DeviceUpdater:
     #: (no copy-out).  False: pack everything, two H2D copies, one launch, one D2H, a host copy
     #: out; tools/bench_client_update.py --ab times both
     zero_copy = True
-    chunk_bytes = 32 << 20  # w_glob bytes per zero-copy chunk (the middle ones)
+    #: with zero_copy: how the chunks cross PCIe.  "dma": each packed chunk is copied to the GPU
+    #: by a copy engine on its own stream, updated there, and its result copied back into the
+    #: pinned result by another copy engine — H2D and D2H run concurrently at DMA rate;
+    #: "kernel": the update kernel itself reads the pinned staging and writes the pinned result
+    #: over PCIe (zero-copy loads run below the DMA rate: 38 vs ~55 GB/s, round 4)
+    transfer = "kernel"
+    chunk_bytes = 64 << 20  # w_glob bytes per zero-copy chunk (the middle ones; 32 MiB: +0.3-0.8 ms, round 4)
     first_chunk_bytes = 4 << 20  # the first chunks grow from this (x2 each) so the GPU starts early
     last_chunk_bytes = 8 << 20  # ... and the last ones shrink towards this: a short exposed tail
     #: a list to receive per-call phase times (tools/bench_client_update.py --phases), or None
@@ -108,12 +115,18 @@ class DeviceUpdater:
         self._stage = None  # pinned staging of the current layout (local, global, result)
 
     def _layout(self, w_glob):
+        """[(key, shape, offset, numel)], total — cached on the (key, shape) signature: the same
+        model comes back every round."""
+        sig = tuple((k, g.shape) for k, g in w_glob.items())
+        hit = getattr(self, "_lay_cache", None)
+        if hit is not None and hit[0] == sig:
+            return hit[1], hit[2]
         lay, off = [], 0
-        for k, g in w_glob.items():
-            shape = tuple(np.shape(g))
-            n = int(np.prod(shape)) if shape else 1
+        for k, shape in sig:
+            n = math.prod(shape) if shape else 1
             lay.append((k, shape, off, n))
             off += -(-max(n, 1) // ALIGN) * ALIGN
+        self._lay_cache = (sig, lay, off)
         return lay, off
 
     def reset(self):
@@ -131,6 +144,14 @@ class DeviceUpdater:
         return out
 
     def __call__(self, w_local, w_glob, **override):
+        t_call = time.perf_counter()
+        n_trace = len(self.trace) if self.trace is not None else 0
+        self._call(w_local, w_glob, **override)
+        if self.trace is not None and len(self.trace) > n_trace:
+            self.trace[-1]["call_s"] = time.perf_counter() - t_call
+        return w_local
+
+    def _call(self, w_local, w_glob, **override):
         na.lib()
         glob, local, host_keys = {}, {}, []
         for k, g in w_glob.items():
@@ -159,9 +180,38 @@ class DeviceUpdater:
 
     def _host_step(self, w_local, w_glob, keys, **override):
         """The reference's per-key numpy arithmetic (avgm.py:19-36 / opt.py:23-65) for the keys the
-        device path does not take; their v_t lives on the host (np.zeros_like(delta) first)."""
+        device path does not take; their v_t lives on the host (np.zeros_like(delta) first).
+        The common case — BN num_batches_tracked: a 0-d int64 local value against a float64
+        scalar in w_glob — runs as ONE vectorised numpy evaluation of the same expressions over
+        all such keys (elementwise, so every value is what the per-key scalar ops give; results
+        are handed back as the np.float64 scalars numpy returns for 0-d operands)."""
         p = dict(self.params, **override)
         vh = self.v_host
+        batch = [k for k in keys if type(w_local[k]) is np.ndarray and w_local[k].ndim == 0
+                 and w_local[k].dtype == np.int64 and type(w_glob[k]) in (np.float64, float)
+                 and (k not in vh or type(vh[k]) is np.float64)]
+        if len(batch) > 1:
+            lv = np.array([w_local[k] for k in batch], dtype=np.int64)
+            g = np.array([w_glob[k] for k in batch], dtype=np.float64)
+            delta = g - lv
+            v = np.array([vh[k] if k in vh else 0.0 for k in batch], dtype=np.float64)
+            if self.op == na.OP_AVGM:
+                v = delta + p["beta"] * v
+                out = lv + v
+            else:
+                sq = np.multiply(delta, delta)
+                if self.op == na.OP_ADAGRAD:
+                    v = v + sq
+                elif self.op == na.OP_YOGI:
+                    v = v - (1 - p["beta2"]) * sq * np.sign(v - sq)
+                else:
+                    v = p["beta2"] * v + (1 - p["beta2"]) * sq
+                out = lv + p["eta"] * delta / (np.sqrt(v) + p["tau"])
+            for i, k in enumerate(batch):
+                w_local[k] = out[i]
+                vh[k] = v[i]
+            done = set(batch)
+            keys = [k for k in keys if k not in done]
         for k in keys:
             lv = w_local[k]
             if isinstance(lv, torch.Tensor):
@@ -288,40 +338,78 @@ class DeviceUpdater:
         v_in, v_out = self.v, self._v_next
         # the new w_local lives in a fresh pinned buffer the kernel writes over PCIe; the values
         # handed out are views of it (torch's host caching allocator recycles it once they die)
+        t_alloc = time.perf_counter()
         res = torch.empty(total, dtype=tdt, pin_memory=True)
+        dma = self.transfer in ("dma", "dma_in")
+        dma_out = self.transfer == "dma"
+        if dma:
+            dbuf = getattr(self, "_dbuf", None)
+            if dbuf is None or dbuf[0] is not self._stage:
+                # device copies of the staging and the result, and the copy-in / copy-out streams
+                dbuf = self._dbuf = (self._stage, torch.empty(total, dtype=torch.float32, device=dev),
+                                     torch.empty(total, dtype=tdt, device=dev), torch.empty(total, dtype=tdt, device=dev),
+                                     torch.cuda.Stream(dev), torch.cuda.Stream(dev))
+            _, dl, dg, dout, s_in, s_out = dbuf
         tr = [] if self.trace is not None else None
         t0 = time.perf_counter()
+        chunks = self._chunks(lay, total, tdt)
+        # every chunk's pack parts go to the pool at once, in chunk order (the pool runs them
+        # FIFO): the threads stay busy whatever the chunk sizes, and each chunk's kernel is
+        # launched as soon as its own parts are in
+        pool = _pool()
+        futs = [([pool.submit(t) for t in pack_l.tasks(local)], [pool.submit(t) for t in pack_g.tasks(glob)])
+                for _first, _end, pack_l, pack_g, _g in chunks]
         with torch.cuda.device(dev):
             stream = torch.cuda.current_stream(dev)
             sh = stream.cuda_stream
             try:
-                for first, end, pack_l, pack_g, g in self._chunks(lay, total, tdt):
+                for (first, end, pack_l, pack_g, g), (fl, fg) in zip(chunks, futs):
                     tp = time.perf_counter()
-                    tl, tg = pack_l.tasks(local), pack_g.tasks(glob)
-                    rc = _run(tl + tg)
-                    if any(rc[: len(tl)]):  # a value the native pack refuses: copy in Python
+                    if any(f.result() for f in fl):  # a value the native pack refuses: copy in Python
                         for k, s, o, n in g:
                             lh.numpy()[o : o + n] = local[k].reshape(-1)
-                    if any(rc[len(tl) :]):
+                    if any(f.result() for f in fg):
                         for k, s, o, n in g:
                             gh.numpy()[o : o + n] = glob[k].reshape(-1)
                     n = end - first
-                    epi = _epilogue(self.op, lh[first:end], v_in[first:end], p["beta"], p["eta"], p["tau"], p["beta2"],
+                    if dma:  # copy engine in (own stream), the update on the device, copy engine out
+                        with torch.cuda.stream(s_in):
+                            dl[first:end].copy_(lh[first:end], non_blocking=True)
+                            dg[first:end].copy_(gh[first:end], non_blocking=True)
+                        stream.wait_stream(s_in)
+                        src_l, src_g = dl[first:end], dg[first:end]
+                        out = (dout if dma_out else res)[first:end].data_ptr()
+                    else:  # the kernel reads the pinned staging and writes the pinned result over PCIe
+                        src_l, src_g, out = lh[first:end], gh[first:end], res[first:end].data_ptr()
+                    epi = _epilogue(self.op, src_l, v_in[first:end], p["beta"], p["eta"], p["tau"], p["beta2"],
                                     v_out=v_out[first:end])
-                    out = res[first:end].data_ptr()
-                    na.check(L.fa_opt_apply(prec, ctypes.byref(epi), lh[first:end].data_ptr(), gh[first:end].data_ptr(),
+                    na.check(L.fa_opt_apply(prec, ctypes.byref(epi), src_l.data_ptr(), src_g.data_ptr(),
                                             n, None if prec == na.PREC_F64 else out,
                                             out if prec == na.PREC_F64 else None, sh), "fa_opt_apply")
+                    if dma_out:
+                        s_out.wait_stream(stream)
+                        with torch.cuda.stream(s_out):
+                            res[first:end].copy_(dout[first:end], non_blocking=True)
                     if tr is not None:
                         tr.append((end - first, tp - t0, time.perf_counter() - t0))
             except BaseException:
-                stream.synchronize()  # no queued chunk may still read the staging or write `res`
+                for fl, fg in futs:  # no pack may still write the staging ...
+                    for f in fl + fg:
+                        f.cancel()
+                concurrent.futures.wait([f for fl, fg in futs for f in fl + fg])
+                stream.synchronize()  # ... nor a queued chunk read it or write `res`
+                if dma:
+                    s_in.synchronize()
+                    s_out.synchronize()
                 raise
             ts = time.perf_counter()
             stream.synchronize()
+            if dma:
+                s_out.synchronize()
         self.v, self._v_next = v_out, v_in
         if tr is not None:
-            self.trace.append({"chunks": tr, "launched_s": ts - t0, "done_s": time.perf_counter() - t0})
+            self.trace.append({"chunks": tr, "launched_s": ts - t0, "done_s": time.perf_counter() - t0,
+                               "alloc_s": t0 - t_alloc})
         fresh = res.numpy()
         for k, s, o, n in lay:  # replaced per key, like the reference (avgm.py:34-35, opt.py:62-63)
             w_local[k] = fresh[o : o + n].reshape(s)

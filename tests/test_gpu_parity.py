@@ -967,7 +967,7 @@ def test_host_pack_mixed_upload_kinds(shards, cuda):
         assert_dict_bitwise(got, want, f"mixed x{shards}")
 
 
-@pytest.mark.parametrize("mode", ["copy-engine", "zero-copy", "zero-copy-1MiB-chunks"])
+@pytest.mark.parametrize("mode", ["copy-engine", "zero-copy", "zero-copy-1MiB-chunks", "dma-chunks", "dma-1MiB-chunks"])
 @pytest.mark.parametrize("op", ["avgm", "adagrad", "yogi"])
 def test_client_side_update_large_and_fallback_values(op, mode, cuda, monkeypatch):
     """The client update on a model above the copy-part size (parallel native packs) and with
@@ -978,7 +978,8 @@ def test_client_side_update_large_and_fallback_values(op, mode, cuda, monkeypatc
     from flearn_amd.strategy._update import DeviceUpdater
 
     monkeypatch.setattr(DeviceUpdater, "zero_copy", mode != "copy-engine")
-    if mode == "zero-copy-1MiB-chunks":
+    monkeypatch.setattr(DeviceUpdater, "transfer", "dma" if mode.startswith("dma") else "kernel")
+    if mode.endswith("1MiB-chunks"):
         monkeypatch.setattr(DeviceUpdater, "chunk_bytes", 1 << 20)
     rng = np.random.default_rng(21)
     shapes = {"a": (1024, 3000), "b": (3000,), "c": (700, 900), "d": (), "e": (5, 7)}
@@ -1003,8 +1004,9 @@ def test_client_side_update_large_and_fallback_values(op, mode, cuda, monkeypatc
             prev["c"] = np.asfortranarray(prev["c"])
 
 
+@pytest.mark.parametrize("transfer", ["dma", "kernel"])
 @pytest.mark.parametrize("op", ["avgm", "adagrad"])
-def test_client_side_update_failure_mid_call_changes_nothing(op, cuda, monkeypatch):
+def test_client_side_update_failure_mid_call_changes_nothing(op, transfer, cuda, monkeypatch):
     """a zero-copy chunked update that fails on a later chunk (chunks before it already
     queued) must leave v_t and w_local as they were — v_t is double-buffered and swapped only
     after every chunk ran, and the queued chunks are waited for before the error propagates — so
@@ -1013,6 +1015,7 @@ def test_client_side_update_failure_mid_call_changes_nothing(op, cuda, monkeypat
     from flearn_amd.strategy._update import DeviceUpdater
 
     monkeypatch.setattr(DeviceUpdater, "zero_copy", True)
+    monkeypatch.setattr(DeviceUpdater, "transfer", transfer)
     monkeypatch.setattr(DeviceUpdater, "chunk_bytes", 1 << 20)
     rng = np.random.default_rng(5)
     shapes = {"a": (512, 1024), "b": (3000,), "c": (300, 700), "d": (4096,)}

@@ -51,6 +51,7 @@ def main():
     ap.add_argument("--first-mb", type=float, default=None, help="DeviceUpdater.first_chunk_bytes in MiB")
     ap.add_argument("--last-mb", type=float, default=None, help="DeviceUpdater.last_chunk_bytes in MiB")
     ap.add_argument("--phases", action="store_true", help="record the zero-copy pipeline's per-chunk times")
+    ap.add_argument("--transfer", default=None, choices=("dma", "dma_in", "kernel"), help="DeviceUpdater.transfer")
     a = ap.parse_args()
     from flearn_amd.strategy._update import DeviceUpdater
 
@@ -60,6 +61,8 @@ def main():
         DeviceUpdater.last_chunk_bytes = int(a.last_mb * (1 << 20))
     if a.phases:
         DeviceUpdater.trace = []
+    if a.transfer is not None:
+        DeviceUpdater.transfer = a.transfer
 
     if a.zero_copy is not None:
         DeviceUpdater.zero_copy = bool(a.zero_copy)
@@ -104,6 +107,7 @@ def main():
     from flearn_amd.strategy._update import DeviceUpdater
 
     res["zero_copy"] = DeviceUpdater.zero_copy
+    res["transfer"] = DeviceUpdater.transfer
     res["chunk_bytes"] = DeviceUpdater.chunk_bytes
     res["first_chunk_bytes"] = DeviceUpdater.first_chunk_bytes
     res["last_chunk_bytes"] = DeviceUpdater.last_chunk_bytes
@@ -128,6 +132,10 @@ def ab(a):
                     DeviceUpdater.zero_copy = zc
                     s = objs[zc]
                     wl = dict(w_local0)
+                    # drop the previous call's result before the clock starts: freeing the copy-engine
+                    # path's fresh 205-MB array (munmap) inside the next call's timing charged ~8 ms
+                    # to whichever mode ran next (round 4 traces)
+                    out = None
                     t0 = time.perf_counter()
                     out = s.mean_momentum(wl, globs[r], 0.9) if method == "avgm" else s.adaptive_opt(wl, globs[r], "adagrad")
                     dt = time.perf_counter() - t0
@@ -142,8 +150,9 @@ def ab(a):
                        "zero_copy_all_s": [round(t, 4) for t in times[True]],
                        "copy_engine_all_s": [round(t, 4) for t in times[False]]}
         if DeviceUpdater.trace:
-            res[method]["zero_copy_launched_done_ms"] = [
-                [round(t["launched_s"] * 1e3, 2), round(t["done_s"] * 1e3, 2)] for t in DeviceUpdater.trace]
+            res[method]["zero_copy_alloc_launched_done_call_ms"] = [
+                [round(t["alloc_s"] * 1e3, 2), round(t["launched_s"] * 1e3, 2), round(t["done_s"] * 1e3, 2),
+                 round(t.get("call_s", 0) * 1e3, 2)] for t in DeviceUpdater.trace]
             DeviceUpdater.trace.clear()
     DeviceUpdater.zero_copy = True
     print(json.dumps(res))

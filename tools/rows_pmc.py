@@ -3,7 +3,7 @@
 
 flearn's run2 simulator hands the server each client's CUDA state_dict (Communicator.py:287-292):
 every tensor its own allocation.  The product reads them in place through a per-(key, client)
-pointer table (fa_reduce_f32_rows, via AVG(output="device").server); the stack kernel
+pointer table (fa_reduce_f32_rows, the engine's Packer building the table); the stack kernel
 (fa_reduce_f32 over one [N, stride] array) reads the same values packed.  This launches both,
 alternating, --reps times each, and prints their HIP-event times; run it under
 `rocprofv3 --pmc ...` to get per-kernel counters.
@@ -27,10 +27,12 @@ import torch
 REPO = Path(__file__).resolve().parent.parent
 sys.path.insert(0, str(REPO))
 
-import flearn_amd  # noqa: E402
 from flearn_amd import _native as na  # noqa: E402
 from flearn_amd import aggregator as agg  # noqa: E402
 from flearn_amd import layouts  # noqa: E402
+from flearn_amd.aggregator import Aggregator  # noqa: E402
+from flearn_amd.bucket import RowTable, make_plan  # noqa: E402
+from flearn_amd.semantics import KIND_F32  # noqa: E402
 
 CONFIGS = {"ns": ("resnet50", 100, "mean"), "c3": ("resnet50", 100, "avgm"), "c2": ("resnet18", 100, "mean")}
 
@@ -55,61 +57,84 @@ def main():
         m = int(np.prod(s)) if s else 1
         offs.append((k, s, o, m))
         o += -(-m // 64) * 64
+    # the uploads hold the stack's values without a torch copy kernel (the PMC passes crashed the
+    # profiler inside torch's device-to-device copy): every tensor is generated in place with the
+    # stack's (seed, client, column) coordinates
     clients = []
     for i in range(n):
         d = {}
+        flat = None
         if a.alloc == "views":
-            flat = stack[i].clone()
-        for k, s, off, m in offs:
+            flat = torch.empty(stride, dtype=torch.float32, device=dev)
+            agg.fill_uniform(flat, seed=2024, row_begin=i)
+        for k, sh, off, m in offs:
             if a.alloc == "clones":
-                d[k] = stack[i, off : off + m].clone().view(s)
+                t = torch.empty(m, dtype=torch.float32, device=dev)
+                agg.fill_uniform(t, seed=2024, row_begin=i, col_begin=off)
+                d[k] = t.view(sh)
             elif a.alloc == "views":
-                d[k] = flat[off : off + m].view(s)
+                d[k] = flat[off : off + m].view(sh)
             else:
-                d[k] = stack[i, off : off + m].view(s)
+                d[k] = stack[i, off : off + m].view(sh)
         clients.append(d)
-    ups = [{"agg_weight": 1.0, "params": c} for c in clients]
     w = torch.ones(n, dtype=torch.float32, device=dev)
     out = torch.empty(stride, dtype=torch.float32, device=dev)
-    if op == "mean":
-        s = flearn_amd.AVG(output="device")
-        kw = {}
-    else:
-        s = flearn_amd.AVGM(server_side=True, output="device")
-        prev = torch.empty((1, stride), dtype=torch.float32, device=dev)
-        agg.fill_uniform(prev, seed=1)
-        s.server_opt.init_global({k: prev[0, off : off + m].view(sh).cpu().numpy() for k, sh, off, m in offs})
+    out_rows = torch.empty(stride, dtype=torch.float32, device=dev)
+    eng = Aggregator(output="device")
+    plan = make_plan([1.0] * n, clients)
+    if op != "mean":  # double-buffered (prev, v_t) per kernel, same initial state
+        pv, pr = ([torch.empty(stride, dtype=torch.float32, device=dev) for _ in range(2)] for _ in range(2))
+        agg.fill_uniform(pv[0], seed=1)
+        agg.fill_uniform(pr[0], seed=1)
         v = [torch.zeros(stride, dtype=torch.float64, device=dev) for _ in range(2)]
-        pv = [prev[0], torch.empty(stride, dtype=torch.float32, device=dev)]
-        kw = dict(op=na.OP_BY_NAME[op])
-    for _ in range(2):
-        s.server(ups, 0)
-    assert s.engine.packer.last_row_tables.get("f32") == "rows" or "rows" in s.engine.packer.last_row_tables.values(), \
-        s.engine.packer.last_row_tables
-    t_rows, t_stack = [], []
-    cur = 0
-    for r in range(a.reps):
-        e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
-        e0.record()
-        s.server(ups, r)
-        e1.record()
+        vr = [torch.zeros(stride, dtype=torch.float64, device=dev) for _ in range(2)]
+
+    def rows_launch(cur):
+        (sh, table), = eng.packer.pack(plan, clients)[KIND_F32]
+        assert isinstance(table, RowTable), type(table)
+        if op == "mean":
+            agg.reduce_stack(table, w, na.MODE_W32_DIV64, float(n), out32=out_rows)
+        else:
+            agg.reduce_stack(table, w, na.MODE_W32_DIV64, float(n), out32=pr[1 - cur], prev=pr[cur], v=vr[cur],
+                             v_out=vr[1 - cur], op=na.OP_BY_NAME[op])
+
+    def stack_launch(cur):
         if op == "mean":
             agg.reduce_stack(stack, w, na.MODE_W32_DIV64, float(n), out32=out)
         else:
             agg.reduce_stack(stack, w, na.MODE_W32_DIV64, float(n), out32=pv[1 - cur], prev=pv[cur], v=v[cur],
-                             v_out=v[1 - cur], **kw)
-            cur ^= 1
+                             v_out=v[1 - cur], op=na.OP_BY_NAME[op])
+
+    cur = 0
+    for _ in range(2):
+        rows_launch(cur)
+        stack_launch(cur)
+        cur ^= 1
+    torch.cuda.synchronize()
+    # compare the tensors' columns only (the stack's alignment gaps hold fill values the row
+    # kernel never reads or writes)
+    a_, b_ = (out_rows if op == "mean" else pr[cur]), (out if op == "mean" else pv[cur])
+    same = all(bool(torch.equal(a_[off : off + m].view(torch.int32), b_[off : off + m].view(torch.int32)))
+               for _, _, off, m in offs)
+    t_rows, t_stack = [], []
+    for r in range(a.reps):
+        e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+        e0.record()
+        rows_launch(cur)
+        e1.record()
+        stack_launch(cur)
         e2.record()
+        cur ^= 1
         torch.cuda.synchronize()
         t_rows.append(e0.elapsed_time(e1) * 1e3)
         t_stack.append(e1.elapsed_time(e2) * 1e3)
     alg = n * p * 4 + p * 4 + (0 if op == "mean" else p * 4 + 2 * p * 8)
-    print(json.dumps({"config": a.config, "alloc": a.alloc, "clients": n, "params": p,
-                      "server_call_us_median": round(float(np.median(t_rows)), 1),
+    print(json.dumps({"config": a.config, "alloc": a.alloc, "clients": n, "params": p, "bit_equal": same,
+                      "rows_us_median": round(float(np.median(t_rows)), 1),
                       "stack_kernel_us_median": round(float(np.median(t_stack)), 1),
                       "stack_frac": round(alg / float(np.median(t_stack)) / 8e6, 4),
-                      "note": "server_call = the whole AVG.server call on the stream (row kernel + its small launches); "
-                              "take the row kernel's own time from rocprof"}))
+                      "note": "rows = the pointer-table H2D + the row kernel on the stream; the kernel's own "
+                              "time from rocprof"}))
 
 
 if __name__ == "__main__":

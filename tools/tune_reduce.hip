@@ -1053,6 +1053,16 @@ int main(int argc, char** argv) {
       RMXL(4, 4, 1);
     }
   }
+  if (!strcmp(set, "xl4")) {  // KG = 4 (C5): whole-line f64 stores at epilogue batch 1 / 2 (no scratch) vs the product
+    for (int rep = 0; rep < 2; ++rep) {
+      RMXL(4, 4, 0);
+      RMXL(4, 1, 1);
+      RMXL(4, 2, 1);
+      RMXL(4, 1, 0);
+      vs.push_back(op == FA_OP_AVGM ? make_rowmajor_xl<8, 1, 8, 4, FA_OP_AVGM, double, 4, 1>(stack, stride, n, w, ncols, e, bytes, 192)
+                                    : make_rowmajor_xl<8, 1, 8, 4, FA_OP_ADAGRAD, double, 4, 1>(stack, stride, n, w, ncols, e, bytes, 192));
+    }
+  }
   if (!strcmp(set, "nlb")) {  // narrow strips per wave (LB bytes per lane) vs the product's narrow kernel
     NARROW(40, 1);
     NARROW(32, 1);
