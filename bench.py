@@ -317,7 +317,7 @@ def run_job(cfg, layout, n, args, world, rank, dev, g_eff):
     return job, step_s, wall, info
 
 
-def verify_job(job, cfg, world, dev) -> dict:
+def verify_job(job, cfg, world, dev, emulated: bool = False) -> dict:
     """After the timed region: prove the reassembled global model right (flearn_amd.verify).
     Windows on every slice start / rank boundary / replicated-tail edge (>= 64) are regenerated
     for all N clients and reduced UNSHARDED with the same kernel; the bucket the sharded step
@@ -358,7 +358,7 @@ def verify_job(job, cfg, world, dev) -> dict:
         def compare(a, b):
             a64, b64 = a.double(), b.double()
             return bool(torch.linalg.vector_norm(a64 - b64) <= 1e-6 * torch.linalg.vector_norm(b64))
-    res = verify.check_step(plan, full, expect, state=state, width=width, compare=compare)
+    res = verify.check_step(plan, full, expect, state=state, width=width, compare=compare, local_model=emulated)
     res["comparison"] = "<= 1e-6 normwise (--reorder)" if job.reorder else "bitwise"
     res["what"] = ("the returned global bucket vs the unsharded same-kernel reduce of regenerated inputs, on "
                    "windows at every stripe/rank slice boundary and replicated-tail edge"
@@ -578,7 +578,7 @@ def main():
     check = None
     if not args.no_verify:
         log(f"[rank {rank}] verifying the reassembled model ...")
-        check = verify_job(job, cfg, world, dev)
+        check = verify_job(job, cfg, world, dev, emulated=bool(emu))
         if rank == 0:
             log(f"[rank 0] verified={check['verified']} windows={check['windows']} "
                 f"mismatched={check['mismatched_windows']}")

@@ -711,7 +711,8 @@ class Aggregator:
         for kind, g in plan.groups.items():
             tdt = _TORCH[_STORE[kind]]
             pieces = Packer._pieces(g, [Shard(0, dev, 0, g.stride)])
-            host = torch.zeros((n, g.stride), dtype=tdt, pin_memory=True)
+            # one spare row: the split zero-copy round's partial sum (below)
+            host = torch.zeros((n + 1, g.stride), dtype=tdt, pin_memory=True)
             if not _NativeRows.usable(pieces, [host]):
                 plan.memo[key] = False
                 return None
@@ -732,19 +733,23 @@ class Aggregator:
                 args = (stack.data_ptr(), g.stride, n, nm.mode, w.data_ptr(), float(nm.denom), 0, g.stride, None,
                         None if f64 else dout.data_ptr(), dout.data_ptr() if f64 else None)
                 if zc and n >= 4 and nm.mode in (na.MODE_W32_DIV64, na.MODE_W32_DIV32):
-                    # two launches, so the second half is packed while the first is summed: rows
-                    # [0, h) into their fp32 sum (W = 1: the epilogue returns the sum itself),
-                    # written over row h-1, then rows [h-1, n) with weight fl32(1.0) on that row —
-                    # fl32(1 * acc) = acc, so the chain of adds is the single launch's, bit for bit
+                    # two launches, so the second half is packed while the first is summed: clients
+                    # [0, h) sit in rows [0, h) and are summed in fp32 (W = 1: the epilogue returns
+                    # the sum itself) into row h, which that launch does not read; clients [h, n)
+                    # are packed one row down, into rows [h+1, n+1), and the second launch sums rows
+                    # [h, n+1) — the partial with weight fl32(1.0), then the rest: fl32(1 * acc) =
+                    # acc, so the chain of adds is the single launch's, bit for bit, and no launch
+                    # ever writes a row it reads
                     h = n // 2
                     row = g.stride * 4
                     w_b = torch.cat([torch.ones(1, dtype=torch.float32, device=dev), w[h:]])
-                    part = host.data_ptr() + (h - 1) * row
+                    part = host.data_ptr() + h * row
                     args_a = (host.data_ptr(), g.stride, h, na.MODE_W32_DIV32, w.data_ptr(), 1.0, 0, g.stride, None,
                               part, None)
                     args_b = (part, g.stride, n - h + 1, nm.mode, w_b.data_ptr(), float(nm.denom), 0, g.stride, None,
                               None if f64 else dout.data_ptr(), dout.data_ptr() if f64 else None)
-                    split = (h, args_a, args_b, w_b)
+                    nat_b = _NativeRows(pieces, [host[1:]], w_local_lst, [None] * n)  # client i -> row i+1
+                    split = (h, args_a, args_b, w_b, nat_b)
             else:
                 fn = L.fa_reduce_f64 if kind == KIND_F64 else L.fa_reduce_i64
                 args = (stack.data_ptr(), g.stride, n, w.data_ptr(), float(nm.denom), 0, g.stride, dout.data_ptr())
@@ -794,9 +799,9 @@ class Aggregator:
         sh = stream.cuda_stream
         for nat, host, stack, w, dout, hout, hnp, fn, args, out, split in kinds:
             if split is not None:  # zero-copy in two launches: the second half packed meanwhile
-                h, args_a, args_b, _ = split
+                h, args_a, args_b, _, nat_b = split
                 na.check(fn(*args_a, sh), fn.__name__)
-                if pack(lst, nat.keys, len(nat.keys), nat.ptr, h, n) != 0:
+                if pack(lst, nat_b.keys, len(nat_b.keys), nat_b.ptr, h, n) != 0:
                     stream.synchronize()  # the first launch must be done with the staging
                     return None
                 na.check(fn(*args_b, sh), fn.__name__)
@@ -804,7 +809,7 @@ class Aggregator:
             if stack is host:  # zero-copy record
                 na.check(fn(*args, sh), fn.__name__)
                 continue
-            stack.copy_(host, non_blocking=True)
+            stack.copy_(host[: stack.shape[0]], non_blocking=True)
             na.check(fn(*args, sh), fn.__name__)
             hout.copy_(dout, non_blocking=True)
         stream.synchronize()  # also: the staging may be rewritten by the next call

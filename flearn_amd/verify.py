@@ -84,7 +84,7 @@ def segment_windows(plan, width: int = 4096) -> list:
 
 
 def check_step(plan, full: torch.Tensor, expect, state: torch.Tensor | None = None, group=None,
-               width: int = 4096, count: int = 64, compare=None) -> dict:
+               width: int = 4096, count: int = 64, compare=None, local_model: bool = False) -> dict:
     """Check one reassembled step.
 
     full   : the global fp32 bucket the step returned (at least plan.n_cols columns)
@@ -92,16 +92,25 @@ def check_step(plan, full: torch.Tensor, expect, state: torch.Tensor | None = No
              regenerated window (state only when `state` is given)
     state  : this rank's local state buffer after the step (a fused optimizer's v_t) or None
     compare: compare(got, want) -> bool (default: bitwise)
+    local_model: `full` holds only this rank's local columns (no gather: bench.py --emulate-world);
+             the model is then checked on the local segment windows, like the state
     Returns {"windows" (model windows, checked on every rank), "state_windows" and
     "mismatched_windows" (summed over the ranks of `group` when torch.distributed is
     initialised), "first_mismatches" (this rank's), "verified"}."""
     cmp = compare or bits_equal
-    wins = boundary_windows(plan, width, count)
     bad = []
-    for g0, w in wins:
-        want, _ = expect(g0, w)
-        if not cmp(full[g0 : g0 + w], want[:w]):
-            bad.append(("model", g0))
+    if local_model:
+        wins = segment_windows(plan, width)
+        for lo, g0, w in wins:
+            want, _ = expect(g0, w)
+            if not cmp(full[lo : lo + w], want[:w]):
+                bad.append(("model", g0))
+    else:
+        wins = boundary_windows(plan, width, count)
+        for g0, w in wins:
+            want, _ = expect(g0, w)
+            if not cmp(full[g0 : g0 + w], want[:w]):
+                bad.append(("model", g0))
     swins = segment_windows(plan, width) if state is not None else []
     for lo, g0, w in swins:
         _, want_v = expect(g0, w)

@@ -171,3 +171,18 @@ def test_wrong_gather_offset_fails_the_run(world, op):
 def test_corrupted_state_slice_edge_fails_the_run():
     """v_t is never gathered: each rank checks its own slice edges, and the verdict is shared."""
     assert _run(2, 5, 30_001, 2, "avgm", "state_edge") == verify.EXIT_MISMATCH
+
+
+def test_local_model_windows_for_an_emulated_rank():
+    """bench.py --emulate-world: one process holds rank 0's columns only (no gather); the model
+    is checked on that rank's local segment windows, mapped to their global columns."""
+    plan = ShardPlan.make(50_003, 4, 0, 2)
+    glob = torch.arange(plan.full_cols + 4096, dtype=torch.float32)
+    local = torch.zeros(plan.local_cols)
+    for lo, g0, w in plan.segments():
+        local[lo : lo + w] = glob[g0 : g0 + w]
+    res = verify.check_step(plan, local, lambda g0, w: (glob[g0 : g0 + w], None), width=512, local_model=True)
+    assert res["verified"] and res["windows"] == len(verify.segment_windows(plan, 512))
+    local[plan.local_begin(1)] += 1
+    assert not verify.check_step(plan, local, lambda g0, w: (glob[g0 : g0 + w], None), width=512,
+                                 local_model=True)["verified"]
