@@ -176,11 +176,21 @@ def plan_shards(n_cols: int, world: int, model: StripeModel, max_stripes: int = 
     return best[0], best[1]
 
 
-def shard_candidates(n_cols: int, world: int, model: StripeModel, max_stripes: int = 8) -> list:
+#: the reduce's and a concurrent all-gather stand-in's slowdowns measured on one MI355X
+#: (tools/overlap_probe.py, profiles/r04/overlap/: a 32-64-block copy at 0.3-0.55 TB/s beside the
+#: default-grid reduce) — the prior for the contended candidate plans
+CONTENTION_PRIOR = (0.37, 0.82)
+
+
+def shard_candidates(n_cols: int, world: int, model: StripeModel, max_stripes: int = 8,
+                     contention=CONTENTION_PRIOR) -> list:
     """The plans a measured trial chooses among (bench.py times each for a few steps on the
     running job): plan_shards' best, the best plan with no replicated tail, and the best with
-    half and with 1.5x the best's tail — the model ignores that RCCL's kernels and the reduce
-    share CUs and HBM bandwidth, so its overlap is the optimistic end and the measured step picks."""
+    half and with 1.5x the best's tail; then the best plan of the same model with the measured
+    one-GPU contention terms (RCCL's kernels and the reduce share CUs and HBM: a concurrent
+    gather slows the reduce by ~1/3 and itself ~1.8x, profiles/r04/overlap/) and the plain
+    serial plan — one stripe, no overlap at all.  The model's overlap is the optimistic end; the
+    measured step picks."""
     best = plan_shards(n_cols, world, model, max_stripes)
     out = [best]
     if world < 2:
@@ -196,6 +206,10 @@ def shard_candidates(n_cols: int, world: int, model: StripeModel, max_stripes: i
     cands = [(plan_stripes(-(-max(n_cols, 1) // world), model, max_stripes), 0)]
     if best[1] >= 4 * world * ALIGN:
         cands += [with_tail(best[1] // 2), with_tail(min(int(best[1] * 1.5), int(n_cols * 0.75)))]
+    if contention is not None and (model.c_r, model.c_g) == (0.0, 0.0):
+        cands.append(plan_shards(n_cols, world, model.with_contention(*contention), max_stripes))
+    lc = -(-max(n_cols, 1) // world)
+    cands.append(((-(-lc // ALIGN) * ALIGN,), 0))  # serial: reduce everything, then one gather
     for c in cands:
         if c is not None and c not in out:
             out.append(c)

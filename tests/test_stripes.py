@@ -121,6 +121,13 @@ def test_shard_candidates_for_the_measured_trial(world):
         plan = ShardPlan.from_widths(p, world, 0, w, rep=rep)
         assert plan.full_cols >= p
     assert shard_candidates(p, 1, m) == [plan_shards(p, 1, m)]
+    # the serial plan (one stripe, no tail: no overlap to lose to contention) is always tried,
+    # and so is the plan of the model with the measured contention terms
+    lc = -(-p // world)
+    assert ((-(-lc // ALIGN) * ALIGN,), 0) in [(tuple(w), r) for w, r in c]
+    from flearn_amd.dist import CONTENTION_PRIOR
+    cp = plan_shards(p, world, m.with_contention(*CONTENTION_PRIOR))
+    assert (tuple(cp[0]), cp[1]) in [(tuple(w), r) for w, r in c]
 
 
 def test_makespan_contention_terms():
