@@ -222,6 +222,7 @@ def calibrate(job: Job, world: int, dev, reps: int = 5):
     out = job.red.local_out
     r_big = _event_time(lambda: job.fn(0, big, out[:big]), reps)
     r_small = _event_time(lambda: job.fn(0, small, out[:small]), reps)
+    r_conc = g_conc = None
     if world > 1:
         full = torch.empty(world * big, dtype=torch.float32, device=dev)
         for _ in range(2):  # RCCL's first calls set up channels / buffers
@@ -231,14 +232,61 @@ def calibrate(job: Job, world: int, dev, reps: int = 5):
         dist.barrier()
         g_big = _event_time(lambda: all_gather_into(full, out[:big]), reps)
         g_small = _event_time(lambda: all_gather_into(full[: world * small], out[:small]), reps)
+        r_conc, g_conc = _contention(job, full, out, big, dev, reps)
         del full
     else:
         m = StripeModel.assumed(job.n, p.world)
         g_big, g_small = m.a_g + m.b_g * big, m.a_g + m.b_g * small
-    r_big, r_small, g_big, g_small = _max_over_ranks((r_big, r_small, g_big, g_small), world, dev)
-    return StripeModel.fit(big, small, r_big, r_small, g_big, g_small), dict(
-        width_cols=[big, small], reduce_us=[round(r_big * 1e6, 2), round(r_small * 1e6, 2)],
-        gather_us=[round(g_big * 1e6, 2), round(g_small * 1e6, 2)], measured_gather=world > 1)
+    vals = (r_big, r_small, g_big, g_small) + ((r_conc, g_conc) if r_conc is not None else ())
+    vals = _max_over_ranks(vals, world, dev)
+    r_big, r_small, g_big, g_small = vals[:4]
+    c_r = c_g = 0.0
+    cal = dict(width_cols=[big, small], reduce_us=[round(r_big * 1e6, 2), round(r_small * 1e6, 2)],
+               gather_us=[round(g_big * 1e6, 2), round(g_small * 1e6, 2)], measured_gather=world > 1)
+    if r_conc is not None:
+        r_conc, g_conc = vals[4:]
+        # the slowdown each stream saw while the other ran (equal widths: the shorter one was
+        # concurrent for all of its time, the longer one for part of it — an effective value)
+        c_r, c_g = max(r_conc / r_big - 1.0, 0.0), max(g_conc / g_big - 1.0, 0.0)
+        cal.update(concurrent_reduce_us=round(r_conc * 1e6, 2), concurrent_gather_us=round(g_conc * 1e6, 2),
+                   c_r=round(c_r, 4), c_g=round(c_g, 4))
+    return StripeModel.fit(big, small, r_big, r_small, g_big, g_small, c_r=c_r, c_g=c_g), cal
+
+
+def _contention(job, full, out, cols, dev, reps: int):
+    """The reduce and the all-gather of the whole local width run concurrently (real RCCL over
+    xGMI at N > 1): (reduce time beside the gather, gather time beside the reduce), each taken on
+    the stream of the one being measured.  Host-staged gloo gathers are synchronous: no overlap."""
+    side = torch.cuda.Stream(dev)
+    out2 = torch.empty_like(out)
+    cur = torch.cuda.current_stream(dev)
+    r_t, g_t = [], []
+    for _ in range(reps):
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        # (a) the reduce on this stream, the gather issued first on RCCL's
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(cur)
+        w = all_gather_into(full, out[:cols], async_op=True)
+        job.fn(0, cols, out2[:cols])
+        e1.record(cur)
+        if w is not None:
+            w.wait()
+        torch.cuda.synchronize(dev)
+        r_t.append(e0.elapsed_time(e1) / 1e3)
+        dist.barrier()
+        # (b) the gather enqueued on this stream's order, the reduce on a side stream
+        e2, e3 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        side.wait_stream(cur)
+        e2.record(cur)
+        with torch.cuda.stream(side):
+            job.fn(0, cols, out2[:cols])
+        all_gather_into(full, out[:cols])
+        e3.record(cur)
+        cur.wait_stream(side)
+        torch.cuda.synchronize(dev)
+        g_t.append(e2.elapsed_time(e3) / 1e3)
+    return float(np.median(r_t)), float(np.median(g_t))
 
 
 def run_job(cfg, layout, n, args, world, rank, dev, g_eff):
@@ -281,7 +329,8 @@ def run_job(cfg, layout, n, args, world, rank, dev, g_eff):
                                    "fitted on this job" + ("; the fastest of the model's plan and its neighbours "
                                                            "over 5 measured steps each" if trials else "")),
                     model={"a_r_us": round(model.a_r * 1e6, 3), "b_r_ns_per_col": round(model.b_r * 1e9, 5),
-                           "a_g_us": round(model.a_g * 1e6, 3), "b_g_ns_per_col": round(model.b_g * 1e9, 5)},
+                           "a_g_us": round(model.a_g * 1e6, 3), "b_g_ns_per_col": round(model.b_g * 1e9, 5),
+                           "c_r": round(model.c_r, 4), "c_g": round(model.c_g, 4)},
                     calibration=cal, predicted_ms=round(pred * 1e3, 4),
                     predicted_exposed_gather_ms=round(exposed * 1e3, 4))
         if trials:

@@ -45,6 +45,12 @@ def test_bench_two_ranks_rehearsal(config, cuda):
     assert d["config"]["clients"] == 100  # the fixed problem
     mg = d["multi_gpu"]
     assert mg["calibration"]["measured_gather"] is True
+    # the reduce / gather contention of this node, measured concurrently, is in the fitted model
+    cal = mg["calibration"]
+    assert cal["c_r"] >= 0 and cal["c_g"] >= 0 and cal["concurrent_reduce_us"] > 0
+    assert mg["model"]["c_r"] == cal["c_r"] and mg["model"]["c_g"] == cal["c_g"]
+    # the serial plan (one stripe, no tail) is among the measured trials
+    assert any(len(t["stripe_widths"]) == 1 and t["replicated_cols"] == 0 for t in mg["plan_trials"])
     # stripes (padded) or stripes + a replicated tail cover the bucket
     assert sum(mg["stripe_widths"]) * 2 + mg["replicated_cols"] >= d["config"]["params"]
     if mg["replicated_cols"]:
