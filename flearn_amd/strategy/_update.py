@@ -250,6 +250,10 @@ class DeviceUpdater:
             self._v_next = None
             self._stage = None
         st = self._staging(lay, total, tdt, dev)
+        ev = getattr(self, "_h2d_done", None)
+        if ev is not None:  # update_on_device's DMAs out of the shared pinned staging are done
+            ev.synchronize()
+            self._h2d_done = None
         if self.zero_copy:
             return self._device_step_zc(w_local, glob, local, lay, total, tdt, dev, **override)
         lh, gh, oh, pack_l, pack_g = st
@@ -413,6 +417,120 @@ class DeviceUpdater:
         fresh = res.numpy()
         for k, s, o, n in lay:  # replaced per key, like the reference (avgm.py:34-35, opt.py:62-63)
             w_local[k] = fresh[o : o + n].reshape(s)
+
+    # ---- the model already on the GPU (client_receive with a CUDA model) ---------------------
+    @staticmethod
+    def device_model_ok(weights, w_glob) -> bool:
+        """True when client_receive can update the model where it lives: every state_dict value
+        a contiguous float32 CUDA tensor on one device, and every w_glob value an ndarray of the
+        same shape, all float64 or all float32 (what the server returns for fp32 models).
+        Anything else — BN counters (whose numpy scalars make the reference's convert_to_tensor
+        raise), CPU models, other dtypes — takes the reference's host path unchanged."""
+        if not weights or not w_glob:
+            return False
+        devs = set()
+        for v in weights.values():
+            if not (isinstance(v, torch.Tensor) and v.is_cuda and v.dtype == torch.float32 and v.is_contiguous()):
+                return False
+            devs.add(v.device)
+        if len(devs) != 1:
+            return False
+        gdt = None
+        for k, g in w_glob.items():
+            lv = weights.get(k)
+            if lv is None or type(g) is not np.ndarray or g.dtype not in (np.float64, np.float32):
+                return False
+            if tuple(g.shape) != tuple(lv.shape):
+                return False
+            if gdt is None:
+                gdt = g.dtype
+            elif g.dtype != gdt:
+                return False
+        return True
+
+    def update_on_device(self, local: dict, w_glob: dict, **override) -> dict:
+        """The update of a model that lives on the GPU: w_local's values are the model's float32
+        CUDA tensors (gathered in one launch, fa_gather_rows), w_glob's host arrays go to the GPU
+        in chunks (packed by the pool into pinned staging, one DMA each) and each chunk's update
+        runs as soon as it lands.  Returns {key: the new value as a CUDA tensor in w_glob's dtype}
+        for w_glob's keys — what load_state_dict then casts into the float32 parameters, exactly
+        as it casts the reference's float64 host arrays.  Only the server's model crosses PCIe
+        (the reference moves the local model down and the result back up as well).  v_t is the
+        same double-buffered state the host path keeps, so the two paths may alternate."""
+        na.lib()
+        glob = {k: np.ascontiguousarray(g) for k, g in w_glob.items()}
+        gdt = next(iter(glob.values())).dtype
+        tdt = torch.float64 if gdt == np.float64 else torch.float32
+        dev = next(iter(local.values())).device
+        lay, total = self._layout(glob)
+        if self.v is not None and (self.layout != lay or self.v.dtype != tdt):
+            raise ValueError("the model layout or w_glob's dtype changed between rounds: v_t no longer matches; "
+                             "call reset() to start the optimizer state afresh")
+        if self.v is None:
+            self.layout = lay
+            self.v = torch.zeros(total, dtype=tdt, device=dev)
+            self._v_next = None
+            self._stage = None
+        self._staging(lay, total, tdt, dev)
+        gh = self._stage[1]
+        ev = getattr(self, "_h2d_done", None)
+        if ev is not None:  # the previous call's DMAs out of the pinned staging are complete
+            ev.synchronize()
+        key = ("devmodel", self._stage[1].data_ptr(), str(dev))
+        db = getattr(self, "_devbuf", None)
+        if db is None or db[0] != key:
+            segs = torch.tensor([o for _, _, o, _ in lay] + [n for _, _, _, n in lay], dtype=torch.int64).to(dev)
+            db = self._devbuf = (key, torch.zeros(total, dtype=torch.float32, device=dev),
+                                 torch.empty(total, dtype=tdt, device=dev), torch.empty(total, dtype=tdt, device=dev),
+                                 segs, torch.empty(len(lay), dtype=torch.int64, pin_memory=True),
+                                 torch.empty(len(lay), dtype=torch.int64, device=dev))
+        _, dl, dg, dout, segs, ptr_h, ptr_d = db
+        if self._v_next is None or self._v_next.shape != self.v.shape or self._v_next.dtype != self.v.dtype:
+            self._v_next = torch.empty_like(self.v)
+        v_in, v_out = self.v, self._v_next
+        from ..aggregator import _epilogue
+
+        L = na.lib()
+        prec = na.PREC_F64 if tdt == torch.float64 else na.PREC_F32
+        p = dict(self.params, **override)
+        chunks = self._chunks(lay, total, tdt)
+        pool = _pool()
+        futs = [[pool.submit(t) for t in pack_g.tasks(glob)] for _f, _e, _pl, pack_g, _g in chunks]
+        with torch.cuda.device(dev):
+            stream = torch.cuda.current_stream(dev)
+            sh = stream.cuda_stream
+            try:
+                # the local model: one gather launch of every tensor into its layout slot
+                ptr_h.numpy()[:] = [local[k].data_ptr() for k, _, _, _ in lay]
+                ptr_d.copy_(ptr_h, non_blocking=True)
+                na.check(L.fa_gather_rows(dl.data_ptr(), total, 1, 4, ptr_d.data_ptr(), segs.data_ptr(), len(lay), sh),
+                         "fa_gather_rows")
+                for (first, end, _pl, _pg, g), fg in zip(chunks, futs):
+                    if any(f.result() for f in fg):  # a value the native pack refuses: copy in Python
+                        for k, _s, o, n in g:
+                            gh.numpy()[o : o + n] = glob[k].reshape(-1)
+                    dg[first:end].copy_(gh[first:end], non_blocking=True)
+                    epi = _epilogue(self.op, dl[first:end], v_in[first:end], p["beta"], p["eta"], p["tau"], p["beta2"],
+                                    v_out=v_out[first:end])
+                    out = dout[first:end].data_ptr()
+                    na.check(L.fa_opt_apply(prec, ctypes.byref(epi), dl[first:end].data_ptr(), dg[first:end].data_ptr(),
+                                            end - first, None if prec == na.PREC_F64 else out,
+                                            out if prec == na.PREC_F64 else None, sh), "fa_opt_apply")
+            except BaseException:
+                for fg in futs:
+                    for f in fg:
+                        f.cancel()
+                concurrent.futures.wait([f for fg in futs for f in fg])
+                stream.synchronize()
+                raise
+            done = torch.cuda.Event()
+            done.record(stream)
+        self._h2d_done = done
+        self.v, self._v_next = v_out, v_in
+        # fresh result buffer per call: the returned tensors must not be overwritten by the next
+        res = dout
+        self._devbuf = db[:3] + (torch.empty(total, dtype=tdt, device=dev),) + db[4:]
+        return {k: res[o : o + n].view(s) for k, s, o, n in lay}
 
     def _staging(self, lay, total, tdt, dev):
         """Pinned staging for this layout, reused across calls (zeroed once: only the segments

@@ -39,12 +39,15 @@ class AVGM(AVG):
         return {"w_glob": self._ensemble_or_exit(ensemble_params_lst, server_opt=self.server_opt)}
 
     # ---- client --------------------------------------------------------------------------
+    def _get_updater(self):
+        if self._updater is None:
+            self._updater = DeviceUpdater("avgm", self.__dict__.get("device"))
+        return self._updater
+
     def mean_momentum(self, w_local, w_glob, beta):
         """avgm.py:19-36: delta = w_glob - w_local; v_t = delta + beta*v_t; w_local += v_t."""
         self.beta = beta
-        if self._updater is None:
-            self._updater = DeviceUpdater("avgm", self.__dict__.get("device"))
-        return self._updater(w_local, w_glob, beta=beta)
+        return self._get_updater()(w_local, w_glob, beta=beta)
 
     @property
     def v_t(self):
@@ -54,7 +57,15 @@ class AVGM(AVG):
         if self.server_side:
             return super().client_receive(trainer, server_p_bytes)
         server_p = self.receive_processing(server_p_bytes)
-        w_local = convert_to_np(trainer.weight)
+        weights = trainer.weight
+        if DeviceUpdater.device_model_ok(weights, server_p["w_glob"]):
+            # the model lives on the GPU: update it there (only w_glob crosses PCIe); the values
+            # load_state_dict receives are the reference's float64 results, cast the same way
+            self.beta = beta
+            new = self._get_updater().update_on_device(weights, server_p["w_glob"], beta=beta)
+            trainer.model.load_state_dict({**weights, **new})
+            return server_p
+        w_local = convert_to_np(weights)
         w_local = self.mean_momentum(w_local, server_p["w_glob"], beta)
         trainer.model.load_state_dict(convert_to_tensor(w_local))
         return server_p

@@ -45,6 +45,9 @@ class OPT(AVG):
     def adaptive_opt(self, w_local, w_glob, method):
         """opt.py:23-65: delta = w_glob - w_local; v_t update by `method`;
         w_local += eta*delta / (sqrt(v_t) + tau)."""
+        return self._get_updater(method)(w_local, w_glob)
+
+    def _get_updater(self, method):
         if method not in _METHODS:
             raise ValueError(method)
         # one v_t shared across methods, as the reference's single self.v_t attribute
@@ -55,7 +58,7 @@ class OPT(AVG):
         from .. import _native as na
 
         up.op = na.OP_BY_NAME[method]
-        return up(w_local, w_glob)
+        return up
 
     @property
     def v_t(self):
@@ -68,7 +71,13 @@ class OPT(AVG):
         server_p = self.receive_processing(server_p_bytes)
         method = method.lower()
         assert method in _METHODS
-        w_local = convert_to_np(trainer.weight)
+        weights = trainer.weight
+        if DeviceUpdater.device_model_ok(weights, server_p["w_glob"]):
+            # the model lives on the GPU: update it there (only w_glob crosses PCIe)
+            new = self._get_updater(method).update_on_device(weights, server_p["w_glob"])
+            trainer.model.load_state_dict({**weights, **new})
+            return server_p
+        w_local = convert_to_np(weights)
         w_local = self.adaptive_opt(w_local, server_p["w_glob"], method)
         trainer.model.load_state_dict(convert_to_tensor(w_local))
         return server_p

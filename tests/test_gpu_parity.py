@@ -1053,6 +1053,80 @@ def test_client_side_update_failure_mid_call_changes_nothing(op, transfer, cuda,
         prev = {k: np.asarray(got[k]).astype(np.float32) for k in shapes}
 
 
+class _Trainer:
+    """What flearn's client_receive touches: .model and .weight (Trainer.py:228-230)."""
+
+    def __init__(self, model):
+        self.model = model
+
+    @property
+    def weight(self):
+        return self.model.state_dict()
+
+
+def _cuda_model(seed, cuda):
+    torch.manual_seed(seed)
+    return torch.nn.Sequential(torch.nn.Conv2d(3, 8, 3), torch.nn.ReLU(), torch.nn.Flatten(),
+                               torch.nn.Linear(8 * 30 * 30, 65), torch.nn.LayerNorm(65),
+                               torch.nn.Linear(65, 10)).to(cuda)
+
+
+@pytest.mark.parametrize("op", ["avgm", "adagrad", "yogi"])
+@pytest.mark.parametrize("glob_dtype", [np.float64, np.float32])
+def test_client_receive_updates_a_cuda_model_in_place(op, glob_dtype, cuda, monkeypatch):
+    """client_receive with a model on the GPU (flearn trains there): the update runs where the
+    model lives (only w_glob crosses PCIe) and load_state_dict gets the reference's values — the
+    parameters equal, bit for bit, the reference's host path (convert_to_np -> numpy update ->
+    load_state_dict of the float64 arrays) over 3 rounds, v_t included; in small chunks too."""
+    from flearn_amd.strategy._update import DeviceUpdater
+
+    monkeypatch.setattr(DeviceUpdater, "chunk_bytes", 1 << 20)
+    monkeypatch.setattr(DeviceUpdater, "first_chunk_bytes", 1 << 18)
+    monkeypatch.setattr(DeviceUpdater, "last_chunk_bytes", 1 << 18)
+    model = _cuda_model(3, cuda)
+    tr = _Trainer(model)
+    s = AVGM() if op == "avgm" else OPT()
+    calls = {"dev": 0}
+    real = DeviceUpdater.update_on_device
+
+    def counted(self, *a, **k):
+        calls["dev"] += 1
+        return real(self, *a, **k)
+
+    monkeypatch.setattr(DeviceUpdater, "update_on_device", counted)
+    rng = np.random.default_rng(11)
+    v = None
+    for r in range(3):
+        local = {k: t.detach().cpu().numpy().copy() for k, t in model.state_dict().items()}
+        glob = {k: (a.astype(np.float64) + rng.standard_normal(a.shape)).astype(glob_dtype) for k, a in local.items()}
+        if op == "avgm":
+            want, v = oracle.mean_momentum(dict(local), glob, v, 0.9)
+            s.client_receive(tr, {"w_glob": glob}, 0.9)
+        else:
+            want, v = oracle.adaptive_opt(dict(local), glob, v, op)
+            s.client_receive(tr, {"w_glob": glob}, op)
+        got = {k: t.detach().cpu().numpy() for k, t in model.state_dict().items()}
+        for k in want:  # load_state_dict's cast of the reference's result
+            w32 = torch.from_numpy(np.asarray(want[k])).to(torch.float32).numpy()
+            assert got[k].tobytes() == w32.tobytes(), (op, r, k)
+        assert_dict_bitwise(s.v_t, v, f"{op} v{r}")
+    assert calls["dev"] == 3
+
+
+def test_client_receive_keeps_the_host_path_for_bn_models(cuda):
+    """A BN model's int64 counters make the reference's convert_to_tensor raise SystemError on the
+    numpy scalars its update returns; that model keeps the host path, and its behaviour."""
+    from flearn_amd.strategy._update import DeviceUpdater
+
+    model = torch.nn.Sequential(torch.nn.Linear(4, 4), torch.nn.BatchNorm1d(4)).to(cuda)
+    w = model.state_dict()
+    glob = {k: np.asarray(t.detach().cpu().numpy(), dtype=np.float64) for k, t in w.items()}
+    glob["1.num_batches_tracked"] = np.float64(0.0)
+    assert not DeviceUpdater.device_model_ok(w, glob)
+    with pytest.raises(SystemError):
+        AVGM().client_receive(_Trainer(model), {"w_glob": glob}, 0.9)
+
+
 @pytest.mark.parametrize("op", ["avgm", "adagrad", "adam"])
 def test_client_side_update_bn_model(op, cuda):
     """A BatchNorm model: the server's w_glob holds np.float64 scalars for the int64

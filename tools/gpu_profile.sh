@@ -16,8 +16,8 @@ cd /tmp && export TMPDIR=/tmp
 for e in ${ENTRIES:-ns:ns}; do
   IFS=: read -r tag cfg flags <<< "$e"
   flags=${flags//,/ }
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace_$tag -o $tag -- python3 $R/bench.py --config $cfg $flags --no-cpu-baseline > $O/trace_${tag}_bench.json 2> $O/trace_$tag.err
-  timeout -k 10 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/fetch_$tag -o $tag -- python3 $R/bench.py --config $cfg $flags --no-cpu-baseline --steps 5 --warmup 1 > /dev/null 2> $O/fetch_$tag.err
-  timeout -k 10 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/write_$tag -o $tag -- python3 $R/bench.py --config $cfg $flags --no-cpu-baseline --steps 5 --warmup 1 > /dev/null 2> $O/write_$tag.err
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace_$tag -o $tag -- python3 $R/bench.py --config $cfg $flags --no-cpu-baseline --no-verify > $O/trace_${tag}_bench.json 2> $O/trace_$tag.err
+  timeout -k 10 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/fetch_$tag -o $tag -- python3 $R/bench.py --config $cfg $flags --no-cpu-baseline --no-verify --steps 5 --warmup 1 > /dev/null 2> $O/fetch_$tag.err
+  timeout -k 10 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/write_$tag -o $tag -- python3 $R/bench.py --config $cfg $flags --no-cpu-baseline --no-verify --steps 5 --warmup 1 > /dev/null 2> $O/write_$tag.err
 done
 echo done

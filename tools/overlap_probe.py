@@ -55,6 +55,10 @@ def main():
     L.probe_copy_rep.restype = ctypes.c_int
     L.probe_spin.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p]
     L.probe_spin.restype = ctypes.c_int
+    L.probe_read.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p]
+    L.probe_read.restype = ctypes.c_int
+    L.probe_write.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_void_p]
+    L.probe_write.restype = ctypes.c_int
     na.lib()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
@@ -78,7 +82,21 @@ def main():
     small_dst = torch.empty_like(small)
     spin_out = torch.empty(256 * 256, dtype=torch.float32, device=dev)
 
+    sink = torch.empty(4096 * 256 * 4, dtype=torch.int32, device=dev)
+
     def copy_fn(kind):
+        if kind.startswith("rd"):  # HBM reads only
+            blocks = int(kind[2:])
+
+            def f():
+                assert L.probe_read(src.data_ptr(), nbytes // 16, blocks, sink.data_ptr(), sb.cuda_stream) == 0
+            return f
+        if kind.startswith("wr"):  # HBM writes only
+            blocks = int(kind[2:])
+
+            def f():
+                assert L.probe_write(dst.data_ptr(), nbytes // 16, blocks, sb.cuda_stream) == 0
+            return f
         if kind.startswith("spin"):  # ALU only, no memory traffic: do CUs / dispatch interfere?
             blocks = int(kind[4:])
 

@@ -16,25 +16,66 @@ import csv
 import json
 from pathlib import Path
 
-KERNEL = "reduce_kernel"
+KERNEL = "fa::reduce_kernel"  # the engine's reduce kernels (not torch's at::native::reduce_kernel)
 
 
-def per_dispatch(counter_csv: Path, counter: str, kernel: str = KERNEL):
-    vals = {}
-    with open(counter_csv) as f:
-        for row in csv.DictReader(f):
-            if kernel in row["Kernel_Name"] and row["Counter_Name"] == counter:
-                vals[row["Dispatch_Id"]] = vals.get(row["Dispatch_Id"], 0.0) + float(row["Counter_Value"])
-    return list(vals.values())
-
-
-def kernel_stats(stats_csv: Path, kernel: str = KERNEL):
+def dominant_kernel(stats_csv: Path, kernel: str = KERNEL):
+    """The engine reduce kernel with the largest total time in a rocprofv3 kernel_stats file: the
+    bench's own launches (bench.py's self-check adds narrow-window launches of other kernels)."""
+    best = None
     with open(stats_csv) as f:
         for row in csv.DictReader(f):
             if kernel in row["Name"]:
-                return {"name": row["Name"], "calls": int(row["Calls"]), "avg_ns": float(row["AverageNs"]),
-                        "min_ns": float(row["MinNs"]), "max_ns": float(row["MaxNs"])}
-    return None
+                tot = float(row.get("TotalDurationNs") or 0.0) or float(row["AverageNs"]) * int(row["Calls"])
+                if best is None or tot > best[0]:
+                    best = (tot, row)
+    return None if best is None else best[1]
+
+
+def per_dispatch(counter_csv: Path, counter: str, kernel: str = KERNEL, exact: str | None = None):
+    """Per-dispatch values of `counter` for the kernel named `exact` (else: every kernel whose
+    name contains `kernel`, keeping the name with the most bytes per dispatch)."""
+    vals, names, grids = {}, {}, {}
+    with open(counter_csv) as f:
+        for row in csv.DictReader(f):
+            name = row["Kernel_Name"]
+            if (name == exact if exact else kernel in name) and row["Counter_Name"] == counter:
+                vals[row["Dispatch_Id"]] = vals.get(row["Dispatch_Id"], 0.0) + float(row["Counter_Value"])
+                names[row["Dispatch_Id"]] = name
+                grids[row["Dispatch_Id"]] = int(row["Grid_Size"])
+    if vals:  # the bench's launches: the largest grid of each kernel (the self-check's windows are narrower)
+        top = {}
+        for d, g in grids.items():
+            top[names[d]] = max(top.get(names[d], 0), g)
+        vals = {d: v for d, v in vals.items() if grids[d] == top[names[d]]}
+    if exact or not vals:
+        return list(vals.values())
+    by = {}
+    for d, v in vals.items():
+        by.setdefault(names[d], []).append(v)
+    return max(by.values(), key=lambda xs: sum(xs) / len(xs))
+
+
+def kernel_stats(stats_csv: Path, kernel: str = KERNEL):
+    """The dominant kernel's launch statistics: from the kernel trace next to the stats file
+    (its largest-grid dispatches only: bench.py's own launches, not the self-check's narrow
+    windows), else from the stats file."""
+    row = dominant_kernel(stats_csv, kernel)
+    if row is None:
+        return None
+    trace = Path(str(stats_csv).replace("_kernel_stats.csv", "_kernel_trace.csv"))
+    if trace.exists():
+        durs = []
+        with open(trace) as f:
+            rows = [r for r in csv.DictReader(f) if r["Kernel_Name"] == row["Name"]]
+        if rows:
+            top = max(int(r["Grid_Size_X"]) for r in rows)
+            durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rows if int(r["Grid_Size_X"]) == top]
+        if durs:
+            return {"name": row["Name"], "calls": len(durs), "avg_ns": sum(durs) / len(durs), "min_ns": float(min(durs)),
+                    "max_ns": float(max(durs)), "from": "kernel trace, the bench's largest-grid dispatches"}
+    return {"name": row["Name"], "calls": int(row["Calls"]), "avg_ns": float(row["AverageNs"]),
+            "min_ns": float(row["MinNs"]), "max_ns": float(row["MaxNs"])}
 
 
 def main():
@@ -47,8 +88,12 @@ def main():
     ap.add_argument("--out", default="profiles/traffic.json")
     ap.add_argument("--source", default=None)
     a = ap.parse_args()
-    fetch = per_dispatch(Path(a.fetch), "FETCH_SIZE")
-    write = per_dispatch(Path(a.write), "WRITE_SIZE")
+    exact = None
+    if a.stats:
+        dk = dominant_kernel(Path(a.stats))
+        exact = dk["Name"] if dk is not None else None
+    fetch = per_dispatch(Path(a.fetch), "FETCH_SIZE", exact=exact)
+    write = per_dispatch(Path(a.write), "WRITE_SIZE", exact=exact)
     if not fetch or not write:
         raise SystemExit("no reduce_kernel dispatches with FETCH_SIZE / WRITE_SIZE found")
     f_kib = sum(fetch) / len(fetch)

@@ -48,3 +48,34 @@ extern "C" int probe_spin(float* out, int32_t blocks, int32_t iters, void* strea
   hipLaunchKernelGGL(probe_spin_k, dim3((unsigned)blocks), dim3(256), 0, static_cast<hipStream_t>(stream), out, iters);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
+
+// read-only stream (no stores but one per block): does the reduce suffer from foreign READS as
+// much as from a copy's read + write mix (HBM bus turnaround)?
+__global__ __launch_bounds__(256) void probe_read16(const uint4* __restrict__ src, int64_t n, uint4* __restrict__ sink) {
+  uint4 acc = {0u, 0u, 0u, 0u};
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const uint4 v = src[i];
+    acc.x ^= v.x; acc.y ^= v.y; acc.z ^= v.z; acc.w ^= v.w;
+  }
+  if ((acc.x & 0x7fffffffu) == 0x12345678u) sink[blockIdx.x * 256 + threadIdx.x] = acc;  // keeps the loads
+}
+
+// write-only stream
+__global__ __launch_bounds__(256) void probe_write16(uint4* __restrict__ dst, int64_t n) {
+  const uint4 v = {1u, 2u, 3u, 4u};
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) dst[i] = v;
+}
+
+extern "C" int probe_read(const void* src, int64_t n16, int32_t blocks, void* sink, void* stream) {
+  if (!src || !sink || n16 <= 0 || blocks <= 0 || blocks > 4096) return -1;
+  hipLaunchKernelGGL(probe_read16, dim3((unsigned)blocks), dim3(256), 0, static_cast<hipStream_t>(stream),
+                     static_cast<const uint4*>(src), n16, static_cast<uint4*>(sink));
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+extern "C" int probe_write(void* dst, int64_t n16, int32_t blocks, void* stream) {
+  if (!dst || n16 <= 0 || blocks <= 0) return -1;
+  hipLaunchKernelGGL(probe_write16, dim3((unsigned)blocks), dim3(256), 0, static_cast<hipStream_t>(stream),
+                     static_cast<uint4*>(dst), n16);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
