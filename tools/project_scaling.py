@@ -34,19 +34,26 @@ def one_gpu_step(cfg: str) -> float:
     return d["ms_per_step"] / 1e3
 
 
-OVERLAP = REPO / "profiles" / "r04" / "overlap" / "overlap.json"
+OVERLAP = (REPO / "profiles" / "r04" / "overlap" / "overlap.json",
+           REPO / "profiles" / "r04" / "overlap" / "overlap_rw.json")
 
 
-def contention(ingress_bs: float, path=OVERLAP):
+def contention(ingress_bs: float, paths=OVERLAP):
     """(c_r, c_g, the stand-in used) for a gather bringing `ingress_bs` into each GPU: from the
-    one-GPU overlap probe (tools/overlap_probe.py) at the library's default reduce grid, the
+    one-GPU overlap probes (tools/overlap_probe.py) at the library's default reduce grid, the
     smallest copy stand-in whose local HBM traffic (2 x its copy rate: read + write) is at least
     the gather's (2 x ingress: the received bytes written, the rank's own slice read once per
-    peer) — the next measured point above, or the largest."""
-    d = json.loads(Path(path).read_text())
-    row = next(r for r in d["rows"] if r["grid"] == "default")
-    pts = sorted(((v["copy_alone_gbs"] * 1e9, v["reduce_slowdown"] - 1.0, v["copy_slowdown"] - 1.0, k)
-                  for k, v in row["with"].items() if k != "dma"))
+    peer) — the next measured point above, or the largest.  Copy points of every probe file
+    (2-64 blocks: 19-552 GB/s)."""
+    pts = []
+    for path in paths:
+        if not Path(path).exists():
+            continue
+        d = json.loads(Path(path).read_text())
+        row = next(r for r in d["rows"] if r["grid"] == "default")
+        pts += [(v["copy_alone_gbs"] * 1e9, v["reduce_slowdown"] - 1.0, v["copy_slowdown"] - 1.0, k)
+                for k, v in row["with"].items() if k.isdigit()]
+    pts.sort()
     for rate, c_r, c_g, k in pts:
         if rate >= ingress_bs:
             return c_r, c_g, f"copy on {k} blocks ({rate / 1e9:.0f} GB/s)"
