@@ -1253,34 +1253,44 @@ __global__ __launch_bounds__(64 * W) void reduce_kernel_narrow(const float* __re
   finish_piece<T, OP, A, 1, 64 * W, 1>(e, qb, cols, accs);
 }
 
+// piece j of the group starting at slot g0: quads [qb, qb + bytes/16) of every row (interleaved
+// over the grid as in reduce_kernel_rows); the window's ragged last quad included (per-dword range
+// check: its missing elements load as 0 and are never stored); bytes 0: every access dropped
+__device__ __forceinline__ void rowmajor_piece_geom(int64_t g0, int j, int64_t k, int64_t pc, int64_t pieces,
+                                                    int64_t nquads, int64_t ncols, int64_t* qb, uint32_t* bytes) {
+  const int64_t pj = blockIdx.x + (g0 + j) * (int64_t)gridDim.x;
+  int64_t q = pj * pc * 64;
+  const int64_t qe = q + pc * 64 < nquads ? q + pc * 64 : nquads;
+  const int64_t ce = qe * 4 < ncols ? qe * 4 : ncols;
+  const int64_t left = ce - q * 4;
+  const uint32_t b = (pj < pieces && g0 + j < k && left > 0) ? (uint32_t)left * 4u : 0u;
+  *qb = b ? q : 0;
+  *bytes = b;
+}
+
 // One group of a row-major block: KG of the block's pieces (slots g0 .. g0+KG-1, interleaved
 // over the grid as in reduce_kernel_rows), all rows swept once, then the group epilogue.
-template <class P, typename T, int OP, int V, int D, int W, int KG, bool NT, int EPIB, bool TR, int XLM = -1>
+// PFG (cross-group prefetch): x arrives holding this group's first D steps (issued by the previous
+// group, or by the kernel for the first), and after this group's last row the first D steps of the
+// NEXT group (slot g0 + KG) are issued into x BEFORE this group's epilogue — so its result stores
+// are younger than those loads, and the next group's first wait (vmcnt counts loads and stores in
+// order) does not wait for them; without PFG every group end drained the stores before the next
+// group's first product (NS: the result stores cost ~2.3x their bytes, profiles/r04/nostore).
+template <class P, typename T, int OP, int V, int D, int W, int KG, bool NT, int EPIB, bool TR, int XLM = -1,
+          bool PFG = false>
 __device__ __forceinline__ void rowmajor_group(const char* __restrict__ base, int64_t row_bytes, int n,
                                                const typename P::w_t* __restrict__ w, int64_t g0, int64_t k,
                                                int64_t pc, int64_t pieces, int64_t nquads, int64_t ncols,
-                                               int gi, const Epi<T>& e) {
+                                               int gi, const Epi<T>& e,
+                                               typename vec4<float>::type (&x)[D][V]) {
   static_assert(KG % D == 0, "pipeline depth must divide the group size");
   typedef typename P::acc_t A;
-  typedef typename vec4<float>::type XV;
   typedef typename vec4<A>::type AV;
-  const int64_t g = gridDim.x;
   const int voff = (int)threadIdx.x * 16;
-  // piece j: columns [qb*4, qb*4 + cols), the window's ragged last quad included (per-dword
-  // range check: its missing elements load as 0 and are never stored)
   int64_t qb[KG];
   uint32_t bytes[KG];  // 4 x the piece's columns; 0: every access of this slot is dropped
 #pragma unroll
-  for (int j = 0; j < KG; ++j) {
-    const int64_t pj = blockIdx.x + (g0 + j) * g;  // interleaved pieces, as reduce_kernel_rows
-    qb[j] = pj * pc * 64;
-    const int64_t qe = qb[j] + pc * 64 < nquads ? qb[j] + pc * 64 : nquads;
-    const int64_t ce = qe * 4 < ncols ? qe * 4 : ncols;
-    const int64_t left = ce - qb[j] * 4;
-    bytes[j] = (pj < pieces && g0 + j < k && left > 0) ? (uint32_t)left * 4u : 0u;
-    if (bytes[j] == 0) qb[j] = 0;
-  }
-  XV x[D][V];
+  for (int j = 0; j < KG; ++j) rowmajor_piece_geom(g0, j, k, pc, pieces, nquads, ncols, &qb[j], &bytes[j]);
   AV acc[KG][V];
   // step s = (i, j), i = s / KG, j = s % KG; slot = j % D
 #define FA_RM_LOAD(slot, row, j)                                                                      \
@@ -1288,8 +1298,10 @@ __device__ __forceinline__ void rowmajor_group(const char* __restrict__ base, in
     const __amdgpu_buffer_rsrc_t r_ = row_rsrc(base + qb[j] * 16 + (int64_t)(row) * row_bytes, bytes[j]); \
     _Pragma("unroll") for (int v = 0; v < V; ++v) x[slot][v] = buf_load_quad<NT>(r_, voff + v * 64 * W * 16, 0); \
   }
+  if constexpr (!PFG) {
 #pragma unroll
-  for (int d = 0; d < D; ++d) FA_RM_LOAD(d, 0, d);
+    for (int d = 0; d < D; ++d) FA_RM_LOAD(d, 0, d);
+  }
   // row 0: products initialise the sums
 #pragma unroll
   for (int j = 0; j < KG; ++j) {
@@ -1330,6 +1342,19 @@ __device__ __forceinline__ void rowmajor_group(const char* __restrict__ base, in
     }
   }
 #undef FA_RM_LOAD
+  if constexpr (PFG) {  // the next group's first D steps, before this group's epilogue stores
+    if (g0 + KG < k) {
+#pragma unroll
+      for (int d = 0; d < D; ++d) {
+        int64_t qn;
+        uint32_t bn;
+        rowmajor_piece_geom(g0 + KG, d, k, pc, pieces, nquads, ncols, &qn, &bn);
+        const __amdgpu_buffer_rsrc_t r_ = row_rsrc(base + qn * 16, bn);
+#pragma unroll
+        for (int v = 0; v < V; ++v) x[d][v] = buf_load_quad<NT>(r_, voff + v * 64 * W * 16, 0);
+      }
+    }
+  }
   if constexpr (TR) {
     if (threadIdx.x == 0 && gi < 7) e.trace[blockIdx.x * 16 + 1 + 2 * gi] = wall_clock64();
   }
@@ -1392,7 +1417,7 @@ __device__ __forceinline__ void rowmajor_group(const char* __restrict__ base, in
 // TR (tools/tune_reduce.hip set "timeline"): wave 0 of every block stamps the 100-MHz wall clock
 // at its start and at each group's sweep end and epilogue end into e.trace[block * 16 + slot].
 template <class P, typename T, int OP, int V, int D, int W, int KG, bool NT, int EPIB = (V >= 2 ? 2 : V),
-          bool TR = false, int XLM = -1>
+          bool TR = false, int XLM = -1, bool PFG = false>
 __global__ __launch_bounds__(64 * W) void reduce_kernel_rowmajor(const float* __restrict__ stack,
                                                                  int64_t stride, int n,
                                                                  const typename P::w_t* __restrict__ w,
@@ -1409,8 +1434,22 @@ __global__ __launch_bounds__(64 * W) void reduce_kernel_rowmajor(const float* __
   if constexpr (TR) {
     if (threadIdx.x == 0) e.trace[blockIdx.x * 16] = wall_clock64();
   }
+  typename vec4<float>::type x[D][V];
+  if constexpr (PFG) {  // the first group's first D steps (later groups get theirs from the previous one)
+    const int voff = (int)threadIdx.x * 16;
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      int64_t q0;
+      uint32_t b0;
+      rowmajor_piece_geom(0, d, k, pc, pieces, nquads, ncols, &q0, &b0);
+      const __amdgpu_buffer_rsrc_t r_ = row_rsrc(base + q0 * 16, b0);
+#pragma unroll
+      for (int v = 0; v < V; ++v) x[d][v] = buf_load_quad<NT>(r_, voff + v * 64 * W * 16, 0);
+    }
+  }
 #define FA_RM_GROUP(KGX, G0, GI) \
-  rowmajor_group<P, T, OP, V, D, W, KGX, NT, EPIB, TR, XLM>(base, row_bytes, n, w, G0, k, pc, pieces, nquads, ncols, GI, e)
+  rowmajor_group<P, T, OP, V, D, W, KGX, NT, EPIB, TR, XLM, PFG>(base, row_bytes, n, w, G0, k, pc, pieces, nquads, ncols, \
+                                                                 GI, e, x)
   int gi = 0;
   for (int64_t g0 = 0; g0 < k; g0 += KG) FA_RM_GROUP(KG, g0, gi++);
 #undef FA_RM_GROUP

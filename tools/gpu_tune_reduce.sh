@@ -19,6 +19,8 @@ case $SET in
   stagger) SHAPES="100:11699136:mean 200:11699136:mean 1000:11699136:mean 100:25610176:avgm" ;;
   deep3) SHAPES="1000:177704:mean 800:365632:mean 400:731200:mean 100:1462400:mean 200:5849600:mean 1000:177704:avgm" ;;
   xlg) SHAPES="100:86567680:adagrad 100:86567680:avgm" ;;
+  pfg) SHAPES="100:25610176:mean 100:25610176:avgm 100:86567680:adagrad 100:11699136:mean 1000:11699136:mean 100:86567680:mean" ;;
+  nostore) SHAPES="100:25610176:mean 100:25610176:mean" ;;
   xl4) SHAPES="100:86567680:adagrad 100:86567680:avgm" ;;
   xl) SHAPES="100:25610176:avgm 100:25610176:adagrad 100:86567680:adagrad 100:11699136:avgm 300:25610176:avgm" ;;
   nlb) SHAPES="1000:44426:mean 2000:44426:mean 400:44426:mean 100:44426:mean 1000:44426:avgm 300:70001:mean 1000:177704:mean" ;;

@@ -424,9 +424,10 @@ __global__ __launch_bounds__(64 * W) void reduce_kernel_rowmajor_tail(const floa
     const int64_t pc = (chunks_s + g * k - 1) / (g * k);
     const int64_t pieces = (chunks_s + pc - 1) / pc;
     int gi = 0;
+    typename vec4<float>::type x[D][V];
     for (int64_t g0 = 0; g0 < k; g0 += KG)
       rowmajor_group<P, T, OP, V, D, W, KG, NT, EPIB, false>(base, row_bytes, n, w, g0, k, pc, pieces, nquads_s,
-                                                            ncols_static, gi++, e);
+                                                            ncols_static, gi++, e, x);
   }
   // the tail: strips of 64*W quads from quad ncols_static/4 (ncols_static is a multiple of 4)
   const int64_t nquads = (ncols + 3) / 4;
@@ -682,6 +683,22 @@ Variant make_rowmajor_xl(const float* stack, int64_t stride, int n, const float*
   return {name, bytes,
           [=] {
             hipLaunchKernelGGL((reduce_kernel_rowmajor<AccF32, T, OP, V, D, W, KG, true, EPIB, false, XLM>),
+                               dim3((unsigned)grid), dim3(64 * W), 0, 0, stack, stride, n, w, (int64_t)0, ncols, e);
+          },
+          true, {}};
+}
+
+template <int V, int D, int W, int KG, int OP, typename T, int EPIB, int XLM, bool PFG>
+Variant make_rowmajor_pfg(const float* stack, int64_t stride, int n, const float* w, int64_t ncols, Epi<T> e,
+                          double bytes, int64_t grid) {
+  const int64_t chunks = ((ncols + 3) / 4 + 63) / 64;
+  if (grid > chunks) grid = chunks;
+  char name[112];
+  snprintf(name, sizeof name, "rowmajor V%d W%d KG%d g%lld epib%d xl%d pfg%d", V, W, KG, (long long)grid, EPIB, XLM,
+           (int)PFG);
+  return {name, bytes,
+          [=] {
+            hipLaunchKernelGGL((reduce_kernel_rowmajor<AccF32, T, OP, V, D, W, KG, true, EPIB, false, XLM, PFG>),
                                dim3((unsigned)grid), dim3(64 * W), 0, 0, stack, stride, n, w, (int64_t)0, ncols, e);
           },
           true, {}};
@@ -1051,6 +1068,35 @@ int main(int argc, char** argv) {
       RMXL(4, 4, 1);
       RMXL(4, 4, 0);
       RMXL(4, 4, 1);
+    }
+  }
+  if (!strcmp(set, "pfg")) {  // cross-group prefetch (the next group's first step before the epilogue stores)
+    const int64_t chunks = ((ncols + 3) / 4 + 63) / 64;
+    const int64_t k = (chunks + 192 * 64 - 1) / (192 * 64);
+    const int kg = k % 3 == 0 ? 3 : 4;
+    printf("# k %lld KG %d\n", (long long)k, kg);
+#define PFGV(KG, EB, PF)                                                                                           \
+  vs.push_back(op == FA_OP_AVGM      ? make_rowmajor_pfg<16, 1, 4, KG, FA_OP_AVGM, double, EB, -1, PF>(stack, stride, n, w, ncols, e, bytes, 192) \
+               : op == FA_OP_ADAGRAD ? make_rowmajor_pfg<16, 1, 4, KG, FA_OP_ADAGRAD, double, EB, -1, PF>(stack, stride, n, w, ncols, e, bytes, 192) \
+                                     : make_rowmajor_pfg<16, 1, 4, KG, FA_OP_MEAN, double, EB, -1, PF>(stack, stride, n, w, ncols, e, bytes, 192))
+    for (int rep = 0; rep < 2; ++rep) {
+      if (kg == 3) {
+        if (op == FA_OP_MEAN) { PFGV(3, 2, false); PFGV(3, 2, true); } else { PFGV(3, 4, false); PFGV(3, 4, true); }
+      } else {
+        if (op == FA_OP_MEAN) { PFGV(4, 2, false); PFGV(4, 2, true); } else { PFGV(4, 4, false); PFGV(4, 4, true); }
+      }
+    }
+#undef PFGV
+  }
+  if (!strcmp(set, "nostore")) {  // NS product geometry (KG 3) with and without its fp32 result stores
+    for (int rep = 0; rep < 3; ++rep) {
+      RMXL(3, 2, -1);
+      Epi<double> e2 = e;
+      e2.out32 = nullptr;  // every result store dropped by the descriptor's empty range
+      Variant v = make_rowmajor_xl<16, 1, 4, 3, FA_OP_MEAN, double, 2, -1>(stack, stride, n, w, ncols, e2, bytes, 192);
+      v.name += " NOSTORE";
+      v.checks_output = false;
+      vs.push_back(v);
     }
   }
   if (!strcmp(set, "xl4")) {  // KG = 4 (C5): whole-line f64 stores at epilogue batch 1 / 2 (no scratch) vs the product
