@@ -37,7 +37,7 @@ def build_pyhost(force: bool = False, verbose: bool = False) -> Path:
         return PYHOST_OUT
     PYHOST_OUT.parent.mkdir(parents=True, exist_ok=True)
     tmp = PYHOST_OUT.with_suffix(".so.tmp")
-    cmd = [os.environ.get("CC", "gcc"), "-O2", "-fPIC", "-shared", "-Wall", "-Werror",
+    cmd = [os.environ.get("CC", "gcc"), "-O2", "-fPIC", "-shared", "-pthread", "-Wall", "-Werror",
            f"-I{sysconfig.get_paths()['include']}", f"-I{numpy.get_include()}", str(PYHOST_SOURCE), "-o", str(tmp)]
     if verbose:
         print(" ".join(cmd))

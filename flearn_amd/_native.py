@@ -111,6 +111,16 @@ def load_pyhost():
             L.fa_py_pack_rows.restype = ctypes.c_int
             L.fa_py_same_signature.argtypes = [O, O]
             L.fa_py_same_signature.restype = ctypes.c_int
+            L.fa_py_pack_start.argtypes = [O, O, I64, P, I64, I64, ctypes.c_int32, ctypes.POINTER(ctypes.c_int32)]
+            L.fa_py_pack_start.restype = P
+            L.fa_py_pack_end.argtypes = [P]
+            L.fa_py_pack_end.restype = ctypes.c_int
+            # fa_pack_wait blocks on native copies: the same library through CDLL, so the call
+            # releases the GIL while it waits
+            W = ctypes.CDLL(str(PYHOST_PATH))
+            W.fa_pack_wait.argtypes = [P, I64]
+            W.fa_pack_wait.restype = ctypes.c_int
+            L.fa_pack_wait = W.fa_pack_wait
             _pyhost = L
     return _pyhost
 

@@ -231,3 +231,222 @@ int fa_py_same_signature(PyObject *clients, PyObject *keys) {
   }
   return result;
 }
+
+// ---- asynchronous pack (the client-side update's chunked pipeline, strategy/_update.py) -------
+// fa_py_pack_start resolves every piece's source under the GIL (all-or-nothing: one value that is
+// not a C-contiguous array of the planned format and size and nothing is queued), splits the
+// copies into jobs of at most split_bytes in chunk order and hands them to a persistent pool of
+// native threads; fa_pack_wait(h, c) — called through ctypes.CDLL, so without the GIL — returns
+// once chunk c's copies are done, copying jobs of chunks <= c itself while it waits;
+// fa_py_pack_end waits for every copy and releases the values.  Python-side pool tasks (one GIL
+// hand-off per 4 MiB part, ~16 threads contending for it) kept the first chunk ~0.5-0.9 ms from
+// its launch; this path has no per-job interpreter work.
+#include <pthread.h>
+#include <stdatomic.h>
+#include <unistd.h>
+
+typedef struct {
+  char *dst;
+  const char *src;
+  int64_t n;
+  int64_t chunk;
+} PackJob;
+
+typedef struct Pack {
+  PackJob *jobs;
+  int64_t njobs;
+  atomic_llong next;  // next unclaimed job
+  atomic_llong *left; // per chunk: jobs not yet copied
+  int64_t nchunks;
+  Val *vals;
+  int64_t nvals;
+  pthread_mutex_t mu;  // chunk completion
+  pthread_cond_t cv;
+  int refs;            // workers inside this pack (g_mu)
+  int queued;          // still on the pool's queue (g_mu)
+  struct Pack *qnext;
+} Pack;
+
+static pthread_mutex_t g_mu = PTHREAD_MUTEX_INITIALIZER;
+static pthread_cond_t g_work = PTHREAD_COND_INITIALIZER;  // a pack was queued
+static pthread_cond_t g_idle = PTHREAD_COND_INITIALIZER;  // a worker left a pack
+static Pack *g_head = NULL, *g_tail = NULL;
+static int g_workers = 0;
+static pid_t g_pid = 0;
+
+static void pack_done_job(Pack *p, int64_t chunk) {
+  if (atomic_fetch_sub(&p->left[chunk], 1) == 1) {
+    pthread_mutex_lock(&p->mu);
+    pthread_cond_broadcast(&p->cv);
+    pthread_mutex_unlock(&p->mu);
+  }
+}
+
+static void unqueue_locked(Pack *p) {  // g_mu held
+  if (!p->queued) return;
+  Pack **pp = &g_head, *prev = NULL;
+  while (*pp && *pp != p) { prev = *pp; pp = &(*pp)->qnext; }
+  if (*pp) {
+    *pp = p->qnext;
+    if (g_tail == p) g_tail = prev;
+  }
+  p->queued = 0;
+}
+
+static void *pack_worker(void *arg) {
+  (void)arg;
+  for (;;) {
+    pthread_mutex_lock(&g_mu);
+    while (!g_head) pthread_cond_wait(&g_work, &g_mu);
+    Pack *p = g_head;
+    p->refs++;
+    pthread_mutex_unlock(&g_mu);
+    for (;;) {
+      const int64_t i = atomic_fetch_add(&p->next, 1);
+      if (i >= p->njobs) break;
+      memcpy(p->jobs[i].dst, p->jobs[i].src, (size_t)p->jobs[i].n);
+      pack_done_job(p, p->jobs[i].chunk);
+    }
+    pthread_mutex_lock(&g_mu);
+    unqueue_locked(p);  // every job is claimed: nothing left for the other workers
+    p->refs--;
+    pthread_cond_broadcast(&g_idle);
+    pthread_mutex_unlock(&g_mu);
+  }
+  return NULL;
+}
+
+// GIL held.  dicts: a tuple or list of dicts.  keys: tuple, one per piece.  desc: int64 table,
+// 5 rows of npieces:
+//   src[p]    index into dicts of the dict holding the piece's value (the whole value is copied)
+//   total[p]  the value's size in bytes
+//   fmt[p]    format class ('f', 'd' or 'i')
+//   dst[p]    destination address
+//   chunk[p]  chunk index, non-decreasing in p, < nchunks
+// Returns a handle, or NULL with *status FA_PY_FALLBACK (a value off the plan; nothing queued,
+// no exception set) or FA_PY_NOMEM.
+void *fa_py_pack_start(PyObject *dicts, PyObject *keys, int64_t npieces, const int64_t *desc,
+                       int64_t nchunks, int64_t split_bytes, int32_t threads, int32_t *status) {
+  const int64_t *src = desc, *total = desc + npieces, *fmt = desc + 2 * npieces, *dst = desc + 3 * npieces,
+                *chunk = desc + 4 * npieces;
+  *status = FA_PY_FALLBACK;
+  if (!PySequence_Check(dicts) || !PyTuple_Check(keys) || PyTuple_GET_SIZE(keys) != npieces || nchunks < 1 ||
+      split_bytes < 4096)
+    return NULL;
+  PyObject *seq = PySequence_Fast(dicts, "dicts");
+  if (!seq) { PyErr_Clear(); return NULL; }
+  const Py_ssize_t nd = PySequence_Fast_GET_SIZE(seq);
+  Pack *p = (Pack *)calloc(1, sizeof(Pack));
+  Val *vals = (Val *)calloc((size_t)(npieces > 0 ? npieces : 1), sizeof(Val));
+  atomic_llong *left = (atomic_llong *)calloc((size_t)nchunks, sizeof(atomic_llong));
+  int64_t held = 0, njobs = 0;
+  int rc = (p && vals && left) ? FA_PY_OK : FA_PY_NOMEM;
+  for (int64_t i = 0; i < npieces && rc == FA_PY_OK; i++) {
+    if (src[i] < 0 || src[i] >= nd || chunk[i] < 0 || chunk[i] >= nchunks || (i && chunk[i] < chunk[i - 1])) {
+      rc = FA_PY_FALLBACK;
+      break;
+    }
+    PyObject *d = PySequence_Fast_GET_ITEM(seq, src[i]);
+    if (!PyDict_Check(d)) { rc = FA_PY_FALLBACK; break; }
+    PyObject *v = PyDict_GetItemWithError(d, PyTuple_GET_ITEM(keys, i));  // borrowed
+    if (!v) { PyErr_Clear(); rc = FA_PY_FALLBACK; break; }
+    if (val_get(v, &vals[held]) != 0) { rc = FA_PY_FALLBACK; break; }
+    held++;
+    if (vals[i].len != total[i] || vals[i].fmt != fmt[i]) { rc = FA_PY_FALLBACK; break; }
+    njobs += (total[i] + split_bytes - 1) / split_bytes;
+  }
+  Py_DECREF(seq);
+  PackJob *jobs = NULL;
+  if (rc == FA_PY_OK) {
+    jobs = (PackJob *)malloc((size_t)(njobs > 0 ? njobs : 1) * sizeof(PackJob));
+    if (!jobs) rc = FA_PY_NOMEM;
+  }
+  if (rc != FA_PY_OK) {
+    for (int64_t i = 0; i < held; i++) val_release(&vals[i]);
+    free(vals);
+    free(left);
+    free(p);
+    *status = rc;
+    return NULL;
+  }
+  int64_t j = 0;
+  for (int64_t i = 0; i < npieces; i++)
+    for (int64_t o = 0; o < total[i]; o += split_bytes) {
+      const int64_t n = total[i] - o < split_bytes ? total[i] - o : split_bytes;
+      jobs[j++] = (PackJob){(char *)(intptr_t)dst[i] + o, vals[i].buf + o, n, chunk[i]};
+      atomic_fetch_add(&left[chunk[i]], 1);
+    }
+  p->jobs = jobs;
+  p->njobs = njobs;
+  atomic_init(&p->next, 0);
+  p->left = left;
+  p->nchunks = nchunks;
+  p->vals = vals;
+  p->nvals = held;
+  pthread_mutex_init(&p->mu, NULL);
+  pthread_cond_init(&p->cv, NULL);
+  *status = FA_PY_OK;
+  if (njobs == 0) return p;
+  const int want = threads < 1 ? 1 : threads > 64 ? 64 : threads;
+  pthread_mutex_lock(&g_mu);
+  if (g_pid != getpid()) {  // first use, or a forked child (its parent's workers do not exist here)
+    g_pid = getpid();
+    g_workers = 0;
+    g_head = g_tail = NULL;
+  }
+  while (g_workers < want) {
+    pthread_t t;
+    pthread_attr_t at;
+    pthread_attr_init(&at);
+    pthread_attr_setdetachstate(&at, PTHREAD_CREATE_DETACHED);
+    const int ok = pthread_create(&t, &at, pack_worker, NULL) == 0;
+    pthread_attr_destroy(&at);
+    if (!ok) break;  // fewer workers: the waiting caller copies the rest itself
+    g_workers++;
+  }
+  p->queued = 1;
+  if (g_tail) g_tail->qnext = p; else g_head = p;
+  g_tail = p;
+  pthread_cond_broadcast(&g_work);
+  pthread_mutex_unlock(&g_mu);
+  return p;
+}
+
+// No GIL needed (call through ctypes.CDLL).  0 once chunk c's copies are done; -1 bad arguments.
+int fa_pack_wait(void *h, int64_t c) {
+  Pack *p = (Pack *)h;
+  if (!p || c < 0 || c >= p->nchunks) return -1;
+  for (;;) {  // help: copy unclaimed jobs of chunks <= c
+    int64_t i = atomic_load(&p->next);
+    if (i >= p->njobs || p->jobs[i].chunk > c) break;
+    if (!atomic_compare_exchange_weak(&p->next, &i, i + 1)) continue;
+    memcpy(p->jobs[i].dst, p->jobs[i].src, (size_t)p->jobs[i].n);
+    pack_done_job(p, p->jobs[i].chunk);
+  }
+  pthread_mutex_lock(&p->mu);
+  while (atomic_load(&p->left[c]) > 0) pthread_cond_wait(&p->cv, &p->mu);
+  pthread_mutex_unlock(&p->mu);
+  return 0;
+}
+
+// GIL held.  Waits for every copy (and for the workers to leave the pack), releases the values,
+// frees the handle.  0, or -1 for a NULL handle.
+int fa_py_pack_end(void *h) {
+  Pack *p = (Pack *)h;
+  if (!p) return -1;
+  Py_BEGIN_ALLOW_THREADS
+  for (int64_t c = 0; c < p->nchunks; c++) fa_pack_wait(p, c);
+  pthread_mutex_lock(&g_mu);
+  unqueue_locked(p);
+  while (p->refs > 0) pthread_cond_wait(&g_idle, &g_mu);
+  pthread_mutex_unlock(&g_mu);
+  Py_END_ALLOW_THREADS
+  for (int64_t i = 0; i < p->nvals; i++) val_release(&p->vals[i]);
+  pthread_mutex_destroy(&p->mu);
+  pthread_cond_destroy(&p->cv);
+  free(p->vals);
+  free(p->left);
+  free(p->jobs);
+  free(p);
+  return 0;
+}

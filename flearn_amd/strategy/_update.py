@@ -20,6 +20,8 @@ from .. import _native as na
 from ..bucket import ALIGN
 
 _FMT = {np.dtype(np.float32): ord("f"), np.dtype(np.float64): ord("d")}
+_F32 = np.dtype(np.float32)
+_DEV_GLOB = (np.dtype(np.float64), _F32)  # w_glob dtypes the device path takes
 _PART_BYTES = 16 << 20  # host copies are split into parts of about this size, one per pool task
 _POOL = None
 
@@ -85,6 +87,54 @@ class _DictPack:
         return all(rc == 0 for rc in _run(self.tasks(d)))
 
 
+class _AsyncPack:
+    """A chunk plan's copies into the pinned staging as one native job list
+    (csrc/fa_pyhost.c fa_py_pack_start / fa_pack_wait / fa_py_pack_end): per key, w_local's
+    float32 value (when `lh_ptr` is given) and w_glob's value, in chunk order.  `start` returns
+    None when a value is off the plan (the caller then packs through the Python pool, which
+    copies such values the Python way); nothing was copied then."""
+
+    SPLIT = 512 << 10  # bytes per native copy job
+
+    def __init__(self, chunks, lh_ptr, gh_ptr, gdtype):
+        item = torch.empty((), dtype=gdtype).element_size()
+        gfmt = ord("d") if item == 8 else ord("f")
+        keys, rows = [], []
+        for j, (_f, _e, _pl, _pg, g) in enumerate(chunks):
+            for k, _s, o, n in g:
+                if lh_ptr is not None:
+                    keys.append(k)
+                    rows.append((0, n * 4, ord("f"), lh_ptr + o * 4, j))
+                keys.append(k)
+                rows.append((1, n * item, gfmt, gh_ptr + o * item, j))
+        self.keys = tuple(keys)
+        self.desc = np.ascontiguousarray(np.array(rows, dtype=np.int64).reshape(-1, 5).T).reshape(-1)
+        self.nchunks = len(chunks)
+        self.L = na.load_pyhost()
+        try:
+            cpus = len(os.sched_getaffinity(0))
+        except (AttributeError, OSError):
+            cpus = os.cpu_count() or 8
+        self.threads = max(4, min(16, cpus))
+
+    def start(self, local, glob):
+        st = ctypes.c_int32(0)
+        h = self.L.fa_py_pack_start((local if local is not None else {}, glob), self.keys, len(self.keys),
+                                    self.desc.ctypes.data, self.nchunks, self.SPLIT, self.threads, ctypes.byref(st))
+        if not h:
+            if st.value == 2:
+                raise MemoryError("fa_py_pack_start: out of host memory")
+            return None
+        return h
+
+    def wait(self, h, j):
+        if self.L.fa_pack_wait(h, j) != 0:
+            raise RuntimeError(f"fa_pack_wait({j}) failed")
+
+    def end(self, h):
+        self.L.fa_py_pack_end(h)
+
+
 class DeviceUpdater:
     #: zero-copy, chunked: the update kernel reads w_local / w_glob from the pinned staging and
     #: writes the result straight into a fresh pinned buffer over PCIe, one chunk of keys at a
@@ -101,6 +151,10 @@ class DeviceUpdater:
     chunk_bytes = 64 << 20  # w_glob bytes per zero-copy chunk (the middle ones; 32 MiB: +0.3-0.8 ms, round 4)
     first_chunk_bytes = 4 << 20  # the first chunks grow from this (x2 each) so the GPU starts early
     last_chunk_bytes = 8 << 20  # ... and the last ones shrink towards this: a short exposed tail
+    #: the zero-copy chunks are packed by native threads (fa_py_pack_start: 512 KiB jobs, no
+    #: interpreter work per job, the waiting thread copies too); False: Python pool tasks of
+    #: 4 MiB parts (the fallback for values the native pack refuses)
+    native_pack = True
     #: a list to receive per-call phase times (tools/bench_client_update.py --phases), or None
     trace = None
 
@@ -154,25 +208,36 @@ class DeviceUpdater:
     def _call(self, w_local, w_glob, **override):
         na.lib()
         glob, local, host_keys = {}, {}, []
+        gdt = None
+        nd, tt = np.ndarray, torch.Tensor
         for k, g in w_glob.items():
-            if isinstance(g, torch.Tensor):
-                g = g.detach().cpu().numpy()
             lv = w_local[k]
-            if isinstance(lv, torch.Tensor):
-                lv = lv.detach().cpu().numpy()
-            # the device handles fp32 parameters against a float64 / float32 global model; anything
-            # else (BN num_batches_tracked: int64 local, numpy-scalar global) takes the reference's
-            # numpy ops on the host, key by key, as avgm.py / opt.py compute them
-            if (isinstance(g, np.ndarray) and g.ndim >= 1 and g.dtype in (np.float64, np.float32)
-                    and isinstance(lv, np.ndarray) and lv.dtype == np.float32 and lv.shape == g.shape):
+            # exact-type tests first: this loop runs over every key of every call (~0.2 ms for
+            # ResNet-50's 320 keys with isinstance chains, part of what the call costs)
+            if type(g) is not nd:
+                if isinstance(g, tt):
+                    g = g.detach().cpu().numpy()
+                elif not isinstance(g, nd):
+                    host_keys.append(k)
+                    continue
+            if type(lv) is not nd:
+                if isinstance(lv, tt):
+                    lv = lv.detach().cpu().numpy()
+                elif not isinstance(lv, nd):
+                    host_keys.append(k)
+                    continue
+            # the device handles fp32 parameters against a float64 / float32 global model, one
+            # precision per call (the first key's); anything else (BN num_batches_tracked: int64
+            # local, numpy-scalar global) takes the reference's numpy ops on the host, key by key,
+            # as avgm.py / opt.py compute them
+            dt = g.dtype
+            if (g.ndim >= 1 and lv.dtype == _F32 and lv.shape == g.shape and dt in _DEV_GLOB
+                    and (gdt is None or dt == gdt)):
+                gdt = dt
                 glob[k], local[k] = g, lv
             else:
                 host_keys.append(k)
         if glob:
-            gdt = next(iter(glob.values())).dtype
-            for k in [k for k, g in glob.items() if g.dtype != gdt]:  # one device precision per call
-                host_keys.append(k)
-                del glob[k], local[k]
             self._device_step(w_local, glob, local, gdt, **override)
         if host_keys:
             self._host_step(w_local, w_glob, host_keys, **override)
@@ -325,7 +390,16 @@ class DeviceUpdater:
             out.append((first, end, _DictPack(g, np.float32, lh.data_ptr(), 4 << 20),
                         _DictPack(g, gdt, gh.data_ptr(), 4 << 20), g))
         self._chunk_plan = (self._stage, out)
+        self._apacks = {}
         return out
+
+    def _apack(self, chunks, with_local: bool):
+        """The chunk plan's native async pack (w_glob only, or w_local and w_glob), cached with it."""
+        ap = self._apacks.get(with_local)
+        if ap is None:
+            ap = self._apacks[with_local] = _AsyncPack(chunks, self._stage[0].data_ptr() if with_local else None,
+                                                       self._stage[1].data_ptr(), self._stage[1].dtype)
+        return ap
 
     def _device_step_zc(self, w_local, glob, local, lay, total, tdt, dev, **override):
         """All or nothing: v_t advances into the second buffer, which becomes v_t only after
@@ -357,24 +431,32 @@ class DeviceUpdater:
         tr = [] if self.trace is not None else None
         t0 = time.perf_counter()
         chunks = self._chunks(lay, total, tdt)
-        # every chunk's pack parts go to the pool at once, in chunk order (the pool runs them
-        # FIFO): the threads stay busy whatever the chunk sizes, and each chunk's kernel is
-        # launched as soon as its own parts are in
-        pool = _pool()
-        futs = [([pool.submit(t) for t in pack_l.tasks(local)], [pool.submit(t) for t in pack_g.tasks(glob)])
-                for _first, _end, pack_l, pack_g, _g in chunks]
+        # every chunk's copies are queued at once, in chunk order: native threads (or, for values
+        # the native pack refuses, the Python pool) stay busy whatever the chunk sizes, and each
+        # chunk's kernel is launched as soon as its own copies are in
+        ap = self._apack(chunks, True) if self.native_pack else None
+        h = ap.start(local, glob) if ap is not None else None
+        futs = None
+        if h is None:
+            pool = _pool()
+            futs = [([pool.submit(t) for t in pack_l.tasks(local)], [pool.submit(t) for t in pack_g.tasks(glob)])
+                    for _first, _end, pack_l, pack_g, _g in chunks]
         with torch.cuda.device(dev):
             stream = torch.cuda.current_stream(dev)
             sh = stream.cuda_stream
             try:
-                for (first, end, pack_l, pack_g, g), (fl, fg) in zip(chunks, futs):
+                for j, (first, end, pack_l, pack_g, g) in enumerate(chunks):
                     tp = time.perf_counter()
-                    if any(f.result() for f in fl):  # a value the native pack refuses: copy in Python
-                        for k, s, o, n in g:
-                            lh.numpy()[o : o + n] = local[k].reshape(-1)
-                    if any(f.result() for f in fg):
-                        for k, s, o, n in g:
-                            gh.numpy()[o : o + n] = glob[k].reshape(-1)
+                    if h is not None:
+                        ap.wait(h, j)
+                    else:
+                        fl, fg = futs[j]
+                        if any(f.result() for f in fl):  # a value the native pack refuses: copy in Python
+                            for k, s, o, n in g:
+                                lh.numpy()[o : o + n] = local[k].reshape(-1)
+                        if any(f.result() for f in fg):
+                            for k, s, o, n in g:
+                                gh.numpy()[o : o + n] = glob[k].reshape(-1)
                     n = end - first
                     if dma:  # copy engine in (own stream), the update on the device, copy engine out
                         with torch.cuda.stream(s_in):
@@ -397,16 +479,24 @@ class DeviceUpdater:
                     if tr is not None:
                         tr.append((end - first, tp - t0, time.perf_counter() - t0))
             except BaseException:
-                for fl, fg in futs:  # no pack may still write the staging ...
-                    for f in fl + fg:
-                        f.cancel()
-                concurrent.futures.wait([f for fl, fg in futs for f in fl + fg])
+                if h is not None:  # no pack may still write the staging ...
+                    ap.end(h)
+                else:
+                    for fl, fg in futs:
+                        for f in fl + fg:
+                            f.cancel()
+                    concurrent.futures.wait([f for fl, fg in futs for f in fl + fg])
                 stream.synchronize()  # ... nor a queued chunk read it or write `res`
                 if dma:
                     s_in.synchronize()
                     s_out.synchronize()
                 raise
             ts = time.perf_counter()
+            if h is not None:
+                ap.end(h)  # every copy is done: releases the values
+            # the new values' views are made while the GPU finishes (they read nothing yet)
+            fresh = res.numpy()
+            views = [(k, fresh[o : o + n].reshape(s)) for k, s, o, n in lay]
             stream.synchronize()
             if dma:
                 s_out.synchronize()
@@ -414,9 +504,7 @@ class DeviceUpdater:
         if tr is not None:
             self.trace.append({"chunks": tr, "launched_s": ts - t0, "done_s": time.perf_counter() - t0,
                                "alloc_s": t0 - t_alloc})
-        fresh = res.numpy()
-        for k, s, o, n in lay:  # replaced per key, like the reference (avgm.py:34-35, opt.py:62-63)
-            w_local[k] = fresh[o : o + n].reshape(s)
+        w_local.update(views)  # replaced per key, like the reference (avgm.py:34-35, opt.py:62-63)
 
     # ---- the model already on the GPU (client_receive with a CUDA model) ---------------------
     @staticmethod
@@ -494,8 +582,12 @@ class DeviceUpdater:
         prec = na.PREC_F64 if tdt == torch.float64 else na.PREC_F32
         p = dict(self.params, **override)
         chunks = self._chunks(lay, total, tdt)
-        pool = _pool()
-        futs = [[pool.submit(t) for t in pack_g.tasks(glob)] for _f, _e, _pl, pack_g, _g in chunks]
+        ap = self._apack(chunks, False) if self.native_pack else None
+        h = ap.start(None, glob) if ap is not None else None
+        futs = None
+        if h is None:
+            pool = _pool()
+            futs = [[pool.submit(t) for t in pack_g.tasks(glob)] for _f, _e, _pl, pack_g, _g in chunks]
         with torch.cuda.device(dev):
             stream = torch.cuda.current_stream(dev)
             sh = stream.cuda_stream
@@ -505,8 +597,10 @@ class DeviceUpdater:
                 ptr_d.copy_(ptr_h, non_blocking=True)
                 na.check(L.fa_gather_rows(dl.data_ptr(), total, 1, 4, ptr_d.data_ptr(), segs.data_ptr(), len(lay), sh),
                          "fa_gather_rows")
-                for (first, end, _pl, _pg, g), fg in zip(chunks, futs):
-                    if any(f.result() for f in fg):  # a value the native pack refuses: copy in Python
+                for j, (first, end, _pl, _pg, g) in enumerate(chunks):
+                    if h is not None:
+                        ap.wait(h, j)
+                    elif any(f.result() for f in futs[j]):  # a value the native pack refuses: copy in Python
                         for k, _s, o, n in g:
                             gh.numpy()[o : o + n] = glob[k].reshape(-1)
                     dg[first:end].copy_(gh[first:end], non_blocking=True)
@@ -517,12 +611,17 @@ class DeviceUpdater:
                                             end - first, None if prec == na.PREC_F64 else out,
                                             out if prec == na.PREC_F64 else None, sh), "fa_opt_apply")
             except BaseException:
-                for fg in futs:
-                    for f in fg:
-                        f.cancel()
-                concurrent.futures.wait([f for fg in futs for f in fg])
+                if h is not None:
+                    ap.end(h)
+                else:
+                    for fg in futs:
+                        for f in fg:
+                            f.cancel()
+                    concurrent.futures.wait([f for fg in futs for f in fg])
                 stream.synchronize()
                 raise
+            if h is not None:
+                ap.end(h)
             done = torch.cuda.Event()
             done.record(stream)
         self._h2d_done = done

@@ -50,6 +50,7 @@ def main():
     ap.add_argument("--chunk-mb", type=float, default=None, help="DeviceUpdater.chunk_bytes in MiB")
     ap.add_argument("--first-mb", type=float, default=None, help="DeviceUpdater.first_chunk_bytes in MiB")
     ap.add_argument("--last-mb", type=float, default=None, help="DeviceUpdater.last_chunk_bytes in MiB")
+    ap.add_argument("--native-pack", type=int, default=None, help="DeviceUpdater.native_pack (0: Python pool)")
     ap.add_argument("--phases", action="store_true", help="record the zero-copy pipeline's per-chunk times")
     ap.add_argument("--device-model", action="store_true",
                     help="client_receive with the model on the GPU: device path vs the reference's host path")
@@ -65,6 +66,8 @@ def main():
         DeviceUpdater.trace = []
     if a.transfer is not None:
         DeviceUpdater.transfer = a.transfer
+    if a.native_pack is not None:
+        DeviceUpdater.native_pack = bool(a.native_pack)
 
     if a.zero_copy is not None:
         DeviceUpdater.zero_copy = bool(a.zero_copy)
@@ -100,10 +103,18 @@ def main():
         med = float(np.median(ts[1:]))
         if a.phases and DeviceUpdater.trace:
             last = DeviceUpdater.trace[-1]
+            calls = DeviceUpdater.trace[1:] or DeviceUpdater.trace
+
+            def med_ms(f):
+                return round(float(np.median([f(t) for t in calls])) * 1e3, 3)
+
             res[f"{method}_phases"] = {
                 "launched_ms": round(last["launched_s"] * 1e3, 3), "done_ms": round(last["done_s"] * 1e3, 3),
                 "chunks": [[n, round(t0 * 1e3, 3), round(t1 * 1e3, 3)] for n, t0, t1 in last["chunks"]],
-                "note": "per chunk: [elements, pack start ms, launch queued ms]"}
+                "median": {"first_launch_ms": med_ms(lambda t: t["chunks"][0][2]),
+                           "launched_ms": med_ms(lambda t: t["launched_s"]), "done_ms": med_ms(lambda t: t["done_s"]),
+                           "call_ms": med_ms(lambda t: t.get("call_s", float("nan")))},
+                "note": "per chunk (last call): [elements, pack start ms, launch queued ms]; median over calls after the first"}
             DeviceUpdater.trace.clear()
         res[method] = {"flearn_amd_s": round(med, 4), "first_call_s": round(ts[0], 4),
                        "reference_s": round(float(np.median(rs[1:] if len(rs) > 1 else rs)), 4),
@@ -115,6 +126,7 @@ def main():
     res["chunk_bytes"] = DeviceUpdater.chunk_bytes
     res["first_chunk_bytes"] = DeviceUpdater.first_chunk_bytes
     res["last_chunk_bytes"] = DeviceUpdater.last_chunk_bytes
+    res["native_pack"] = DeviceUpdater.native_pack
     res["note"] = "host arrays in and out (PCIe-inclusive); reference = its numpy ops on 1 core; median after round 0"
     print(json.dumps(res))
 
