@@ -17,7 +17,7 @@ from pathlib import Path
 import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 
 LIB_PATH = Path(__file__).resolve().parent / "lib" / "libflearn_amd.so"
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 FA_OK = 0
 FA_ERR_ARG, FA_ERR_ALIGN, FA_ERR_LAUNCH = -1, -2, -3
@@ -42,6 +42,7 @@ EXPORTS = (
     "fa_gather_rows",
     "fa_gather_rows_f64",
     "fa_fill_uniform_f32",
+    "fa_copy",
     "fa_set_reduce_grid",
     "fa_b64_decoded_size",
     "fa_b64_decode",
@@ -188,6 +189,7 @@ def load(require_gpu: bool = False):
                 "fa_gather_rows": ([P, I64, I32, I32, P, P, I32, P], ctypes.c_int),
                 "fa_gather_rows_f64": ([P, I64, I32, P, P, I32, P], ctypes.c_int),
                 "fa_fill_uniform_f32": ([P, I64, I32, I64, ctypes.c_uint64, I64, I64, P], ctypes.c_int),
+                "fa_copy": ([P, P, I64, P], ctypes.c_int),
                 "fa_set_reduce_grid": ([I32], ctypes.c_int),
                 "fa_b64_decoded_size": ([P, I64], I64),
                 "fa_b64_decode": ([P, I64, P, I64, I32], ctypes.c_int),

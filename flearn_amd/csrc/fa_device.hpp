@@ -1490,6 +1490,20 @@ __global__ __launch_bounds__(kThreads) void apply_kernel(const T* __restrict__ g
   finish_quad<T, OP, T>(e, c, valid, g);  // denom == 1: T(g)/1 == g exactly
 }
 
+// Plain copy (fa_copy): 16-B non-temporal loads and stores, grid-stride; the last nbytes % 16
+// bytes by the first block's lanes.  Pointers 16-byte aligned (checked on the host).
+__global__ __launch_bounds__(kThreads) void copy_kernel(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src,
+                                                        int64_t nbytes) {
+  typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+  const int64_t quads = nbytes >> 4;
+  const u4* s = reinterpret_cast<const u4*>(src);
+  u4* d = reinterpret_cast<u4*>(dst);
+  for (int64_t q = (int64_t)blockIdx.x * kThreads + threadIdx.x; q < quads; q += (int64_t)gridDim.x * kThreads)
+    __builtin_nontemporal_store(__builtin_nontemporal_load(s + q), d + q);
+  const int64_t tail = nbytes - (quads << 4);
+  if (blockIdx.x == 0 && threadIdx.x < tail) dst[(quads << 4) + threadIdx.x] = src[(quads << 4) + threadIdx.x];
+}
+
 __device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
   z += 0x9E3779B97F4A7C15ull;
   z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;

@@ -263,6 +263,7 @@ typedef struct Pack {
   pthread_mutex_t mu;  // chunk completion
   pthread_cond_t cv;
   int refs;            // workers inside this pack (g_mu)
+  int max_workers;     // at most this many workers copy for this pack at once
   int queued;          // still on the pool's queue (g_mu)
   struct Pack *qnext;
 } Pack;
@@ -297,8 +298,13 @@ static void *pack_worker(void *arg) {
   (void)arg;
   for (;;) {
     pthread_mutex_lock(&g_mu);
-    while (!g_head) pthread_cond_wait(&g_work, &g_mu);
-    Pack *p = g_head;
+    Pack *p;
+    for (;;) {  // the oldest queued pack that still takes another worker
+      for (p = g_head; p && p->refs >= p->max_workers; p = p->qnext) {
+      }
+      if (p) break;
+      pthread_cond_wait(&g_work, &g_mu);
+    }
     p->refs++;
     pthread_mutex_unlock(&g_mu);
     for (;;) {
@@ -311,24 +317,28 @@ static void *pack_worker(void *arg) {
     unqueue_locked(p);  // every job is claimed: nothing left for the other workers
     p->refs--;
     pthread_cond_broadcast(&g_idle);
+    pthread_cond_broadcast(&g_work);  // a worker slot of some queued pack may have opened
     pthread_mutex_unlock(&g_mu);
   }
   return NULL;
 }
 
 // GIL held.  dicts: a tuple or list of dicts.  keys: tuple, one per piece.  desc: int64 table,
-// 5 rows of npieces:
-//   src[p]    index into dicts of the dict holding the piece's value (the whole value is copied)
+// 7 rows of npieces:
+//   src[p]    index into dicts of the dict holding the piece's value
 //   total[p]  the value's size in bytes
 //   fmt[p]    format class ('f', 'd' or 'i')
 //   dst[p]    destination address
 //   chunk[p]  chunk index, non-decreasing in p, < nchunks
-// Returns a handle, or NULL with *status FA_PY_FALLBACK (a value off the plan; nothing queued,
+//   lo[p]     first byte of the value copied
+//   nbytes[p] bytes copied (lo + nbytes <= total)
+// At most `threads` pool workers copy for this pack at once (the pool grows to the largest
+// `threads` asked for).  Returns a handle, or NULL with *status FA_PY_FALLBACK (a value off the plan; nothing queued,
 // no exception set) or FA_PY_NOMEM.
 void *fa_py_pack_start(PyObject *dicts, PyObject *keys, int64_t npieces, const int64_t *desc,
                        int64_t nchunks, int64_t split_bytes, int32_t threads, int32_t *status) {
   const int64_t *src = desc, *total = desc + npieces, *fmt = desc + 2 * npieces, *dst = desc + 3 * npieces,
-                *chunk = desc + 4 * npieces;
+                *chunk = desc + 4 * npieces, *lo = desc + 5 * npieces, *nbytes = desc + 6 * npieces;
   *status = FA_PY_FALLBACK;
   if (!PySequence_Check(dicts) || !PyTuple_Check(keys) || PyTuple_GET_SIZE(keys) != npieces || nchunks < 1 ||
       split_bytes < 4096)
@@ -352,8 +362,12 @@ void *fa_py_pack_start(PyObject *dicts, PyObject *keys, int64_t npieces, const i
     if (!v) { PyErr_Clear(); rc = FA_PY_FALLBACK; break; }
     if (val_get(v, &vals[held]) != 0) { rc = FA_PY_FALLBACK; break; }
     held++;
-    if (vals[i].len != total[i] || vals[i].fmt != fmt[i]) { rc = FA_PY_FALLBACK; break; }
-    njobs += (total[i] + split_bytes - 1) / split_bytes;
+    if (vals[i].len != total[i] || vals[i].fmt != fmt[i] || lo[i] < 0 || nbytes[i] < 0 ||
+        lo[i] + nbytes[i] > total[i]) {
+      rc = FA_PY_FALLBACK;
+      break;
+    }
+    njobs += (nbytes[i] + split_bytes - 1) / split_bytes;
   }
   Py_DECREF(seq);
   PackJob *jobs = NULL;
@@ -371,9 +385,9 @@ void *fa_py_pack_start(PyObject *dicts, PyObject *keys, int64_t npieces, const i
   }
   int64_t j = 0;
   for (int64_t i = 0; i < npieces; i++)
-    for (int64_t o = 0; o < total[i]; o += split_bytes) {
-      const int64_t n = total[i] - o < split_bytes ? total[i] - o : split_bytes;
-      jobs[j++] = (PackJob){(char *)(intptr_t)dst[i] + o, vals[i].buf + o, n, chunk[i]};
+    for (int64_t o = 0; o < nbytes[i]; o += split_bytes) {
+      const int64_t n = nbytes[i] - o < split_bytes ? nbytes[i] - o : split_bytes;
+      jobs[j++] = (PackJob){(char *)(intptr_t)dst[i] + o, vals[i].buf + lo[i] + o, n, chunk[i]};
       atomic_fetch_add(&left[chunk[i]], 1);
     }
   p->jobs = jobs;
@@ -388,6 +402,7 @@ void *fa_py_pack_start(PyObject *dicts, PyObject *keys, int64_t npieces, const i
   *status = FA_PY_OK;
   if (njobs == 0) return p;
   const int want = threads < 1 ? 1 : threads > 64 ? 64 : threads;
+  p->max_workers = want;
   pthread_mutex_lock(&g_mu);
   if (g_pid != getpid()) {  // first use, or a forked child (its parent's workers do not exist here)
     g_pid = getpid();

@@ -719,6 +719,21 @@ int fa_set_reduce_grid(int32_t grid) {
   return g_reduce_grid.exchange(grid);
 }
 
+int fa_copy(void* dst, const void* src, int64_t nbytes, void* stream) {
+  if ((!dst || !src) && nbytes > 0) return fail(FA_ERR_ARG, "null copy pointer");
+  if (nbytes < 0) return fail(FA_ERR_ARG, "negative copy size");
+  if (nbytes == 0) return FA_OK;
+  if (((uintptr_t)dst | (uintptr_t)src) & 15) return fail(FA_ERR_ALIGN, "copy pointers must be 16-byte aligned");
+  // 512 blocks of 256 lanes, grid-stride: enough 16-B stores in flight for PCIe (tools/probe_zc.cpp)
+  const int64_t quads = nbytes / 16;
+  int64_t blocks = (quads + kThreads - 1) / kThreads;
+  if (blocks > 512) blocks = 512;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(copy_kernel, dim3((unsigned)blocks), dim3(kThreads), 0, static_cast<hipStream_t>(stream),
+                     static_cast<uint8_t*>(dst), static_cast<const uint8_t*>(src), nbytes);
+  return launch_check();
+}
+
 int fa_fill_uniform_f32(float* dst, int64_t row_stride, int32_t n_rows, int64_t n_cols,
                         uint64_t seed, int64_t row_begin, int64_t col_global_begin, void* stream) {
   if (!dst || n_rows < 0 || n_cols < 0 || row_stride < n_cols) return fail(FA_ERR_ARG, "bad fill");

@@ -17,7 +17,7 @@ import numpy as np
 import torch
 
 from .. import _native as na
-from ..bucket import ALIGN
+from ..bucket import ALIGN, AsyncPack
 
 _FMT = {np.dtype(np.float32): ord("f"), np.dtype(np.float64): ord("d")}
 _F32 = np.dtype(np.float32)
@@ -87,14 +87,9 @@ class _DictPack:
         return all(rc == 0 for rc in _run(self.tasks(d)))
 
 
-class _AsyncPack:
-    """A chunk plan's copies into the pinned staging as one native job list
-    (csrc/fa_pyhost.c fa_py_pack_start / fa_pack_wait / fa_py_pack_end): per key, w_local's
-    float32 value (when `lh_ptr` is given) and w_glob's value, in chunk order.  `start` returns
-    None when a value is off the plan (the caller then packs through the Python pool, which
-    copies such values the Python way); nothing was copied then."""
-
-    SPLIT = 512 << 10  # bytes per native copy job
+class _AsyncPack(AsyncPack):
+    """The zero-copy chunk plan's copies into the pinned staging as one native job list: per
+    key, w_local's float32 value (when `lh_ptr` is given) and w_glob's value, in chunk order."""
 
     def __init__(self, chunks, lh_ptr, gh_ptr, gdtype):
         item = torch.empty((), dtype=gdtype).element_size()
@@ -104,35 +99,13 @@ class _AsyncPack:
             for k, _s, o, n in g:
                 if lh_ptr is not None:
                     keys.append(k)
-                    rows.append((0, n * 4, ord("f"), lh_ptr + o * 4, j))
+                    rows.append((0, n * 4, ord("f"), lh_ptr + o * 4, j, 0, n * 4))
                 keys.append(k)
-                rows.append((1, n * item, gfmt, gh_ptr + o * item, j))
-        self.keys = tuple(keys)
-        self.desc = np.ascontiguousarray(np.array(rows, dtype=np.int64).reshape(-1, 5).T).reshape(-1)
-        self.nchunks = len(chunks)
-        self.L = na.load_pyhost()
-        try:
-            cpus = len(os.sched_getaffinity(0))
-        except (AttributeError, OSError):
-            cpus = os.cpu_count() or 8
-        self.threads = max(4, min(16, cpus))
+                rows.append((1, n * item, gfmt, gh_ptr + o * item, j, 0, n * item))
+        super().__init__(tuple(keys), np.array(rows, dtype=np.int64).reshape(-1, 7), len(chunks))
 
     def start(self, local, glob):
-        st = ctypes.c_int32(0)
-        h = self.L.fa_py_pack_start((local if local is not None else {}, glob), self.keys, len(self.keys),
-                                    self.desc.ctypes.data, self.nchunks, self.SPLIT, self.threads, ctypes.byref(st))
-        if not h:
-            if st.value == 2:
-                raise MemoryError("fa_py_pack_start: out of host memory")
-            return None
-        return h
-
-    def wait(self, h, j):
-        if self.L.fa_pack_wait(h, j) != 0:
-            raise RuntimeError(f"fa_pack_wait({j}) failed")
-
-    def end(self, h):
-        self.L.fa_py_pack_end(h)
+        return super().start((local if local is not None else {}, glob))
 
 
 class DeviceUpdater:

@@ -140,6 +140,16 @@ def test_apply_and_fill_validation(L):
     assert L.fa_fill_uniform_f32(FAKE, 8, 1, 64, 1, 0, 0, None) == header_define("FA_ERR_ARG")
 
 
+def test_copy_validation(L):
+    """fa_copy: 16-byte aligned pointers only (the caller then takes the copy engine), no
+    negative sizes, and an empty copy touches nothing."""
+    assert L.fa_copy(FAKE + 8, FAKE, 64, None) == header_define("FA_ERR_ALIGN")
+    assert L.fa_copy(FAKE, FAKE + 4, 64, None) == header_define("FA_ERR_ALIGN")
+    assert L.fa_copy(FAKE, FAKE, -1, None) == header_define("FA_ERR_ARG")
+    assert L.fa_copy(None, FAKE, 64, None) == header_define("FA_ERR_ARG")
+    assert L.fa_copy(None, None, 0, None) == 0
+
+
 def test_piece_struct_layout_matches_c(tmp_path):
     src = tmp_path / "piece.c"
     src.write_text('#include <stddef.h>\n#include <stdio.h>\n#include "flearn_amd.h"\n'

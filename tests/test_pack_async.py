@@ -145,3 +145,22 @@ def test_bad_wait_index_raises():
     with pytest.raises(RuntimeError):
         ap.wait(h, len(chunks))
     ap.end(h)
+
+
+@pytest.mark.parametrize("threads", [1, 2])
+def test_worker_cap_still_copies_everything(threads):
+    from flearn_amd.bucket import AsyncPack
+
+    shapes = [(200_000,), (3,), (70_001,)] * 4
+    chunks, total = _plan(shapes, 3)
+    lh, gh = np.zeros(total, np.float32), np.zeros(total)
+    base = _AsyncPack(chunks, lh.ctypes.data, gh.ctypes.data, torch.float64)
+    ap = AsyncPack(base.keys, base.desc.reshape(7, -1).T.copy(), base.nchunks, threads=threads)
+    local, glob = _dicts(shapes, np.float64, 4)
+    h = ap.start((local, glob))
+    for j in range(ap.nchunks):
+        ap.wait(h, j)
+    ap.end(h)
+    for _f, _e, _pl, _pg, g in chunks:
+        for k, s, o, n in g:
+            assert np.array_equal(gh[o : o + n], glob[k].reshape(-1)) and np.array_equal(lh[o : o + n], local[k].reshape(-1))

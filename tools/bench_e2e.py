@@ -36,6 +36,13 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--output", default="reference")
     ap.add_argument("--devices", type=int, default=1, help="split columns over the first K GPUs")
+    ap.add_argument("--native-pack", type=int, default=None, help="Packer.native_async (0: the Python pool)")
+    ap.add_argument("--zero-copy-out", type=int, default=None, help="Packer.zero_copy_out (0: copy engine + host copy)")
+    ap.add_argument("--lookahead", type=int, default=None, help="Packer.async_lookahead (chunks packed ahead; 0: all)")
+    ap.add_argument("--pack-threads", type=int, default=None, help="Packer.async_threads")
+    ap.add_argument("--ab", default=None,
+                    help="alternate round by round between Packer settings, e.g. "
+                         "'native_async=0;native_async=1,async_lookahead=2': per-setting medians")
     a = ap.parse_args()
     name, n = CONFIGS[a.config]
     layout = layouts.get(name)
@@ -51,6 +58,14 @@ def main():
         raise SystemExit(f"--devices {a.devices} but only {torch.cuda.device_count()} GPU(s) visible")
     s = flearn_amd.AVG(output=a.output, devices=[torch.device("cuda", i) for i in range(a.devices)])
     eng = s.engine
+    if a.native_pack is not None:
+        eng.packer.native_async = bool(a.native_pack)
+    if a.zero_copy_out is not None:
+        eng.packer.zero_copy_out = bool(a.zero_copy_out)
+    if a.lookahead is not None:
+        eng.packer.async_lookahead = a.lookahead
+    if a.pack_threads is not None:
+        eng.packer.async_threads = a.pack_threads
     # phase timers around the engine's own steps
     t = {"plan_pack_h2d": [], "reduce": [], "d2h_unpack": [], "total": []}
     orig_pack, orig_finish = eng.packer.pack, eng._finish
@@ -76,6 +91,8 @@ def main():
         return out
 
     eng.packer.pack, eng._finish = pack, finish
+    if a.ab:
+        return ab(a, s, uploads, t, layout)
     for r in range(a.rounds + 1):
         t0 = time.perf_counter()
         w_glob = s.server(uploads, r)["w_glob"]
@@ -99,8 +116,43 @@ def main():
         "pack_h2d_GB_s": round(in_bytes / 1e9 / med["plan_pack_h2d"], 2),
         "reference_server_s": round(min(ref_s), 5),
         "speedup_vs_reference": round(min(ref_s) / med["total"], 2),
+        "pack_path": eng.packer.last_pack_paths.get("f32"), "native_pack": eng.packer.native_async,
+        "zero_copy_out": eng.packer.zero_copy_out, "lookahead": eng.packer.async_lookahead,
+        "pack_threads": eng.packer.async_threads,
         "note": "uploads are host numpy views (flearn loopback); first round (pinned-buffer allocation) excluded",
     }
+    print(json.dumps(res))
+
+
+def ab(a, s, uploads, t, layout):
+    """Interleaved A/B of Packer settings in one process: round r uses setting r % k; medians
+    per setting over the rounds after each setting's first."""
+    settings = []
+    for spec in a.ab.split(";"):
+        kv = {}
+        for item in filter(None, spec.split(",")):
+            k, v = item.split("=")
+            kv[k.strip()] = int(v)
+        settings.append(kv)
+    eng = s.engine
+    per = [{"plan_pack_h2d": [], "d2h_unpack": [], "total": [], "path": None} for _ in settings]
+    for r in range((a.rounds + 1) * len(settings)):
+        i = r % len(settings)
+        for k, v in settings[i].items():
+            setattr(eng.packer, k, type(getattr(eng.packer, k))(v))
+        n0 = len(t["plan_pack_h2d"])
+        t0 = time.perf_counter()
+        w_glob = s.server(uploads, r)["w_glob"]
+        per[i]["total"].append(time.perf_counter() - t0)
+        per[i]["plan_pack_h2d"].append(t["plan_pack_h2d"][n0])
+        per[i]["d2h_unpack"].append(t["d2h_unpack"][n0])
+        per[i]["path"] = eng.packer.last_pack_paths.get("f32")
+        assert len(w_glob) == len(layout)
+    res = {"config": a.config, "rounds_per_setting": a.rounds, "settings": []}
+    for kv, d in zip(settings, per):
+        res["settings"].append({"set": kv, "path": d["path"],
+                                **{k + "_ms": round(float(np.median(v[1:])) * 1e3, 2) for k, v in d.items() if k != "path"},
+                                "total_ms_all": [round(x * 1e3, 1) for x in d["total"]]})
     print(json.dumps(res))
 
 
