@@ -150,8 +150,9 @@ class Job:
     columns (plan) resident in HBM, the fused HIP reduce per stripe and (world > 1) the RCCL
     all-gather of every stripe."""
 
-    def __init__(self, cfg, layout, n, plan, dev, world, reorder):
+    def __init__(self, cfg, layout, n, plan, dev, world, reorder, push=False):
         self.cfg, self.n, self.plan, self.dev = cfg, n, plan, dev
+        self.push = push
         cols, stride = plan.local_cols, plan.local_stride
         log(f"[rank {plan.rank}] alloc {n} x {cols} fp32 = {n * cols * 4 / 1e9:.2f} GB, stripes {plan.widths}"
             + (f" + replicated tail {plan.rep}" if plan.rep else ""))
@@ -170,7 +171,7 @@ class Job:
             self.reset_state(state)
             epi = dict(op=na.OP_BY_NAME[cfg["op"]], state=state)
         self.fn = hip_reduce_fn(self.stack, self.weights, na.MODE_W32_DIV64, self.denom, reorder=reorder, **epi)
-        self.red = ShardedReducer(plan, self.fn, dev, gather=world > 1, state=state)
+        self.red = ShardedReducer(plan, self.fn, dev, gather=world > 1, state=state, push=push)
 
     def reset_state(self, state=None):
         """The fused optimizers' initial state: prev = the seed-1 synthetic model on this rank's
@@ -182,6 +183,9 @@ class Job:
         st.v[0].zero_()
 
     def release(self):
+        """Collective for a push-gathered job (peers unmap this rank's buffer first)."""
+        if self.red is not None:
+            self.red.release()
         self.stack = self.red = self.fn = None
         torch.cuda.empty_cache()
 
@@ -253,6 +257,88 @@ def calibrate(job: Job, world: int, dev, reps: int = 5):
     return StripeModel.fit(big, small, r_big, r_small, g_big, g_small, c_r=c_r, c_g=c_g), cal
 
 
+def calibrate_push(job: Job, world: int, dev, r_big: float, reps: int = 5):
+    """The one-shot push all-gather (fa_dist.PushGather) on the running job: availability (every
+    rank maps its peers' buffers), a bit-compare against RCCL's all-gather of the same slices, the
+    gather of the whole local width and of 1/8 of it, and its contention with the reduce.
+    Returns (StripeModel or None, calibration dict)."""
+    p = job.plan
+    big = p.local_cols
+    small = max(ALIGN, (big // 8) // ALIGN * ALIGN)
+    out = job.red.local_out
+    full = torch.empty(world * big, dtype=torch.float32, device=dev)
+    try:
+        pg = fa_dist.PushGather(full)
+    except RuntimeError as e:
+        return None, {"available": False, "reason": str(e)}
+    try:
+        pg.gather(out[:big], p.rank * big)
+        want = torch.empty_like(full)
+        all_gather_into(want, out[:big])
+        torch.cuda.synchronize(dev)
+        same = _max_over_ranks((0.0 if torch.equal(full, want) else 1.0,), world, dev)[0] == 0.0
+        del want
+        if not same:
+            return None, {"available": False, "reason": "pushed buckets differ from RCCL's all-gather"}
+        for _ in range(2):
+            pg.gather(out[:big], p.rank * big)
+            pg.gather(out[:small], p.rank * small)
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        g_big = _event_time(lambda: pg.gather(out[:big], p.rank * big), reps)
+        g_small = _event_time(lambda: pg.gather(out[:small], p.rank * small), reps)
+        r_conc, g_conc, g_alone = _contention_push(job, pg, out, big, dev, reps)
+    finally:
+        pg.close()
+    r_small = _event_time(lambda: job.fn(0, small, out[:small]), reps)
+    g_big, g_small, r_conc, g_conc, g_alone, r_small = _max_over_ranks(
+        (g_big, g_small, r_conc, g_conc, g_alone, r_small), world, dev)
+    c_r, c_g = max(r_conc / r_big - 1.0, 0.0), max(g_conc / max(g_alone, 1e-9) - 1.0, 0.0)
+    cal = dict(available=True, checked_against_rccl=True, width_cols=[big, small],
+               gather_us=[round(g_big * 1e6, 2), round(g_small * 1e6, 2)],
+               push_kernel_us=round(g_alone * 1e6, 2), concurrent_reduce_us=round(r_conc * 1e6, 2),
+               concurrent_push_us=round(g_conc * 1e6, 2), c_r=round(c_r, 4), c_g=round(c_g, 4),
+               per_link_gbs=round(big * 4 / max(g_alone, 1e-9) / 1e9, 2))
+    return StripeModel.fit(big, small, r_big, r_small, g_big, g_small, c_r=c_r, c_g=c_g), cal
+
+
+def _contention_push(job, pg, out, cols, dev, reps: int):
+    """(reduce time beside a push, push-kernel time beside a reduce, push-kernel time alone)."""
+    side = torch.cuda.Stream(dev)
+    out2 = torch.empty_like(out)
+    cur = torch.cuda.current_stream(dev)
+    r_t, g_t, a_t = [], [], []
+    src, off = out[:cols], job.plan.rank * cols
+    for _ in range(reps):
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(cur)
+        pg.begin()
+        pg.push(src, off)
+        job.fn(0, cols, out2[:cols])
+        e1.record(cur)
+        pg.end()
+        torch.cuda.synchronize(dev)
+        r_t.append(e0.elapsed_time(e1) / 1e3)
+        for beside in (True, False):
+            dist.barrier()
+            e2, e3 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            pg.begin()
+            side.wait_stream(pg.stream)  # the reduce starts with the push, after the barrier
+            if beside:
+                with torch.cuda.stream(side):
+                    job.fn(0, cols, out2[:cols])
+            e2.record(pg.stream)
+            pg.push(src, off)
+            e3.record(pg.stream)
+            pg.end()
+            cur.wait_stream(side)
+            torch.cuda.synchronize(dev)
+            (g_t if beside else a_t).append(e2.elapsed_time(e3) / 1e3)
+    return float(np.median(r_t)), float(np.median(g_t)), float(np.median(a_t))
+
+
 def _contention(job, full, out, cols, dev, reps: int):
     """The reduce and the all-gather of the whole local width run concurrently (real RCCL over
     xGMI at N > 1): (reduce time beside the gather, gather time beside the reduce), each taken on
@@ -306,23 +392,33 @@ def run_job(cfg, layout, n, args, world, rank, dev, g_eff):
         for _ in range(2):
             probe.reduce_only()
         model, cal = calibrate(probe, world, dev)
+        models = {"rccl": model} if args.gather != "push" else {}
+        if world > 1 and args.gather != "rccl":
+            m_push, cal_push = calibrate_push(probe, world, dev, cal["reduce_us"][0] * 1e-6)
+            info["push_calibration"] = cal_push
+            if m_push is not None:
+                models["push"] = m_push
+        if not models:  # --gather push, but pushing is not available here
+            models = {"rccl": model}
         probe.release()
-        cands = shard_candidates(p_real, g_eff, model)
-        widths, rep = cands[0]
+        cands = [(g, w_c, r_c) for g, m in models.items() for w_c, r_c in shard_candidates(p_real, g_eff, m)]
+        gather, widths, rep = min(cands, key=lambda c: models[c[0]].makespan(c[1], c[2])[0])
         trials = []
         if world > 1 and len(cands) > 1:
-            # the model's plan and its neighbours, each timed for a few steps on this job (real
-            # collectives; max over ranks, so every rank picks the same plan)
-            for w_c, r_c in cands:
+            # every gather's model plan and its neighbours, each timed for a few steps on this job
+            # (real collectives; max over ranks, so every rank picks the same plan)
+            for g, w_c, r_c in cands:
                 tj = Job(cfg, layout, n, ShardPlan.from_widths(p_real, g_eff, rank, w_c, rep=r_c), dev, world,
-                         args.reorder)
+                         args.reorder, push=g == "push")
                 for _ in range(2):
                     tj.red.step()
                 t = _max_over_ranks((_event_time(tj.red.step, 5),), world, dev)[0]
                 tj.release()
-                trials.append({"stripe_widths": list(w_c), "replicated_cols": r_c, "predicted_ms":
-                               round(model.makespan(w_c, r_c)[0] * 1e3, 4), "measured_ms": round(t * 1e3, 4)})
-            widths, rep = cands[min(range(len(cands)), key=lambda i: trials[i]["measured_ms"])]
+                trials.append({"gather": g, "stripe_widths": list(w_c), "replicated_cols": r_c, "predicted_ms":
+                               round(models[g].makespan(w_c, r_c)[0] * 1e3, 4), "measured_ms": round(t * 1e3, 4)})
+            gather, widths, rep = cands[min(range(len(cands)), key=lambda i: trials[i]["measured_ms"])]
+        model = models[gather]
+        info["gather"] = gather
         plan = ShardPlan.from_widths(p_real, g_eff, rank, widths, rep=rep)
         pred, red_s, exposed = model.makespan(plan.widths, plan.rep)
         info.update(stripe_choice=("model (flearn_amd.dist.plan_shards: stripes + replicated tail), coefficients "
@@ -338,7 +434,9 @@ def run_job(cfg, layout, n, args, world, rank, dev, g_eff):
     info["stripe_widths"] = list(plan.widths)
     # columns every rank reduces itself (no gather): redundant work, counted once in `value`
     info["replicated_cols"] = plan.rep
-    job = Job(cfg, layout, n, plan, dev, world, args.reorder)
+    if world > 1 and args.stripes:
+        info["gather"] = "push" if args.gather == "push" else "rccl"
+    job = Job(cfg, layout, n, plan, dev, world, args.reorder, push=info.get("gather") == "push")
     for _ in range(args.warmup):
         job.red.step()
     torch.cuda.synchronize(dev)
@@ -547,6 +645,9 @@ def main():
     ap.add_argument("--reorder", action="store_true",
                     help="allow the split-N kernel (deterministic, <= 1e-6 normwise, not bit-exact)")
     ap.add_argument("--no-verify", action="store_true", help="skip the post-run check of the reassembled model")
+    ap.add_argument("--gather", choices=("auto", "rccl", "push"), default="auto",
+                    help="N>1: how stripes are reassembled — RCCL's all-gather, the one-shot push over "
+                         "xGMI (peer stores, flearn_amd.dist.PushGather), or whichever measures faster")
     ap.add_argument("--no-loopback", action="store_true",
                     help="N>1: skip the single-process AVG(devices=[...]) loopback measurement")
     args = ap.parse_args()
@@ -663,6 +764,8 @@ def main():
         ojob.release()
 
     if world > 1:
+        if job is not None and job.red is not None:
+            job.red.release()  # unmap the peers' buffers (push) while the group still exists
         dist.barrier()
         dist.destroy_process_group()
     loop = None
@@ -702,7 +805,9 @@ def main():
                 "order": ("split-N allowed (fixed-order tree of client splits, <= 1e-6 normwise)" if args.reorder
                           else "reference client order (bit-exact)"),
                 "parallelism": ("single GPU" if g_eff == 1 else
-                                f"element-range shards x{g_eff} + RCCL all-gather ({plan.stripes} stripes"
+                                f"element-range shards x{g_eff} + "
+                                + ("one-shot push all-gather over xGMI (peer stores)" if info.get("gather") == "push"
+                                   else "RCCL all-gather") + f" ({plan.stripes} stripes"
                                 + (f", widths {'/'.join(str(x) for x in plan.widths)}" if plan.stripes > 1
                                    else "")
                                 + (f"; the last {plan.rep} columns reduced by every rank, not gathered"

@@ -17,7 +17,7 @@ from pathlib import Path
 import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 
 LIB_PATH = Path(__file__).resolve().parent / "lib" / "libflearn_amd.so"
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 FA_OK = 0
 FA_ERR_ARG, FA_ERR_ALIGN, FA_ERR_LAUNCH = -1, -2, -3
@@ -43,6 +43,10 @@ EXPORTS = (
     "fa_gather_rows_f64",
     "fa_fill_uniform_f32",
     "fa_copy",
+    "fa_ipc_handle",
+    "fa_ipc_open",
+    "fa_ipc_close",
+    "fa_push",
     "fa_set_reduce_grid",
     "fa_b64_decoded_size",
     "fa_b64_decode",
@@ -190,6 +194,10 @@ def load(require_gpu: bool = False):
                 "fa_gather_rows_f64": ([P, I64, I32, P, P, I32, P], ctypes.c_int),
                 "fa_fill_uniform_f32": ([P, I64, I32, I64, ctypes.c_uint64, I64, I64, P], ctypes.c_int),
                 "fa_copy": ([P, P, I64, P], ctypes.c_int),
+                "fa_ipc_handle": ([P, P, ctypes.POINTER(I64)], ctypes.c_int),
+                "fa_ipc_open": ([P, ctypes.POINTER(P)], ctypes.c_int),
+                "fa_ipc_close": ([P], ctypes.c_int),
+                "fa_push": ([P, I64, ctypes.POINTER(P), I32, P], ctypes.c_int),
                 "fa_set_reduce_grid": ([I32], ctypes.c_int),
                 "fa_b64_decoded_size": ([P, I64], I64),
                 "fa_b64_decode": ([P, I64, P, I64, I32], ctypes.c_int),

@@ -1504,6 +1504,26 @@ __global__ __launch_bounds__(kThreads) void copy_kernel(uint8_t* __restrict__ ds
   if (blockIdx.x == 0 && threadIdx.x < tail) dst[(quads << 4) + threadIdx.x] = src[(quads << 4) + threadIdx.x];
 }
 
+// One-shot all-gather leg (fa_push): each lane loads 16 B of the local stripe once and stores it
+// into every destination (the peers' receive buffers over their xGMI links, and the local one);
+// the closing system-scope fence makes the peer stores visible once the kernel has completed.
+struct PushDsts {
+  uint8_t* p[8];
+};
+
+__global__ __launch_bounds__(kThreads) void push_kernel(const uint8_t* __restrict__ src, int64_t quads, PushDsts d,
+                                                        int n_dsts) {
+  typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+  const u4* s = reinterpret_cast<const u4*>(src);
+  for (int64_t q = (int64_t)blockIdx.x * kThreads + threadIdx.x; q < quads; q += (int64_t)gridDim.x * kThreads) {
+    const u4 v = __builtin_nontemporal_load(s + q);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      if (i < n_dsts) reinterpret_cast<u4*>(d.p[i])[q] = v;
+  }
+  __threadfence_system();
+}
+
 __device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
   z += 0x9E3779B97F4A7C15ull;
   z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;

@@ -14,6 +14,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <cstring>
 #include <atomic>
 #include <string>
 #include <vector>
@@ -731,6 +732,57 @@ int fa_copy(void* dst, const void* src, int64_t nbytes, void* stream) {
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(copy_kernel, dim3((unsigned)blocks), dim3(kThreads), 0, static_cast<hipStream_t>(stream),
                      static_cast<uint8_t*>(dst), static_cast<const uint8_t*>(src), nbytes);
+  return launch_check();
+}
+
+int fa_ipc_handle(const void* ptr, void* handle, int64_t* offset) {
+  if (!ptr || !handle || !offset) return fail(FA_ERR_ARG, "null ipc argument");
+  static_assert(sizeof(hipIpcMemHandle_t) == FA_IPC_HANDLE_BYTES, "IPC handle size");
+  hipDeviceptr_t base = nullptr;
+  size_t size = 0;
+  hipError_t e = hipMemGetAddressRange(&base, &size, reinterpret_cast<hipDeviceptr_t>(const_cast<void*>(ptr)));
+  if (e != hipSuccess) return fail(FA_ERR_ARG, hipGetErrorString(e));
+  hipIpcMemHandle_t h;
+  e = hipIpcGetMemHandle(&h, reinterpret_cast<void*>(base));
+  if (e != hipSuccess) return fail(FA_ERR_LAUNCH, hipGetErrorString(e));
+  memcpy(handle, &h, sizeof h);
+  *offset = (int64_t)((const char*)ptr - (const char*)base);
+  return FA_OK;
+}
+
+int fa_ipc_open(const void* handle, void** base) {
+  if (!handle || !base) return fail(FA_ERR_ARG, "null ipc argument");
+  hipIpcMemHandle_t h;
+  memcpy(&h, handle, sizeof h);
+  const hipError_t e = hipIpcOpenMemHandle(base, h, hipIpcMemLazyEnablePeerAccess);
+  if (e != hipSuccess) return fail(FA_ERR_LAUNCH, hipGetErrorString(e));
+  return FA_OK;
+}
+
+int fa_ipc_close(void* base) {
+  if (!base) return fail(FA_ERR_ARG, "null ipc base");
+  const hipError_t e = hipIpcCloseMemHandle(base);
+  if (e != hipSuccess) return fail(FA_ERR_LAUNCH, hipGetErrorString(e));
+  return FA_OK;
+}
+
+int fa_push(const void* src, int64_t nbytes, void* const* dsts, int32_t n_dsts, void* stream) {
+  if (nbytes < 0 || n_dsts < 0 || n_dsts > 8) return fail(FA_ERR_ARG, "bad push size or destination count");
+  if (nbytes == 0 || n_dsts == 0) return FA_OK;
+  if (!src || !dsts) return fail(FA_ERR_ARG, "null push pointer");
+  PushDsts d{};
+  uintptr_t any = (uintptr_t)src;
+  for (int i = 0; i < n_dsts; ++i) {
+    if (!dsts[i]) return fail(FA_ERR_ARG, "null push destination");
+    d.p[i] = static_cast<uint8_t*>(dsts[i]);
+    any |= (uintptr_t)dsts[i];
+  }
+  if ((any & 15) || (nbytes & 15)) return fail(FA_ERR_ALIGN, "push pointers and size must be 16-byte multiples");
+  const int64_t quads = nbytes / 16;
+  int64_t blocks = (quads + kThreads - 1) / kThreads;
+  if (blocks > 1024) blocks = 1024;
+  hipLaunchKernelGGL(push_kernel, dim3((unsigned)blocks), dim3(kThreads), 0, static_cast<hipStream_t>(stream),
+                     static_cast<const uint8_t*>(src), quads, d, n_dsts);
   return launch_check();
 }
 

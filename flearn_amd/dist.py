@@ -36,12 +36,14 @@ host memory around the collective (`all_gather_into`).
 """
 from __future__ import annotations
 
+import ctypes
 from dataclasses import dataclass
 
 import torch
 import torch.distributed as dist
 
 ALIGN = 64
+MAX_PUSH_RANKS = 8  # fa_push's destination count: one MI355X node
 
 
 def _host_staged(t: torch.Tensor, group) -> bool:
@@ -59,6 +61,119 @@ def all_gather_into(dst: torch.Tensor, src: torch.Tensor, group=None, async_op: 
     dist.all_gather_into_tensor(hdst, hsrc, group=group)
     dst.copy_(hdst)
     return None
+
+
+class PushGather:
+    """One-shot all-gather over xGMI by direct peer stores (C ABI fa_ipc_* / fa_push).
+
+    Every rank registers its receive buffer `full` once (IPC handles exchanged with
+    all_gather_object) and maps its peers' buffers; a reduced stripe is then pushed by ONE kernel
+    into every rank's `full` at the same offset — each peer's copy crosses that peer's own xGMI
+    link, nothing is forwarded, received data is never re-read, and the receiving GPU spends no
+    kernel on it (RCCL's all-gather forwards chunks along rings and copies them out of its
+    buffers on every GPU: HBM traffic that competes with the reduce).
+    Ordering, all on this object's stream: `begin()` — a barrier after this rank's earlier work on
+    the compute stream (no peer may overwrite a `full` its owner is still reading); `push()` after
+    the stripe's reduce; `end()` — a barrier after the pushes, which the compute stream then waits
+    for: once every rank has passed it, every peer's stores into this rank's `full` are complete
+    (each push kernel ends with a system-scope release).  On RCCL the barriers are 1-element
+    all_reduces ordered on the stream; on gloo (several processes sharing one GPU in the tests)
+    host synchronisations plus dist.barrier.
+    Construction is collective and all-or-nothing: if any rank cannot map a peer, every rank
+    raises RuntimeError (nothing stays mapped) and the caller keeps RCCL's all-gather."""
+
+    def __init__(self, full: torch.Tensor, group=None):
+        from . import _native as na
+
+        self.na, self.L = na, na.lib()
+        self.full, self.group = full, group
+        self.world, self.rank = dist.get_world_size(group), dist.get_rank(group)
+        self.device = full.device
+        self.nccl = dist.get_backend(group) == "nccl"
+        self.bases, self.dst = [], []
+        ok = 1
+        mine = None
+        if self.world > MAX_PUSH_RANKS or not full.is_cuda or not full.is_contiguous():
+            ok = 0
+        else:
+            h, off = ctypes.create_string_buffer(64), ctypes.c_int64(0)
+            if self.L.fa_ipc_handle(full.data_ptr(), h, ctypes.byref(off)) == 0:
+                mine = (bytes(h.raw), int(off.value))
+            else:
+                ok = 0
+        infos = [None] * self.world
+        dist.all_gather_object(infos, mine, group=group)
+        if ok and all(i is not None for i in infos):
+            for r, (hb, off) in enumerate(infos):
+                if r == self.rank:
+                    self.dst.append(full.data_ptr())
+                    continue
+                base = ctypes.c_void_p()
+                if self.L.fa_ipc_open(hb, ctypes.byref(base)) != 0 or not base.value:
+                    ok = 0
+                    break
+                self.bases.append(base.value)
+                self.dst.append(base.value + off)
+        else:
+            ok = 0
+        if not self._all_ok(ok):
+            self._unmap()
+            err = self.L.fa_last_error()
+            raise RuntimeError("PushGather: a rank could not map its peers' receive buffers"
+                               + (f" (here: {err.decode(errors='replace')})" if err and not ok else ""))
+        self.stream = torch.cuda.Stream(self.device)
+        self.flag = torch.zeros(1, dtype=torch.float32, device=self.device)
+
+    def _all_ok(self, ok: int) -> bool:
+        t = torch.tensor([ok], dtype=torch.int32, device=self.device if self.nccl else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self.group)
+        return bool(t.item())
+
+    def _barrier(self):
+        if self.nccl:
+            with torch.cuda.stream(self.stream):
+                dist.all_reduce(self.flag, group=self.group)
+        else:
+            torch.cuda.synchronize(self.device)
+            dist.barrier(group=self.group)
+
+    def begin(self):
+        self.stream.wait_stream(torch.cuda.current_stream(self.device))
+        self._barrier()
+
+    def push(self, src: torch.Tensor, elem_offset: int):
+        """Stores src (this rank's reduced slice) into every rank's `full` at elem_offset."""
+        n = src.numel() * src.element_size()
+        if n == 0:
+            return
+        off = elem_offset * self.full.element_size()
+        if elem_offset < 0 or off + n > self.full.numel() * self.full.element_size():
+            raise ValueError("push outside the receive buffer")
+        self.stream.wait_stream(torch.cuda.current_stream(self.device))
+        dsts = (ctypes.c_void_p * self.world)(*[d + off for d in self.dst])
+        self.na.check(self.L.fa_push(src.data_ptr(), n, dsts, self.world, self.stream.cuda_stream), "fa_push")
+
+    def end(self):
+        self._barrier()
+        torch.cuda.current_stream(self.device).wait_stream(self.stream)
+
+    def gather(self, src: torch.Tensor, elem_offset: int):
+        """A whole all-gather of one slice: begin, push, end."""
+        self.begin()
+        self.push(src, elem_offset)
+        self.end()
+
+    def _unmap(self):
+        for b in self.bases:
+            self.L.fa_ipc_close(b)
+        self.bases, self.dst = [], []
+
+    def close(self):
+        """Collective: after every rank's pushes are done, unmap the peers' buffers."""
+        if self.dst:
+            torch.cuda.synchronize(self.device)
+            dist.barrier(group=self.group)
+            self._unmap()
 
 
 @dataclass(frozen=True)
@@ -366,7 +481,8 @@ class ShardedReducer:
     the oracle to check the sharding and gather logic with gloo.
     """
 
-    def __init__(self, plan: ShardPlan, reduce_fn, device, group=None, local_out=None, gather=None, state=None):
+    def __init__(self, plan: ShardPlan, reduce_fn, device, group=None, local_out=None, gather=None, state=None,
+                 push: bool = False):
         self.plan = plan
         self.reduce_fn = reduce_fn
         self.device = torch.device(device)
@@ -386,6 +502,15 @@ class ShardedReducer:
         # one rank: local columns ARE the global columns, nothing to reassemble
         self.full = (torch.empty(plan.full_cols, dtype=torch.float32, device=self.device) if self.gather
                      else None)
+        # push=True: reassemble with direct peer stores (PushGather) instead of RCCL's all-gather;
+        # raises RuntimeError on every rank when some rank cannot map its peers
+        self.pusher = PushGather(self.full, group) if self.gather and push else None
+
+    def release(self):
+        """Collective when pushing: unmap the peers' buffers before any rank frees its own."""
+        if self.pusher is not None:
+            self.pusher.close()
+            self.pusher = None
 
     @property
     def local_out(self) -> torch.Tensor:
@@ -396,10 +521,15 @@ class ShardedReducer:
         p = self.plan
         works = []
         out = self.local_out
+        pg = self.pusher
+        if pg is not None:
+            pg.begin()
         for c in range(p.stripes):
             lo, sc = p.local_begin(c), p.shard_of(c)
             self.reduce_fn(lo, sc, out[lo : lo + sc])
-            if self.gather:
+            if pg is not None:  # this rank's slice of stripe c, into every rank's bucket
+                pg.push(out[lo : lo + sc], p.world * lo + p.rank * sc)
+            elif self.gather:
                 g0 = p.world * lo  # stripe c's contiguous range of the global bucket
                 dst = self.full[g0 : g0 + p.world * sc]
                 w = all_gather_into(dst, out[lo : lo + sc], group=self.group, async_op=True)
@@ -415,6 +545,8 @@ class ShardedReducer:
                     self.full[g0 : g0 + p.rep].copy_(out[lo : lo + p.rep])
         if self.state is not None:
             self.state.flip()
+        if pg is not None:
+            pg.end()
         for w in works:
             w.wait()
         return self.full[: p.n_cols] if self.gather else out[: p.n_cols]

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define FA_ABI_VERSION 8
+#define FA_ABI_VERSION 9
 
 /* return codes */
 #define FA_OK 0
@@ -226,6 +226,31 @@ int fa_set_reduce_grid(int32_t grid);
  * flearn as numpy arrays, strategy.py:123-129).  FA_ERR_ALIGN when a pointer is not 16-byte
  * aligned (the caller then uses the copy engine).                                             */
 int fa_copy(void* dst, const void* src, int64_t nbytes, void* stream);
+
+/* ---- one-shot all-gather over xGMI (multi-GPU reassembly) -----------------
+ * The reference has no multi-GPU path; these replace the all-gather that reassembles the
+ * column-sharded global model (the north star's "RCCL all-gather over xGMI") with direct peer
+ * stores: every rank maps its peers' receive buffers once (IPC handles exchanged by the caller)
+ * and pushes each reduced stripe straight into all of them, one xGMI link per peer, with no
+ * forwarding and no re-read of received data.  The caller orders pushes and reads with barriers
+ * (flearn_amd.dist.PushGather). */
+#define FA_IPC_HANDLE_BYTES 64
+
+/* The IPC handle of the device allocation holding `ptr` (handle: FA_IPC_HANDLE_BYTES bytes) and
+ * ptr's byte offset in it.                                                                   */
+int fa_ipc_handle(const void* ptr, void* handle, int64_t* offset);
+
+/* Map a peer process's allocation (its fa_ipc_handle) into this process: *base = its start.   */
+int fa_ipc_open(const void* handle, void** base);
+
+/* Unmap a base returned by fa_ipc_open.                                                      */
+int fa_ipc_close(void* base);
+
+/* Copy nbytes from src to each of dsts[0..n_dsts) (n_dsts <= 8; every pointer 16-byte aligned;
+ * dsts: a HOST array of device pointers, local or peer-mapped) in one kernel on `stream`; every
+ * lane ends with a system-scope release so the stores are visible to the peers once the kernel
+ * has completed.                                                                              */
+int fa_push(const void* src, int64_t nbytes, void* const* dsts, int32_t n_dsts, void* stream);
 
 /* ---- wire codec (HOST functions: every pointer below is host memory) -------------------------
  * flearn's HTTP mode ships uploads and global models as base64(pickle.dumps(obj))

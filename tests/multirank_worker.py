@@ -231,8 +231,74 @@ def case_sharded_reducer(rank, world):
                 assert full.tobytes() == want.astype(np.float32).tobytes(), (rank, plan.widths, op, step)
 
 
+def case_sharded_reducer_push(rank, world):
+    """The same ShardedReducer steps reassembled by PushGather (direct peer stores through
+    IPC-mapped receive buffers, fa_push) instead of the all-gather: every rank's model equals the
+    C oracle's bit for bit; plus one PushGather.gather of a rank-stamped slice against
+    all_gather_into, and a push outside the receive buffer refused."""
+    import oracle
+    from flearn_amd import _native as na
+    from flearn_amd import aggregator as agg
+    from flearn_amd.dist import PushGather, ShardedReducer, ShardPlan, StripeModel, all_gather_into, hip_reduce_fn
+    from flearn_amd.dist import plan_shards, plan_stripes
+
+    cuda = torch.device("cuda", 0)
+    full = torch.full((world * 4096,), -1.0, device=cuda)
+    pg = PushGather(full, None)
+    src = torch.arange(4096, dtype=torch.float32, device=cuda) + 10000.0 * rank
+    pg.gather(src, rank * 4096)
+    want = torch.empty_like(full)
+    all_gather_into(want, src)
+    torch.cuda.synchronize()
+    assert torch.equal(full, want), rank
+    try:
+        pg.push(src, world * 4096 - 64)
+        raise AssertionError("push past the end accepted")
+    except ValueError:
+        pass
+    pg.close()
+
+    n, p = 9, 700_001
+    lc = -(-p // world)
+    widths, rep = plan_shards(p, world, StripeModel(1e-6, 2e-9, 2e-6, 1e-8))
+    plans = [ShardPlan.make(p, world, rank, 1), ShardPlan.make(p, world, rank, 2, weights=(3, 1)),
+             ShardPlan.from_widths(p, world, rank, plan_stripes(lc, StripeModel.assumed(n, world))),
+             ShardPlan.from_widths(p, world, rank, widths, rep=rep)]
+    w_h = np.linspace(0.5, 1.5, n).astype(np.float32)
+    denom = float(np.sum([float(x) for x in w_h]))
+    want_mean = oracle.c_reduce(oracle.MODE_W32_DIV64, oracle.fill_uniform(n, p, 3), w_h, denom)
+    for plan in plans:
+        for op in ("mean", "adagrad"):
+            stack = torch.empty((n, plan.local_stride), dtype=torch.float32, device=cuda)
+            for lo, g0, width in plan.segments():
+                agg.fill_uniform(stack[:, lo:], seed=3, col_begin=g0, n_cols=width)
+            w = torch.from_numpy(w_h).to(cuda)
+            epi, local_out = {}, None
+            if op != "mean":
+                prev = torch.empty((1, plan.local_stride), dtype=torch.float32, device=cuda)
+                for lo, g0, width in plan.segments():
+                    agg.fill_uniform(prev[:, lo:], seed=4, col_begin=g0, n_cols=width)
+                epi = dict(op=na.OP_BY_NAME[op], prev=prev[0],
+                           v=torch.zeros(plan.local_stride, dtype=torch.float64, device=cuda))
+                local_out = prev[0]
+            red = ShardedReducer(plan, hip_reduce_fn(stack, w, na.MODE_W32_DIV64, denom, **epi), cuda,
+                                 local_out=local_out, gather=True, push=True)
+            assert red.pusher is not None
+            want = want_mean.copy()
+            prev_h = oracle.fill_uniform(1, p, 4)[0]
+            v_h = np.zeros(p)
+            for step in range(3):
+                full = red.step().cpu().numpy()
+                if op != "mean":
+                    want = oracle.c_update(op, want_mean, prev_h, v_h)
+                    prev_h = want.astype(np.float32)
+                assert full.tobytes() == want.astype(np.float32).tobytes(), (rank, plan.widths, op, step)
+            red.release()
+
+
 CASES = {f.__name__[5:]: f for f in (case_avg_fixtures, case_setup_strategy, case_fused_rounds,
-                                      case_first_round_adopt, case_empty_ranks, case_dyn, case_sharded_reducer)}
+                                      case_first_round_adopt, case_empty_ranks, case_dyn, case_sharded_reducer,
+                                      case_sharded_reducer_push)}
 
 
 def rank_main(rank, world, port, names):

@@ -48,7 +48,13 @@ def test_bench_two_ranks_rehearsal(config, cuda):
     # the reduce / gather contention of this node, measured concurrently, is in the fitted model
     cal = mg["calibration"]
     assert cal["c_r"] >= 0 and cal["c_g"] >= 0 and cal["concurrent_reduce_us"] > 0
-    assert mg["model"]["c_r"] == cal["c_r"] and mg["model"]["c_g"] == cal["c_g"]
+    # the one-shot push gather was set up (IPC-mapped peer buffers: here two processes on one
+    # GPU), checked bit for bit against the all-gather, calibrated, and timed in the trials
+    pc = mg["push_calibration"]
+    assert pc["available"] is True and pc["checked_against_rccl"] is True and pc["push_kernel_us"] > 0
+    assert {t["gather"] for t in mg["plan_trials"]} == {"rccl", "push"}
+    used = cal if mg["gather"] == "rccl" else pc
+    assert mg["model"]["c_r"] == used["c_r"] and mg["model"]["c_g"] == used["c_g"]
     # the serial plan (one stripe, no tail) is among the measured trials
     assert any(len(t["stripe_widths"]) == 1 and t["replicated_cols"] == 0 for t in mg["plan_trials"])
     # stripes (padded) or stripes + a replicated tail cover the bucket
@@ -59,7 +65,8 @@ def test_bench_two_ranks_rehearsal(config, cuda):
     # the plan is the fastest of the measured candidates
     trials = mg["plan_trials"]
     best = min(trials, key=lambda t: t["measured_ms"])
-    assert (best["stripe_widths"], best["replicated_cols"]) == (mg["stripe_widths"], mg["replicated_cols"])
+    assert (best["gather"], best["stripe_widths"], best["replicated_cols"]) == (
+        mg["gather"], mg["stripe_widths"], mg["replicated_cols"])
     assert d["weak"]["clients"] == 200 and d["weak"]["value"] > 0
     assert d["roofline"]["bound"] == "hbm" and d["roofline"]["frac"] > 0
     # the reassembled model was checked bit for bit on >= 64 boundary windows, on both ranks
@@ -75,6 +82,17 @@ def test_bench_two_ranks_rehearsal(config, cuda):
     for o in ("reference", "device"):
         assert lb[o]["verified"] is True and lb[o]["round_ms"] > 0 and lb[o]["pack_h2d_ms"] > 0
         assert len(lb[o]["h2d_gbs_per_gpu"]) == 2 and min(lb[o]["h2d_gbs_per_gpu"]) > 0
+
+
+@pytest.mark.timeout(300)
+def test_bench_push_gather_is_verified(cuda):
+    """--gather push --stripes 3: every stripe reassembled by direct peer stores; the line says so
+    and its self-check passes on both ranks."""
+    p = _rehearse("c3", ("--no-weak", "--no-loopback", "--stripes", "3", "--gather", "push"))
+    assert p.returncode == 0, p.stderr[-4000:]
+    d = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][0])
+    assert d["multi_gpu"]["gather"] == "push" and "push all-gather" in d["config"]["parallelism"]
+    assert d["verify"]["verified"] is True and d["verify"]["ranks_checked"] == 2
 
 
 @pytest.mark.timeout(300)

@@ -71,3 +71,11 @@ def test_sharded_reducer_hip_ranks(world, cuda):
     """bench.py's ShardedReducer with the HIP kernel on every rank: 1 stripe, 3:1 stripes and the
     model-planned stripes; mean, fused AVGM and Adagrad over two steps."""
     _run_ranks(world, ["sharded_reducer"])
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_reducer_push_gather(world, cuda):
+    """ShardedReducer reassembled by PushGather: IPC-mapped peer buffers and one fa_push kernel
+    per stripe (here every "peer" is another process on the same GPU), bit-exact."""
+    _run_ranks(world, ["sharded_reducer_push"])
