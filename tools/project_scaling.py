@@ -38,7 +38,7 @@ OVERLAP = (REPO / "profiles" / "r04" / "overlap" / "overlap.json",
            REPO / "profiles" / "r04" / "overlap" / "overlap_rw.json")
 
 
-def contention(ingress_bs: float, paths=OVERLAP):
+def contention(ingress_bs: float, paths=OVERLAP, local_traffic: float = 2.0):
     """(c_r, c_g, the stand-in used) for a gather bringing `ingress_bs` into each GPU: from the
     one-GPU overlap probes (tools/overlap_probe.py) at the library's default reduce grid, the
     smallest copy stand-in whose local HBM traffic (2 x its copy rate: read + write) is at least
@@ -55,23 +55,28 @@ def contention(ingress_bs: float, paths=OVERLAP):
                 for k, v in row["with"].items() if k.isdigit()]
     pts.sort()
     for rate, c_r, c_g, k in pts:
-        if rate >= ingress_bs:
+        if 2.0 * rate >= local_traffic * ingress_bs:
             return c_r, c_g, f"copy on {k} blocks ({rate / 1e9:.0f} GB/s)"
     rate, c_r, c_g, k = pts[-1]
     return c_r, c_g, f"copy on {k} blocks ({rate / 1e9:.0f} GB/s)"
 
 
-def project(cfg: str, g: int, link_bs: float, launch_s=10e-6, collective_s=30e-6, tail=True, contended=False):
+def project(cfg: str, g: int, link_bs: float, launch_s=10e-6, collective_s=30e-6, tail=True, contended=False,
+            push=False, barrier_s=15e-6):
+    """push: the one-shot push gather (flearn_amd.dist.PushGather) — a launch per stripe instead
+    of a collective, two barriers per step, and local HBM traffic of ingress * (1 + 1/(G-1))
+    (received bytes written, the own slice read once) instead of a ring's ~2 x ingress."""
     n, p = CONFIGS[cfg]
     t1 = one_gpu_step(cfg)
     local = -(-p // g)
     local = -(-local // ALIGN) * ALIGN
     b_r = t1 / p  # the 1-GPU per-column cost (fused state traffic included)
     b_g = (g - 1) * 4.0 / ((g - 1) * link_bs) if g > 1 else 0.0
-    m = StripeModel(launch_s, b_r, collective_s if g > 1 else 0.0, b_g)
+    a_g = (launch_s if push else collective_s) if g > 1 else 0.0
+    m = StripeModel(launch_s, b_r, a_g, b_g)
     stand_in = None
     if contended and g > 1:
-        c_r, c_g, stand_in = contention((g - 1) * link_bs)
+        c_r, c_g, stand_in = contention((g - 1) * link_bs, local_traffic=(1.0 + 1.0 / (g - 1)) if push else 2.0)
         m = m.with_contention(c_r, c_g)
     if g == 1:
         widths, rep = (local,), 0
@@ -80,7 +85,9 @@ def project(cfg: str, g: int, link_bs: float, launch_s=10e-6, collective_s=30e-6
     else:
         widths, rep = plan_stripes(local, m), 0
     step, red, exposed = m.makespan(widths, rep)
-    return {"config": cfg, "gpus": g, "link_GBs": link_bs / 1e9, "ingress_GBs": (g - 1) * link_bs / 1e9,
+    if push and g > 1:
+        step += 2 * barrier_s
+    return {"config": cfg, "gather": "push" if push else "rccl", "gpus": g, "link_GBs": link_bs / 1e9, "ingress_GBs": (g - 1) * link_bs / 1e9,
             "stripes": len(widths), "replicated_frac": round(rep / p, 3), "step_ms": round(step * 1e3, 3),
             "reduce_ms": round(red * 1e3, 3), "exposed_gather_ms": round(exposed * 1e3, 3),
             "speedup": round(t1 / step, 2), "c_r": round(m.c_r, 3), "c_g": round(m.c_g, 3), "stand_in": stand_in}
@@ -91,10 +98,11 @@ def main():
     ap.add_argument("--link-gbs", default="50,64")
     ap.add_argument("--json", action="store_true")
     ap.add_argument("--no-tail", action="store_true", help="stripes only (no replicated tail)")
+    ap.add_argument("--push", action="store_true", help="the one-shot push gather instead of RCCL's all-gather")
     ap.add_argument("--contended", action="store_true",
                     help="reduce / gather slowed by the measured one-GPU contention (profiles/r04/overlap)")
     a = ap.parse_args()
-    rows = [project(c, g, float(l) * 1e9, tail=not a.no_tail, contended=a.contended)
+    rows = [project(c, g, float(l) * 1e9, tail=not a.no_tail, contended=a.contended, push=a.push)
             for l in a.link_gbs.split(",") for c in CONFIGS for g in (2, 4, 8)]
     if a.json:
         print(json.dumps(rows, indent=1))
