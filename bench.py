@@ -150,7 +150,7 @@ class Job:
     columns (plan) resident in HBM, the fused HIP reduce per stripe and (world > 1) the RCCL
     all-gather of every stripe."""
 
-    def __init__(self, cfg, layout, n, plan, dev, world, reorder, push=False):
+    def __init__(self, cfg, layout, n, plan, dev, world, reorder, push=False, push_grid=0):
         self.cfg, self.n, self.plan, self.dev = cfg, n, plan, dev
         self.push = push
         cols, stride = plan.local_cols, plan.local_stride
@@ -171,7 +171,7 @@ class Job:
             self.reset_state(state)
             epi = dict(op=na.OP_BY_NAME[cfg["op"]], state=state)
         self.fn = hip_reduce_fn(self.stack, self.weights, na.MODE_W32_DIV64, self.denom, reorder=reorder, **epi)
-        self.red = ShardedReducer(plan, self.fn, dev, gather=world > 1, state=state, push=push)
+        self.red = ShardedReducer(plan, self.fn, dev, gather=world > 1, state=state, push=push, push_grid=push_grid)
 
     def reset_state(self, state=None):
         """The fused optimizers' initial state: prev = the seed-1 synthetic model on this rank's
@@ -257,6 +257,9 @@ def calibrate(job: Job, world: int, dev, reps: int = 5):
     return StripeModel.fit(big, small, r_big, r_small, g_big, g_small, c_r=c_r, c_g=c_g), cal
 
 
+PUSH_GRIDS = (16, 32, 64, 128, 256)
+
+
 def calibrate_push(job: Job, world: int, dev, r_big: float, reps: int = 5):
     """The one-shot push all-gather (fa_dist.PushGather) on the running job: availability (every
     rank maps its peers' buffers), a bit-compare against RCCL's all-gather of the same slices, the
@@ -285,16 +288,29 @@ def calibrate_push(job: Job, world: int, dev, r_big: float, reps: int = 5):
             pg.gather(out[:small], p.rank * small)
         torch.cuda.synchronize(dev)
         dist.barrier()
+        # the push kernel's grid: the smallest within 3% of the fastest whole-width gather (more
+        # blocks keep more stores in flight for the links but take the memory pipeline from the
+        # reduce beside it: DESIGN.md section 6)
+        by_grid = {}
+        for g in PUSH_GRIDS:
+            pg.grid = g
+            by_grid[g] = _event_time(lambda: pg.gather(out[:big], p.rank * big), 3)
+        times = _max_over_ranks(list(by_grid.values()), world, dev)
+        by_grid = dict(zip(PUSH_GRIDS, times))
+        best = min(times)
+        pg.grid = min(g for g, t in by_grid.items() if t <= 1.03 * best)
         g_big = _event_time(lambda: pg.gather(out[:big], p.rank * big), reps)
         g_small = _event_time(lambda: pg.gather(out[:small], p.rank * small), reps)
         r_conc, g_conc, g_alone = _contention_push(job, pg, out, big, dev, reps)
+        grid = pg.grid
     finally:
         pg.close()
     r_small = _event_time(lambda: job.fn(0, small, out[:small]), reps)
     g_big, g_small, r_conc, g_conc, g_alone, r_small = _max_over_ranks(
         (g_big, g_small, r_conc, g_conc, g_alone, r_small), world, dev)
     c_r, c_g = max(r_conc / r_big - 1.0, 0.0), max(g_conc / max(g_alone, 1e-9) - 1.0, 0.0)
-    cal = dict(available=True, checked_against_rccl=True, width_cols=[big, small],
+    cal = dict(available=True, checked_against_rccl=True, width_cols=[big, small], grid=grid,
+               gather_us_by_grid={str(g): round(t * 1e6, 2) for g, t in by_grid.items()},
                gather_us=[round(g_big * 1e6, 2), round(g_small * 1e6, 2)],
                push_kernel_us=round(g_alone * 1e6, 2), concurrent_reduce_us=round(r_conc * 1e6, 2),
                concurrent_push_us=round(g_conc * 1e6, 2), c_r=round(c_r, 4), c_g=round(c_g, 4),
@@ -392,10 +408,12 @@ def run_job(cfg, layout, n, args, world, rank, dev, g_eff):
         for _ in range(2):
             probe.reduce_only()
         model, cal = calibrate(probe, world, dev)
+        push_grid = 0
         models = {"rccl": model} if args.gather != "push" else {}
         if world > 1 and args.gather != "rccl":
             m_push, cal_push = calibrate_push(probe, world, dev, cal["reduce_us"][0] * 1e-6)
             info["push_calibration"] = cal_push
+            push_grid = cal_push.get("grid", 0)
             if m_push is not None:
                 models["push"] = m_push
         if not models:  # --gather push, but pushing is not available here
@@ -409,7 +427,7 @@ def run_job(cfg, layout, n, args, world, rank, dev, g_eff):
             # (real collectives; max over ranks, so every rank picks the same plan)
             for g, w_c, r_c in cands:
                 tj = Job(cfg, layout, n, ShardPlan.from_widths(p_real, g_eff, rank, w_c, rep=r_c), dev, world,
-                         args.reorder, push=g == "push")
+                         args.reorder, push=g == "push", push_grid=push_grid)
                 for _ in range(2):
                     tj.red.step()
                 t = _max_over_ranks((_event_time(tj.red.step, 5),), world, dev)[0]
@@ -419,6 +437,7 @@ def run_job(cfg, layout, n, args, world, rank, dev, g_eff):
             gather, widths, rep = cands[min(range(len(cands)), key=lambda i: trials[i]["measured_ms"])]
         model = models[gather]
         info["gather"] = gather
+        info["push_grid"] = push_grid if gather == "push" else None
         plan = ShardPlan.from_widths(p_real, g_eff, rank, widths, rep=rep)
         pred, red_s, exposed = model.makespan(plan.widths, plan.rep)
         info.update(stripe_choice=("model (flearn_amd.dist.plan_shards: stripes + replicated tail), coefficients "
@@ -436,7 +455,8 @@ def run_job(cfg, layout, n, args, world, rank, dev, g_eff):
     info["replicated_cols"] = plan.rep
     if world > 1 and args.stripes:
         info["gather"] = "push" if args.gather == "push" else "rccl"
-    job = Job(cfg, layout, n, plan, dev, world, args.reorder, push=info.get("gather") == "push")
+    job = Job(cfg, layout, n, plan, dev, world, args.reorder, push=info.get("gather") == "push",
+              push_grid=info.get("push_grid") or 0)
     for _ in range(args.warmup):
         job.red.step()
     torch.cuda.synchronize(dev)

@@ -618,13 +618,14 @@ class Packer:
                 for j in range(min(ahead, len(aps))):
                     started.append((j, aps[j].start(lst)))
                 for j, (lo, hi) in enumerate(bounds):
-                    _, h = started.popleft()
+                    _, h = started[0]
                     if h is None:  # a value off the plan in this chunk: the _NativeRows / Python pack
                         fill_rows(lo, hi)
                         path = "mixed"
                     else:
                         aps[j].wait(h, 0)
                         aps[j].end(h)
+                    started.popleft()  # only once its copies are done (the finally ends the rest)
                     ship(lo, hi)
                     if j + ahead < len(aps):
                         started.append((j + ahead, aps[j + ahead].start(lst)))

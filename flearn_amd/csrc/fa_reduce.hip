@@ -735,6 +735,10 @@ int fa_copy(void* dst, const void* src, int64_t nbytes, void* stream) {
   return launch_check();
 }
 
+// fa_push's default grid: enough 16-B stores in flight for the links (tools/overlap_probe.py
+// pushhost<B> on one GPU: see DESIGN.md section 6), few enough to leave the reduce its CUs
+constexpr int64_t kPushGrid = 64;
+
 int fa_ipc_handle(const void* ptr, void* handle, int64_t* offset) {
   if (!ptr || !handle || !offset) return fail(FA_ERR_ARG, "null ipc argument");
   static_assert(sizeof(hipIpcMemHandle_t) == FA_IPC_HANDLE_BYTES, "IPC handle size");
@@ -766,8 +770,8 @@ int fa_ipc_close(void* base) {
   return FA_OK;
 }
 
-int fa_push(const void* src, int64_t nbytes, void* const* dsts, int32_t n_dsts, void* stream) {
-  if (nbytes < 0 || n_dsts < 0 || n_dsts > 8) return fail(FA_ERR_ARG, "bad push size or destination count");
+int fa_push(const void* src, int64_t nbytes, void* const* dsts, int32_t n_dsts, int32_t grid, void* stream) {
+  if (nbytes < 0 || n_dsts < 0 || n_dsts > 8 || grid < 0) return fail(FA_ERR_ARG, "bad push size, destination count or grid");
   if (nbytes == 0 || n_dsts == 0) return FA_OK;
   if (!src || !dsts) return fail(FA_ERR_ARG, "null push pointer");
   PushDsts d{};
@@ -780,7 +784,8 @@ int fa_push(const void* src, int64_t nbytes, void* const* dsts, int32_t n_dsts, 
   if ((any & 15) || (nbytes & 15)) return fail(FA_ERR_ALIGN, "push pointers and size must be 16-byte multiples");
   const int64_t quads = nbytes / 16;
   int64_t blocks = (quads + kThreads - 1) / kThreads;
-  if (blocks > 1024) blocks = 1024;
+  const int64_t cap = grid > 0 ? grid : kPushGrid;
+  if (blocks > cap) blocks = cap;
   hipLaunchKernelGGL(push_kernel, dim3((unsigned)blocks), dim3(kThreads), 0, static_cast<hipStream_t>(stream),
                      static_cast<const uint8_t*>(src), quads, d, n_dsts);
   return launch_check();

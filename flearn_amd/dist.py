@@ -123,6 +123,7 @@ class PushGather:
                                + (f" (here: {err.decode(errors='replace')})" if err and not ok else ""))
         self.stream = torch.cuda.Stream(self.device)
         self.flag = torch.zeros(1, dtype=torch.float32, device=self.device)
+        self.grid = 0  # fa_push blocks (0: the library's default)
 
     def _all_ok(self, ok: int) -> bool:
         t = torch.tensor([ok], dtype=torch.int32, device=self.device if self.nccl else "cpu")
@@ -151,7 +152,8 @@ class PushGather:
             raise ValueError("push outside the receive buffer")
         self.stream.wait_stream(torch.cuda.current_stream(self.device))
         dsts = (ctypes.c_void_p * self.world)(*[d + off for d in self.dst])
-        self.na.check(self.L.fa_push(src.data_ptr(), n, dsts, self.world, self.stream.cuda_stream), "fa_push")
+        self.na.check(self.L.fa_push(src.data_ptr(), n, dsts, self.world, self.grid, self.stream.cuda_stream),
+                      "fa_push")
 
     def end(self):
         self._barrier()
@@ -482,7 +484,7 @@ class ShardedReducer:
     """
 
     def __init__(self, plan: ShardPlan, reduce_fn, device, group=None, local_out=None, gather=None, state=None,
-                 push: bool = False):
+                 push: bool = False, push_grid: int = 0):
         self.plan = plan
         self.reduce_fn = reduce_fn
         self.device = torch.device(device)
@@ -505,6 +507,8 @@ class ShardedReducer:
         # push=True: reassemble with direct peer stores (PushGather) instead of RCCL's all-gather;
         # raises RuntimeError on every rank when some rank cannot map its peers
         self.pusher = PushGather(self.full, group) if self.gather and push else None
+        if self.pusher is not None:
+            self.pusher.grid = push_grid
 
     def release(self):
         """Collective when pushing: unmap the peers' buffers before any rank frees its own."""

@@ -155,15 +155,16 @@ def test_push_and_ipc_validation(L):
     an empty push touches nothing.  fa_ipc_*: null arguments refused before any HIP call."""
     P = ctypes.c_void_p
     dsts = (P * 9)(*([FAKE] * 9))
-    assert L.fa_push(FAKE, 64, dsts, 9, None) == header_define("FA_ERR_ARG")
-    assert L.fa_push(FAKE, 64, dsts, -1, None) == header_define("FA_ERR_ARG")
-    assert L.fa_push(FAKE, -16, dsts, 2, None) == header_define("FA_ERR_ARG")
-    assert L.fa_push(FAKE, 0, dsts, 2, None) == 0
-    assert L.fa_push(FAKE, 64, dsts, 0, None) == 0
-    assert L.fa_push(FAKE + 8, 64, dsts, 2, None) == header_define("FA_ERR_ALIGN")
-    assert L.fa_push(FAKE, 72, dsts, 2, None) == header_define("FA_ERR_ALIGN")
+    assert L.fa_push(FAKE, 64, dsts, 9, 0, None) == header_define("FA_ERR_ARG")
+    assert L.fa_push(FAKE, 64, dsts, -1, 0, None) == header_define("FA_ERR_ARG")
+    assert L.fa_push(FAKE, -16, dsts, 2, 0, None) == header_define("FA_ERR_ARG")
+    assert L.fa_push(FAKE, 0, dsts, 2, 0, None) == 0
+    assert L.fa_push(FAKE, 64, dsts, 0, 0, None) == 0
+    assert L.fa_push(FAKE + 8, 64, dsts, 2, 0, None) == header_define("FA_ERR_ALIGN")
+    assert L.fa_push(FAKE, 72, dsts, 2, 0, None) == header_define("FA_ERR_ALIGN")
     bad = (P * 2)(FAKE, None)
-    assert L.fa_push(FAKE, 64, bad, 2, None) == header_define("FA_ERR_ARG")
+    assert L.fa_push(FAKE, 64, bad, 2, 0, None)
+    assert L.fa_push(FAKE, 64, dsts, 2, -1, None) == header_define("FA_ERR_ARG") == header_define("FA_ERR_ARG")
     off = ctypes.c_int64()
     assert L.fa_ipc_handle(None, ctypes.create_string_buffer(64), ctypes.byref(off)) == header_define("FA_ERR_ARG")
     assert L.fa_ipc_open(None, ctypes.byref(P())) == header_define("FA_ERR_ARG")

@@ -83,6 +83,7 @@ def main():
     spin_out = torch.empty(256 * 256, dtype=torch.float32, device=dev)
 
     sink = torch.empty(4096 * 256 * 4, dtype=torch.int32, device=dev)
+    host_dst = None
 
     def copy_fn(kind):
         if kind.startswith("rd"):  # HBM reads only
@@ -109,6 +110,19 @@ def main():
             def f():
                 assert L.probe_copy_rep(small_dst.data_ptr(), small.data_ptr(), small.numel() // 4, blocks, 64,
                                         sb.cuda_stream) == 0
+            return f
+        if kind.startswith("pushhost"):  # fa_push into pinned host memory: a LINK-bound push kernel (PCIe
+            # standing in for an xGMI link), which reads its source once from local HBM and
+            # writes nothing to it — the sender's side of the one-shot push gather
+            nonlocal host_dst
+            if host_dst is None:
+                host_dst = torch.empty(nbytes // 4, dtype=torch.float32, pin_memory=True)
+            Lf = na.lib()
+            dsts = (ctypes.c_void_p * 1)(host_dst.data_ptr())
+            pgrid = int(kind[8:] or 0)  # pushhost<B>: B blocks (none: the library's default)
+
+            def f():
+                assert Lf.fa_push(src.data_ptr(), nbytes, dsts, 1, pgrid, sb.cuda_stream) == 0
             return f
         if kind == "dma":
             def f():

@@ -61,6 +61,26 @@ def contention(ingress_bs: float, paths=OVERLAP, local_traffic: float = 2.0):
     return c_r, c_g, f"copy on {k} blocks ({rate / 1e9:.0f} GB/s)"
 
 
+PUSH_PROBE = REPO / "profiles" / "r04" / "overlap" / "overlap_push.json"
+
+
+def push_contention(ingress_bs: float, path=PUSH_PROBE):
+    """(c_r, c_g, stand-in) of the one-shot push from the one-GPU probe: the sender's push kernel
+    (pushhost<B>: a link-bound fa_push into pinned memory over PCIe, at the smallest grid that
+    reaches 95% of its best rate) slows the reduce and is slowed by it; the peers' stores landing
+    in this GPU's HBM act like a write-only stream at the ingress rate (wr<B>: the first one at
+    or above it).  The two reduce terms add."""
+    d = json.loads(Path(path).read_text())
+    w = next(r for r in d["rows"] if r["grid"] == "default")["with"]
+    ph = sorted((int(k[8:]), v) for k, v in w.items() if k.startswith("pushhost") and k[8:])
+    top = max(v["copy_alone_gbs"] for _, v in ph)
+    b, v = next((b, v) for b, v in ph if v["copy_alone_gbs"] >= 0.95 * top)
+    wr = sorted((v["copy_alone_gbs"] * 1e9, v) for k, v in w.items() if k.startswith("wr"))
+    rate, wv = next(((r, v) for r, v in wr if r >= ingress_bs), wr[-1])
+    c_r = (v["reduce_slowdown"] - 1.0) + (wv["reduce_slowdown"] - 1.0)
+    return c_r, v["copy_slowdown"] - 1.0, f"push on {b} blocks + writes at {rate / 1e9:.0f} GB/s"
+
+
 def project(cfg: str, g: int, link_bs: float, launch_s=10e-6, collective_s=30e-6, tail=True, contended=False,
             push=False, barrier_s=15e-6):
     """push: the one-shot push gather (flearn_amd.dist.PushGather) — a launch per stripe instead
@@ -76,7 +96,8 @@ def project(cfg: str, g: int, link_bs: float, launch_s=10e-6, collective_s=30e-6
     m = StripeModel(launch_s, b_r, a_g, b_g)
     stand_in = None
     if contended and g > 1:
-        c_r, c_g, stand_in = contention((g - 1) * link_bs, local_traffic=(1.0 + 1.0 / (g - 1)) if push else 2.0)
+        c_r, c_g, stand_in = (push_contention((g - 1) * link_bs) if push else
+                              contention((g - 1) * link_bs))
         m = m.with_contention(c_r, c_g)
     if g == 1:
         widths, rep = (local,), 0
