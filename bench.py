@@ -258,9 +258,10 @@ def calibrate(job: Job, world: int, dev, reps: int = 5):
 
 
 PUSH_GRIDS = (16, 32, 64, 128, 256)
+PUSH_MODE = {"push": "kernel", "push_dma": "dma"}  # --gather name -> PushGather mode
 
 
-def calibrate_push(job: Job, world: int, dev, r_big: float, reps: int = 5):
+def calibrate_push(job: Job, world: int, dev, r_big: float, reps: int = 5, mode: str = "kernel"):
     """The one-shot push all-gather (fa_dist.PushGather) on the running job: availability (every
     rank maps its peers' buffers), a bit-compare against RCCL's all-gather of the same slices, the
     gather of the whole local width and of 1/8 of it, and its contention with the reduce.
@@ -271,7 +272,7 @@ def calibrate_push(job: Job, world: int, dev, r_big: float, reps: int = 5):
     out = job.red.local_out
     full = torch.empty(world * big, dtype=torch.float32, device=dev)
     try:
-        pg = fa_dist.PushGather(full)
+        pg = fa_dist.PushGather(full, mode=mode)
     except RuntimeError as e:
         return None, {"available": False, "reason": str(e)}
     try:
@@ -292,13 +293,14 @@ def calibrate_push(job: Job, world: int, dev, r_big: float, reps: int = 5):
         # blocks keep more stores in flight for the links but take the memory pipeline from the
         # reduce beside it: DESIGN.md section 6)
         by_grid = {}
-        for g in PUSH_GRIDS:
+        for g in (PUSH_GRIDS if mode == "kernel" else ()):
             pg.grid = g
             by_grid[g] = _event_time(lambda: pg.gather(out[:big], p.rank * big), 3)
-        times = _max_over_ranks(list(by_grid.values()), world, dev)
-        by_grid = dict(zip(PUSH_GRIDS, times))
-        best = min(times)
-        pg.grid = min(g for g, t in by_grid.items() if t <= 1.03 * best)
+        if by_grid:
+            times = _max_over_ranks(list(by_grid.values()), world, dev)
+            by_grid = dict(zip(PUSH_GRIDS, times))
+            best = min(times)
+            pg.grid = min(g for g, t in by_grid.items() if t <= 1.03 * best)
         g_big = _event_time(lambda: pg.gather(out[:big], p.rank * big), reps)
         g_small = _event_time(lambda: pg.gather(out[:small], p.rank * small), reps)
         r_conc, g_conc, g_alone = _contention_push(job, pg, out, big, dev, reps)
@@ -309,7 +311,7 @@ def calibrate_push(job: Job, world: int, dev, r_big: float, reps: int = 5):
     g_big, g_small, r_conc, g_conc, g_alone, r_small = _max_over_ranks(
         (g_big, g_small, r_conc, g_conc, g_alone, r_small), world, dev)
     c_r, c_g = max(r_conc / r_big - 1.0, 0.0), max(g_conc / max(g_alone, 1e-9) - 1.0, 0.0)
-    cal = dict(available=True, checked_against_rccl=True, width_cols=[big, small], grid=grid,
+    cal = dict(available=True, mode=mode, checked_against_rccl=True, width_cols=[big, small], grid=grid,
                gather_us_by_grid={str(g): round(t * 1e6, 2) for g, t in by_grid.items()},
                gather_us=[round(g_big * 1e6, 2), round(g_small * 1e6, 2)],
                push_kernel_us=round(g_alone * 1e6, 2), concurrent_reduce_us=round(r_conc * 1e6, 2),
@@ -347,6 +349,7 @@ def _contention_push(job, pg, out, cols, dev, reps: int):
                     job.fn(0, cols, out2[:cols])
             e2.record(pg.stream)
             pg.push(src, off)
+            pg.join()
             e3.record(pg.stream)
             pg.end()
             cur.wait_stream(side)
@@ -409,13 +412,18 @@ def run_job(cfg, layout, n, args, world, rank, dev, g_eff):
             probe.reduce_only()
         model, cal = calibrate(probe, world, dev)
         push_grid = 0
-        models = {"rccl": model} if args.gather != "push" else {}
+        models = {"rccl": model} if args.gather in ("auto", "rccl") else {}
         if world > 1 and args.gather != "rccl":
-            m_push, cal_push = calibrate_push(probe, world, dev, cal["reduce_us"][0] * 1e-6)
-            info["push_calibration"] = cal_push
-            push_grid = cal_push.get("grid", 0)
-            if m_push is not None:
-                models["push"] = m_push
+            # the one-shot push, by kernel stores (fa_push) and by copy engines (one per peer)
+            for g_name, mode, key in (("push", "kernel", "push_calibration"), ("push_dma", "dma", "push_dma_calibration")):
+                if args.gather not in ("auto", g_name):
+                    continue
+                m_push, cal_push = calibrate_push(probe, world, dev, cal["reduce_us"][0] * 1e-6, mode=mode)
+                info[key] = cal_push
+                if m_push is not None:
+                    models[g_name] = m_push
+                    if mode == "kernel":
+                        push_grid = cal_push.get("grid", 0)
         if not models:  # --gather push, but pushing is not available here
             models = {"rccl": model}
         probe.release()
@@ -427,7 +435,7 @@ def run_job(cfg, layout, n, args, world, rank, dev, g_eff):
             # (real collectives; max over ranks, so every rank picks the same plan)
             for g, w_c, r_c in cands:
                 tj = Job(cfg, layout, n, ShardPlan.from_widths(p_real, g_eff, rank, w_c, rep=r_c), dev, world,
-                         args.reorder, push=g == "push", push_grid=push_grid)
+                         args.reorder, push=PUSH_MODE.get(g, False), push_grid=push_grid)
                 for _ in range(2):
                     tj.red.step()
                 t = _max_over_ranks((_event_time(tj.red.step, 5),), world, dev)[0]
@@ -454,8 +462,8 @@ def run_job(cfg, layout, n, args, world, rank, dev, g_eff):
     # columns every rank reduces itself (no gather): redundant work, counted once in `value`
     info["replicated_cols"] = plan.rep
     if world > 1 and args.stripes:
-        info["gather"] = "push" if args.gather == "push" else "rccl"
-    job = Job(cfg, layout, n, plan, dev, world, args.reorder, push=info.get("gather") == "push",
+        info["gather"] = args.gather if args.gather != "auto" else "rccl"
+    job = Job(cfg, layout, n, plan, dev, world, args.reorder, push=PUSH_MODE.get(info.get("gather"), False),
               push_grid=info.get("push_grid") or 0)
     for _ in range(args.warmup):
         job.red.step()
@@ -665,9 +673,10 @@ def main():
     ap.add_argument("--reorder", action="store_true",
                     help="allow the split-N kernel (deterministic, <= 1e-6 normwise, not bit-exact)")
     ap.add_argument("--no-verify", action="store_true", help="skip the post-run check of the reassembled model")
-    ap.add_argument("--gather", choices=("auto", "rccl", "push"), default="auto",
+    ap.add_argument("--gather", choices=("auto", "rccl", "push", "push_dma"), default="auto",
                     help="N>1: how stripes are reassembled — RCCL's all-gather, the one-shot push over "
-                         "xGMI (peer stores, flearn_amd.dist.PushGather), or whichever measures faster")
+                         "xGMI by kernel stores or by copy engines (flearn_amd.dist.PushGather), or "
+                         "whichever measures fastest")
     ap.add_argument("--no-loopback", action="store_true",
                     help="N>1: skip the single-process AVG(devices=[...]) loopback measurement")
     args = ap.parse_args()
@@ -826,8 +835,9 @@ def main():
                           else "reference client order (bit-exact)"),
                 "parallelism": ("single GPU" if g_eff == 1 else
                                 f"element-range shards x{g_eff} + "
-                                + ("one-shot push all-gather over xGMI (peer stores)" if info.get("gather") == "push"
-                                   else "RCCL all-gather") + f" ({plan.stripes} stripes"
+                                + {"push": "one-shot push all-gather over xGMI (peer stores)",
+                                   "push_dma": "one-shot push all-gather over xGMI (copy engines, one per peer)"}.get(
+                                       info.get("gather"), "RCCL all-gather") + f" ({plan.stripes} stripes"
                                 + (f", widths {'/'.join(str(x) for x in plan.widths)}" if plan.stripes > 1
                                    else "")
                                 + (f"; the last {plan.rep} columns reduced by every rank, not gathered"

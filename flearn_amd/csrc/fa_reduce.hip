@@ -791,6 +791,15 @@ int fa_push(const void* src, int64_t nbytes, void* const* dsts, int32_t n_dsts, 
   return launch_check();
 }
 
+int fa_copy_dma(void* dst, const void* src, int64_t nbytes, void* stream) {
+  if (nbytes < 0) return fail(FA_ERR_ARG, "negative copy size");
+  if (nbytes == 0) return FA_OK;
+  if (!dst || !src) return fail(FA_ERR_ARG, "null copy pointer");
+  const hipError_t e = hipMemcpyAsync(dst, src, (size_t)nbytes, hipMemcpyDeviceToDevice, static_cast<hipStream_t>(stream));
+  if (e != hipSuccess) return fail(FA_ERR_LAUNCH, hipGetErrorString(e));
+  return FA_OK;
+}
+
 int fa_fill_uniform_f32(float* dst, int64_t row_stride, int32_t n_rows, int64_t n_cols,
                         uint64_t seed, int64_t row_begin, int64_t col_global_begin, void* stream) {
   if (!dst || n_rows < 0 || n_cols < 0 || row_stride < n_cols) return fail(FA_ERR_ARG, "bad fill");

@@ -82,9 +82,12 @@ class PushGather:
     Construction is collective and all-or-nothing: if any rank cannot map a peer, every rank
     raises RuntimeError (nothing stays mapped) and the caller keeps RCCL's all-gather."""
 
-    def __init__(self, full: torch.Tensor, group=None):
+    def __init__(self, full: torch.Tensor, group=None, mode: str = "kernel"):
         from . import _native as na
 
+        if mode not in ("kernel", "dma"):
+            raise ValueError(f"PushGather mode {mode!r}")
+        self.mode = mode
         self.na, self.L = na, na.lib()
         self.full, self.group = full, group
         self.world, self.rank = dist.get_world_size(group), dist.get_rank(group)
@@ -124,6 +127,10 @@ class PushGather:
         self.stream = torch.cuda.Stream(self.device)
         self.flag = torch.zeros(1, dtype=torch.float32, device=self.device)
         self.grid = 0  # fa_push blocks (0: the library's default)
+        # mode "dma": one stream per peer, each leg a copy-engine copy (fa_copy_dma) — copies on
+        # one stream would run one after the other, one link at a time
+        self.peer_streams = ([torch.cuda.Stream(self.device) for _ in range(self.world - 1)] if mode == "dma"
+                             else [])
 
     def _all_ok(self, ok: int) -> bool:
         t = torch.tensor([ok], dtype=torch.int32, device=self.device if self.nccl else "cpu")
@@ -150,12 +157,28 @@ class PushGather:
         off = elem_offset * self.full.element_size()
         if elem_offset < 0 or off + n > self.full.numel() * self.full.element_size():
             raise ValueError("push outside the receive buffer")
-        self.stream.wait_stream(torch.cuda.current_stream(self.device))
-        dsts = (ctypes.c_void_p * self.world)(*[d + off for d in self.dst])
-        self.na.check(self.L.fa_push(src.data_ptr(), n, dsts, self.world, self.grid, self.stream.cuda_stream),
-                      "fa_push")
+        cur = torch.cuda.current_stream(self.device)
+        self.stream.wait_stream(cur)
+        if self.mode == "kernel":
+            dsts = (ctypes.c_void_p * self.world)(*[d + off for d in self.dst])
+            self.na.check(self.L.fa_push(src.data_ptr(), n, dsts, self.world, self.grid, self.stream.cuda_stream),
+                          "fa_push")
+            return
+        # copy engines: the peers' legs on their own streams (after the step's barrier and the
+        # stripe's reduce), this rank's own copy by a kernel on the pusher's stream
+        peers = [d for r, d in enumerate(self.dst) if r != self.rank]
+        for s, d in zip(self.peer_streams, peers):
+            s.wait_stream(self.stream)
+            self.na.check(self.L.fa_copy_dma(d + off, src.data_ptr(), n, s.cuda_stream), "fa_copy_dma")
+        self.na.check(self.L.fa_copy(self.dst[self.rank] + off, src.data_ptr(), n, self.stream.cuda_stream), "fa_copy")
+
+    def join(self):
+        """The pusher's stream waits for the copy-engine legs (mode "dma")."""
+        for s in self.peer_streams:
+            self.stream.wait_stream(s)
 
     def end(self):
+        self.join()
         self._barrier()
         torch.cuda.current_stream(self.device).wait_stream(self.stream)
 
@@ -484,7 +507,7 @@ class ShardedReducer:
     """
 
     def __init__(self, plan: ShardPlan, reduce_fn, device, group=None, local_out=None, gather=None, state=None,
-                 push: bool = False, push_grid: int = 0):
+                 push: bool | str = False, push_grid: int = 0):
         self.plan = plan
         self.reduce_fn = reduce_fn
         self.device = torch.device(device)
@@ -506,7 +529,9 @@ class ShardedReducer:
                      else None)
         # push=True: reassemble with direct peer stores (PushGather) instead of RCCL's all-gather;
         # raises RuntimeError on every rank when some rank cannot map its peers
-        self.pusher = PushGather(self.full, group) if self.gather and push else None
+        # push: False (RCCL's all-gather), True / "kernel" (fa_push stores) or "dma" (copy engines)
+        self.pusher = (PushGather(self.full, group, mode="dma" if push == "dma" else "kernel")
+                       if self.gather and push else None)
         if self.pusher is not None:
             self.pusher.grid = push_grid
 

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define FA_ABI_VERSION 10
+#define FA_ABI_VERSION 11
 
 /* return codes */
 #define FA_OK 0
@@ -253,6 +253,12 @@ int fa_ipc_close(void* base);
  * the links and leaves the CUs' memory pipelines to a reduce running beside it (a link-bound push
  * on 1024 blocks slowed the reduce 1.8x on one GPU).  ABI 10 adds `grid`. */
 int fa_push(const void* src, int64_t nbytes, void* const* dsts, int32_t n_dsts, int32_t grid, void* stream);
+
+/* hipMemcpyAsync(dst, src, nbytes, device-to-device) on `stream`: between two GPUs' memories
+ * (a peer bucket mapped with fa_ipc_open) the runtime drives it with a copy engine, so a push
+ * leg costs the reduce no CUs and no memory-pipeline slots (the copy-engine form of the one-shot
+ * all-gather: one stream per peer).  ABI 11.                                                  */
+int fa_copy_dma(void* dst, const void* src, int64_t nbytes, void* stream);
 
 /* ---- wire codec (HOST functions: every pointer below is host memory) -------------------------
  * flearn's HTTP mode ships uploads and global models as base64(pickle.dumps(obj))

@@ -231,11 +231,12 @@ def case_sharded_reducer(rank, world):
                 assert full.tobytes() == want.astype(np.float32).tobytes(), (rank, plan.widths, op, step)
 
 
-def case_sharded_reducer_push(rank, world):
+def case_sharded_reducer_push(rank, world, mode="kernel"):
     """The same ShardedReducer steps reassembled by PushGather (direct peer stores through
-    IPC-mapped receive buffers, fa_push) instead of the all-gather: every rank's model equals the
-    C oracle's bit for bit; plus one PushGather.gather of a rank-stamped slice against
-    all_gather_into, and a push outside the receive buffer refused."""
+    IPC-mapped receive buffers: fa_push, or copy engines with mode "dma") instead of the
+    all-gather: every rank's model equals the C oracle's bit for bit; plus one PushGather.gather
+    of a rank-stamped slice against all_gather_into, and a push outside the receive buffer
+    refused."""
     import oracle
     from flearn_amd import _native as na
     from flearn_amd import aggregator as agg
@@ -244,7 +245,7 @@ def case_sharded_reducer_push(rank, world):
 
     cuda = torch.device("cuda", 0)
     full = torch.full((world * 4096,), -1.0, device=cuda)
-    pg = PushGather(full, None)
+    pg = PushGather(full, None, mode=mode)
     src = torch.arange(4096, dtype=torch.float32, device=cuda) + 10000.0 * rank
     pg.gather(src, rank * 4096)
     want = torch.empty_like(full)
@@ -282,7 +283,7 @@ def case_sharded_reducer_push(rank, world):
                            v=torch.zeros(plan.local_stride, dtype=torch.float64, device=cuda))
                 local_out = prev[0]
             red = ShardedReducer(plan, hip_reduce_fn(stack, w, na.MODE_W32_DIV64, denom, **epi), cuda,
-                                 local_out=local_out, gather=True, push=True)
+                                 local_out=local_out, gather=True, push="dma" if mode == "dma" else True)
             assert red.pusher is not None
             want = want_mean.copy()
             prev_h = oracle.fill_uniform(1, p, 4)[0]
@@ -296,9 +297,13 @@ def case_sharded_reducer_push(rank, world):
             red.release()
 
 
+def case_sharded_reducer_push_dma(rank, world):
+    case_sharded_reducer_push(rank, world, mode="dma")
+
+
 CASES = {f.__name__[5:]: f for f in (case_avg_fixtures, case_setup_strategy, case_fused_rounds,
                                       case_first_round_adopt, case_empty_ranks, case_dyn, case_sharded_reducer,
-                                      case_sharded_reducer_push)}
+                                      case_sharded_reducer_push, case_sharded_reducer_push_dma)}
 
 
 def rank_main(rank, world, port, names):

@@ -170,6 +170,9 @@ def test_push_and_ipc_validation(L):
     assert L.fa_ipc_open(None, ctypes.byref(P())) == header_define("FA_ERR_ARG")
     assert L.fa_ipc_close(None) == header_define("FA_ERR_ARG")
     assert header_define("FA_IPC_HANDLE_BYTES") == 64
+    assert L.fa_copy_dma(FAKE, FAKE, -1, None) == header_define("FA_ERR_ARG")
+    assert L.fa_copy_dma(None, FAKE, 64, None) == header_define("FA_ERR_ARG")
+    assert L.fa_copy_dma(None, None, 0, None) == 0
 
 
 def test_piece_struct_layout_matches_c(tmp_path):

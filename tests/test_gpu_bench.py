@@ -50,10 +50,12 @@ def test_bench_two_ranks_rehearsal(config, cuda):
     assert cal["c_r"] >= 0 and cal["c_g"] >= 0 and cal["concurrent_reduce_us"] > 0
     # the one-shot push gather was set up (IPC-mapped peer buffers: here two processes on one
     # GPU), checked bit for bit against the all-gather, calibrated, and timed in the trials
-    pc = mg["push_calibration"]
-    assert pc["available"] is True and pc["checked_against_rccl"] is True and pc["push_kernel_us"] > 0
-    assert {t["gather"] for t in mg["plan_trials"]} == {"rccl", "push"}
-    used = cal if mg["gather"] == "rccl" else pc
+    pc, pd = mg["push_calibration"], mg["push_dma_calibration"]
+    for c in (pc, pd):
+        assert c["available"] is True and c["checked_against_rccl"] is True and c["push_kernel_us"] > 0
+    assert pc["grid"] in (16, 32, 64, 128, 256) and set(pc["gather_us_by_grid"]) == {"16", "32", "64", "128", "256"}
+    assert {t["gather"] for t in mg["plan_trials"]} == {"rccl", "push", "push_dma"}
+    used = {"rccl": cal, "push": pc, "push_dma": pd}[mg["gather"]]
     assert mg["model"]["c_r"] == used["c_r"] and mg["model"]["c_g"] == used["c_g"]
     # the serial plan (one stripe, no tail) is among the measured trials
     assert any(len(t["stripe_widths"]) == 1 and t["replicated_cols"] == 0 for t in mg["plan_trials"])
@@ -88,11 +90,12 @@ def test_bench_two_ranks_rehearsal(config, cuda):
 def test_bench_push_gather_is_verified(cuda):
     """--gather push --stripes 3: every stripe reassembled by direct peer stores; the line says so
     and its self-check passes on both ranks."""
-    p = _rehearse("c3", ("--no-weak", "--no-loopback", "--stripes", "3", "--gather", "push"))
-    assert p.returncode == 0, p.stderr[-4000:]
-    d = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][0])
-    assert d["multi_gpu"]["gather"] == "push" and "push all-gather" in d["config"]["parallelism"]
-    assert d["verify"]["verified"] is True and d["verify"]["ranks_checked"] == 2
+    for g in ("push", "push_dma"):
+        p = _rehearse("c3", ("--no-weak", "--no-loopback", "--stripes", "3", "--gather", g))
+        assert p.returncode == 0, p.stderr[-4000:]
+        d = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][0])
+        assert d["multi_gpu"]["gather"] == g and "push all-gather" in d["config"]["parallelism"]
+        assert d["verify"]["verified"] is True and d["verify"]["ranks_checked"] == 2
 
 
 @pytest.mark.timeout(300)

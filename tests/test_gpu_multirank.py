@@ -77,5 +77,6 @@ def test_sharded_reducer_hip_ranks(world, cuda):
 @pytest.mark.parametrize("world", [2, 3])
 def test_sharded_reducer_push_gather(world, cuda):
     """ShardedReducer reassembled by PushGather: IPC-mapped peer buffers and one fa_push kernel
-    per stripe (here every "peer" is another process on the same GPU), bit-exact."""
-    _run_ranks(world, ["sharded_reducer_push"])
+    per stripe, or one copy-engine copy per peer (here every "peer" is another process on the
+    same GPU), bit-exact."""
+    _run_ranks(world, ["sharded_reducer_push", "sharded_reducer_push_dma"])
