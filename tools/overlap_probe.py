@@ -86,6 +86,7 @@ def main():
     host_dst = None
 
     def copy_fn(kind):
+        nonlocal host_dst
         if kind.startswith("rd"):  # HBM reads only
             blocks = int(kind[2:])
 
@@ -114,7 +115,6 @@ def main():
         if kind.startswith("pushhost"):  # fa_push into pinned host memory: a LINK-bound push kernel (PCIe
             # standing in for an xGMI link), which reads its source once from local HBM and
             # writes nothing to it — the sender's side of the one-shot push gather
-            nonlocal host_dst
             if host_dst is None:
                 host_dst = torch.empty(nbytes // 4, dtype=torch.float32, pin_memory=True)
             Lf = na.lib()
@@ -123,6 +123,15 @@ def main():
 
             def f():
                 assert Lf.fa_push(src.data_ptr(), nbytes, dsts, 1, pgrid, sb.cuda_stream) == 0
+            return f
+        if kind == "dmahost":  # a copy engine moving device memory to pinned host memory over PCIe:
+            # the sender's side of the copy-engine push (an SDMA leg over a link)
+            if host_dst is None:
+                host_dst = torch.empty(nbytes // 4, dtype=torch.float32, pin_memory=True)
+            Ld = na.lib()
+
+            def f():
+                assert Ld.fa_copy_dma(host_dst.data_ptr(), src.data_ptr(), nbytes, sb.cuda_stream) == 0
             return f
         if kind == "dma":
             def f():

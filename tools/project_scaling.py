@@ -62,6 +62,20 @@ def contention(ingress_bs: float, paths=OVERLAP, local_traffic: float = 2.0):
 
 
 PUSH_PROBE = REPO / "profiles" / "r04" / "overlap" / "overlap_push.json"
+PUSH_DMA_PROBE = REPO / "profiles" / "r04" / "overlap" / "overlap_push_dma.json"
+
+
+def push_dma_contention(ingress_bs: float, path=PUSH_DMA_PROBE, push_path=PUSH_PROBE):
+    """(c_r, c_g, stand-in) of the copy-engine push: the sender's legs are copy-engine transfers
+    over a link (dmahost: device -> pinned memory over PCIe), the receiver's HBM takes the peers'
+    stores like a write-only stream at the ingress rate (wr<B> from the push probe)."""
+    d = json.loads(Path(path).read_text())
+    v = next(r for r in d["rows"] if r["grid"] == "default")["with"]["dmahost"]
+    w = next(r for r in json.loads(Path(push_path).read_text())["rows"] if r["grid"] == "default")["with"]
+    wr = sorted((x["copy_alone_gbs"] * 1e9, x) for k, x in w.items() if k.startswith("wr"))
+    rate, wv = next(((r, x) for r, x in wr if r >= ingress_bs), wr[-1])
+    c_r = (v["reduce_slowdown"] - 1.0) + (wv["reduce_slowdown"] - 1.0)
+    return c_r, max(v["copy_slowdown"] - 1.0, 0.0), f"copy engine + writes at {rate / 1e9:.0f} GB/s"
 
 
 def push_contention(ingress_bs: float, path=PUSH_PROBE):
@@ -82,7 +96,7 @@ def push_contention(ingress_bs: float, path=PUSH_PROBE):
 
 
 def project(cfg: str, g: int, link_bs: float, launch_s=10e-6, collective_s=30e-6, tail=True, contended=False,
-            push=False, barrier_s=15e-6):
+            push=False, barrier_s=15e-6, dma=False):
     """push: the one-shot push gather (flearn_amd.dist.PushGather) — a launch per stripe instead
     of a collective, two barriers per step, and local HBM traffic of ingress * (1 + 1/(G-1))
     (received bytes written, the own slice read once) instead of a ring's ~2 x ingress."""
@@ -96,8 +110,8 @@ def project(cfg: str, g: int, link_bs: float, launch_s=10e-6, collective_s=30e-6
     m = StripeModel(launch_s, b_r, a_g, b_g)
     stand_in = None
     if contended and g > 1:
-        c_r, c_g, stand_in = (push_contention((g - 1) * link_bs) if push else
-                              contention((g - 1) * link_bs))
+        c_r, c_g, stand_in = (push_dma_contention((g - 1) * link_bs) if push and dma else
+                              push_contention((g - 1) * link_bs) if push else contention((g - 1) * link_bs))
         m = m.with_contention(c_r, c_g)
     if g == 1:
         widths, rep = (local,), 0
@@ -120,10 +134,11 @@ def main():
     ap.add_argument("--json", action="store_true")
     ap.add_argument("--no-tail", action="store_true", help="stripes only (no replicated tail)")
     ap.add_argument("--push", action="store_true", help="the one-shot push gather instead of RCCL's all-gather")
+    ap.add_argument("--dma", action="store_true", help="with --push: its copy-engine form (one leg per peer)")
     ap.add_argument("--contended", action="store_true",
                     help="reduce / gather slowed by the measured one-GPU contention (profiles/r04/overlap)")
     a = ap.parse_args()
-    rows = [project(c, g, float(l) * 1e9, tail=not a.no_tail, contended=a.contended, push=a.push)
+    rows = [project(c, g, float(l) * 1e9, tail=not a.no_tail, contended=a.contended, push=a.push, dma=a.dma)
             for l in a.link_gbs.split(",") for c in CONFIGS for g in (2, 4, 8)]
     if a.json:
         print(json.dumps(rows, indent=1))
