@@ -74,7 +74,7 @@ def test_sharded_reducer_hip_ranks(world, cuda):
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 4])
 def test_sharded_reducer_push_gather(world, cuda):
     """ShardedReducer reassembled by PushGather: IPC-mapped peer buffers and one fa_push kernel
     per stripe, or one copy-engine copy per peer (here every "peer" is another process on the
