@@ -715,6 +715,18 @@ def main():
             dst.copy_(torch.roll(dst, ALIGN))
 
         fa_dist.all_gather_into = late_gather
+    if os.environ.get("FLEARN_BENCH_INJECT") == "push_offset":
+        # rehearsal of a mis-placed push (tests/test_gpu_bench.py): every pushed slice lands ALIGN
+        # columns off — the self-check must catch it and the run fall back to RCCL's all-gather
+        real_push = fa_dist.PushGather.push
+
+        def off_push(self, src, elem_offset):
+            shifted = elem_offset + ALIGN
+            if shifted + src.numel() > self.full.numel():
+                shifted = elem_offset - ALIGN
+            return real_push(self, src, shifted)
+
+        fa_dist.PushGather.push = off_push
 
     cfg = CONFIGS[args.config]
     layout = layouts.get(cfg["layout"])
@@ -725,6 +737,28 @@ def main():
     main_n = strong_n if args.scaling == "strong" else weak_n
 
     job, step_s, wall, info = run_job(cfg, layout, main_n, args, world, rank, dev, g_eff)
+
+    def self_check(job):
+        log(f"[rank {rank}] verifying the reassembled model ...")
+        c = verify_job(job, cfg, world, dev, emulated=bool(emu))
+        if rank == 0:
+            log(f"[rank 0] verified={c['verified']} windows={c['windows']} mismatched={c['mismatched_windows']}")
+        return c
+
+    check = None
+    if not args.no_verify:
+        check = self_check(job)  # the verdict is shared by every rank
+        if not check["verified"] and world > 1 and info.get("gather") in PUSH_MODE:
+            # a push-reassembled bucket that fails its self-check: say so in the line, and time
+            # and verify the job again with RCCL's all-gather (never report the failed one)
+            failed = {"gather": info["gather"], "mismatched_windows": check["mismatched_windows"],
+                      "first_mismatches": check.get("first_mismatches")}
+            log(f"[rank {rank}] the {info['gather']} gather failed the self-check: re-running with RCCL")
+            job.release()
+            job, step_s, wall, info = run_job(cfg, layout, main_n, argparse.Namespace(**{**vars(args), "gather": "rccl"}),
+                                              world, rank, dev, g_eff)
+            info["push_failed_self_check"] = failed
+            check = self_check(job)
     plan = job.plan
     cols = plan.local_cols
     job_bytes = algorithmic_bytes(main_n, p_real, cfg["op"])
@@ -754,13 +788,6 @@ def main():
     if traffic_src:
         roofline["traffic_source"] = traffic_src
 
-    check = None
-    if not args.no_verify:
-        log(f"[rank {rank}] verifying the reassembled model ...")
-        check = verify_job(job, cfg, world, dev, emulated=bool(emu))
-        if rank == 0:
-            log(f"[rank 0] verified={check['verified']} windows={check['windows']} "
-                f"mismatched={check['mismatched_windows']}")
     if world > 1:
         info["world_size"] = dist.get_world_size()
         info["backend"] = dist.get_backend()

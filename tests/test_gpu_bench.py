@@ -99,6 +99,21 @@ def test_bench_push_gather_is_verified(cuda):
 
 
 @pytest.mark.timeout(300)
+def test_bench_falls_back_to_rccl_when_a_push_fails_its_check(cuda):
+    """FLEARN_BENCH_INJECT=push_offset with --gather push: the pushed bucket fails the self-check,
+    the line records it (`push_failed_self_check`) and the job is timed and verified again with
+    RCCL's all-gather, so the run still ends verified."""
+    p = _rehearse("c2", ("--no-weak", "--no-loopback", "--stripes", "2", "--gather", "push"), inject="push_offset")
+    assert p.returncode == 0, p.stderr[-4000:]
+    assert "failed the self-check: re-running with RCCL" in p.stderr
+    d = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][0])
+    mg = d["multi_gpu"]
+    assert mg["gather"] == "rccl" and mg["push_failed_self_check"]["gather"] == "push"
+    assert mg["push_failed_self_check"]["mismatched_windows"] > 0
+    assert d["verify"]["verified"] is True and "RCCL all-gather" in d["config"]["parallelism"]
+
+
+@pytest.mark.timeout(300)
 def test_bench_fails_on_a_misplaced_gather(cuda):
     """FLEARN_BENCH_INJECT=gather_offset: every gathered slice lands ALIGN columns late; the
     self-check must flag it in the line and the run must exit non-zero (EXIT_MISMATCH)."""
