@@ -643,7 +643,7 @@ class Packer:
         return "pool"
 
     def _async_rows(self, plan: BucketPlan, pieces, hosts, rows):
-        """([AsyncPack per chunk], [(lo, hi)]): chunks of rows that grow 1, 1, 2, 4, ... up to
+        """([AsyncPack per chunk], [(lo, hi)]): chunks of rows that grow 1, 2, 4, ... up to
         ~n/12 (the first DMA starts after one row is packed, ~0.5 ms for ResNet-18, where ~8
         equal chunks of a pool pack held it back by a whole chunk); each chunk's packed rows'
         pieces in row order.  Cached on the plan per staging address and wire-row pattern."""

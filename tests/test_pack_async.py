@@ -164,3 +164,43 @@ def test_worker_cap_still_copies_everything(threads):
     for _f, _e, _pl, _pg, g in chunks:
         for k, s, o, n in g:
             assert np.array_equal(gh[o : o + n], glob[k].reshape(-1)) and np.array_equal(lh[o : o + n], local[k].reshape(-1))
+
+
+@pytest.mark.parametrize("ndev,n,wire", [(1, 7, ()), (2, 5, ()), (3, 9, (0, 4, 8)), (1, 30, (3,))])
+def test_server_row_chunks_land_like_the_python_pack(ndev, n, wire):
+    """Packer._async_rows (the loopback server's native pack): every packed row's pieces land at
+    the bucket layout's offsets of its shard's staging row — checked on CPU staging against the
+    values themselves — chunk bounds grow 1, 2, 4, ... and cover every row once, and rows the
+    wire codec already holds (here: marked) are skipped."""
+    from flearn_amd.bucket import Packer, make_plan
+    from flearn_amd.semantics import KIND_F32
+
+    rng = np.random.default_rng(n)
+    shapes = {"a": (300, 7), "b": (5,), "c": (64, 64), "d": (3, 3, 3, 11), "e": (1,)}
+    ups = [{k: rng.standard_normal(s).astype(np.float32) for k, s in shapes.items()} for _ in range(n)]
+    plan = make_plan([1.0] * n, ups)
+    packer = Packer([torch.device("cpu")] * ndev)
+    g = plan.groups[KIND_F32]
+    shards = packer.shards(plan, KIND_F32)
+    assert len(shards) == ndev
+    pieces = packer._pieces(g, shards)
+    hosts = [torch.full((n, sh.width), -7.0) for sh in shards]
+    rows = [object() if r in wire else None for r in range(n)]
+    aps, bounds = packer._async_rows(plan, pieces, hosts, rows)
+    assert bounds[0] == (0, 1) and bounds[-1][1] == n
+    assert all(a[1] == b[0] for a, b in zip(bounds, bounds[1:]))
+    sizes = [hi - lo for lo, hi in bounds]
+    cap = max(1, -(-n // 12))
+    assert sizes[0] == 1 and max(sizes) <= cap and all(b >= a for a, b in zip(sizes[:-1], sizes[1:-1]))
+    for j, ap in enumerate(aps):
+        h = ap.start(ups)
+        assert h is not None
+        ap.wait(h, 0)
+        ap.end(h)
+    for r in range(n):
+        for s, a, b, sh, d in pieces:
+            got = hosts[sh.index][r, d : d + (b - a)].numpy()
+            if r in wire:
+                assert (got == -7.0).all()
+            else:
+                assert np.array_equal(got, ups[r][s.key].reshape(-1)[a:b]), (r, s.key, sh.index)
