@@ -610,6 +610,12 @@ class Aggregator:
     #: of an H2D copy, the launch and a D2H copy: C1 server call 141 -> 123 us on one box, same
     #: process, bit-equal (tools/prof_host_c1.py --ab, profiles/r03/c1_zc/); False = copy engines
     small_zero_copy = True
+    #: the zero-copy fp32 bucket of a small round may be summed in this many chained launches
+    #: (client parts, each launched as soon as native threads have packed it: bucket.AsyncPack);
+    #: 1 = one native pack on the calling thread, one launch.  At flearn's config 1 every extra
+    #: launch costs more than the overlap saves: 1 / 2 / 3 / 4 launches 113.5 / 120.3 / 127.4 /
+    #: 135.7 us per server call, numpy 142 us (tools/prof_host_c1.py --parts, profiles/r04/c1_parts/)
+    small_parts = 1
 
     def __init__(self, device=None, output: str = "reference", workers: int = 8, devices=None, group=None,
                  reorder: bool = False):
@@ -695,11 +701,11 @@ class Aggregator:
         and the ctypes arguments of its reduce launch, and the (key, offset, size, shape) list
         of the result.  None (cached as False) when the plan does not qualify."""
         zc = bool(self.small_zero_copy)
-        key = ("small_round", id(self.packer), str(self.device), self.output, zc)
+        key = ("small_round", id(self.packer), str(self.device), self.output, zc, int(self.small_parts))
         rec = plan.memo.get(key)
         if rec is not None:
             return rec or None
-        from .bucket import SMALL_BYTES, Packer, Shard, _NativeRows, _STORE, _TORCH
+        from .bucket import _FMT, SMALL_BYTES, AsyncPack, Packer, Shard, _NativeRows, _STORE, _TORCH
 
         n = plan.n_clients
         total = sum(n * g.stride * np.dtype(_STORE[k]).itemsize for k, g in plan.groups.items())
@@ -711,8 +717,9 @@ class Aggregator:
         for kind, g in plan.groups.items():
             tdt = _TORCH[_STORE[kind]]
             pieces = Packer._pieces(g, [Shard(0, dev, 0, g.stride)])
-            # one spare row: the split zero-copy round's partial sum (below)
-            host = torch.zeros((n + 1, g.stride), dtype=tdt, pin_memory=True)
+            # spare rows: the chained zero-copy round's partial sums (below)
+            parts = max(1, min(int(self.small_parts), n // 2))
+            host = torch.zeros((n + parts - 1, g.stride), dtype=tdt, pin_memory=True)
             if not _NativeRows.usable(pieces, [host]):
                 plan.memo[key] = False
                 return None
@@ -732,24 +739,8 @@ class Aggregator:
                 fn = L.fa_reduce_f32
                 args = (stack.data_ptr(), g.stride, n, nm.mode, w.data_ptr(), float(nm.denom), 0, g.stride, None,
                         None if f64 else dout.data_ptr(), dout.data_ptr() if f64 else None)
-                if zc and n >= 4 and nm.mode in (na.MODE_W32_DIV64, na.MODE_W32_DIV32):
-                    # two launches, so the second half is packed while the first is summed: clients
-                    # [0, h) sit in rows [0, h) and are summed in fp32 (W = 1: the epilogue returns
-                    # the sum itself) into row h, which that launch does not read; clients [h, n)
-                    # are packed one row down, into rows [h+1, n+1), and the second launch sums rows
-                    # [h, n+1) — the partial with weight fl32(1.0), then the rest: fl32(1 * acc) =
-                    # acc, so the chain of adds is the single launch's, bit for bit, and no launch
-                    # ever writes a row it reads
-                    h = n // 2
-                    row = g.stride * 4
-                    w_b = torch.cat([torch.ones(1, dtype=torch.float32, device=dev), w[h:]])
-                    part = host.data_ptr() + h * row
-                    args_a = (host.data_ptr(), g.stride, h, na.MODE_W32_DIV32, w.data_ptr(), 1.0, 0, g.stride, None,
-                              part, None)
-                    args_b = (part, g.stride, n - h + 1, nm.mode, w_b.data_ptr(), float(nm.denom), 0, g.stride, None,
-                              None if f64 else dout.data_ptr(), dout.data_ptr() if f64 else None)
-                    nat_b = _NativeRows(pieces, [host[1:]], w_local_lst, [None] * n)  # client i -> row i+1
-                    split = (h, args_a, args_b, w_b, nat_b)
+                if zc and parts >= 2 and nm.mode in (na.MODE_W32_DIV64, na.MODE_W32_DIV32):
+                    split = self._small_chain(g, pieces, host, w, nm, dout, f64, n, parts, dev, AsyncPack, _FMT)
             else:
                 fn = L.fa_reduce_f64 if kind == KIND_F64 else L.fa_reduce_i64
                 args = (stack.data_ptr(), g.stride, n, w.data_ptr(), float(nm.denom), 0, g.stride, dout.data_ptr())
@@ -759,6 +750,54 @@ class Aggregator:
         wsig = (tuple((s.key, s.shape, s.offset) for s in g32.segments) + (g32.stride,)) if g32 is not None else None
         rec = plan.memo[key] = (tuple(kinds), na.load_pyhost().fa_py_pack_rows, wsig)
         return rec
+
+    @staticmethod
+    def _small_chain(g, pieces, host, w, nm, dout, f64, n, parts, dev, AsyncPack, fmt_of):
+        """The fp32 bucket of a small zero-copy round as `parts` chained launches.  Clients are cut
+        into parts b_0 = 0 < b_1 < ... < b_K = n (the first smallest, so the GPU starts early);
+        client i of part k sits in staging row i + k.  Launch 0 sums rows [0, b_1) in fp32 (mode
+        W32_DIV32 with W = 1: the epilogue returns the sum itself) into row b_1; launch k sums
+        rows [b_k + k - 1, b_{k+1} + k) — the previous partial with weight fl32(1.0), then part
+        k's clients — into row b_{k+1} + k, the last one with the real denominator and output.
+        fl32(1 * acc) = acc, so the chain of adds is the single launch's, bit for bit, and no
+        launch writes a row it reads.  The parts are packed by native threads
+        (AsyncPack chunk k = part k) and each launch waits only for its own part.
+        Returns ("chain", AsyncPack, [launch args], [weight tensors kept alive])."""
+        base, rem = divmod(n, parts)
+        sizes = [base] * parts
+        for j in range(rem):  # the remainder goes to the last parts
+            sizes[parts - 1 - j] += 1
+        bounds = [0]
+        for s_ in sizes:
+            bounds.append(bounds[-1] + s_)
+        row = g.stride * 4
+        hp = host.data_ptr()
+        rows = []
+        for k in range(parts):
+            for i in range(bounds[k], bounds[k + 1]):
+                for s, a, b, _sh, d in pieces:
+                    it = s.src_dtype.itemsize
+                    rows.append((i, s.numel * it, fmt_of[s.src_dtype], hp + (i + k) * row + d * it, k, a * it,
+                                 (b - a) * it))
+        keys = tuple(s.key for s, *_ in pieces) * n
+        ap = AsyncPack(keys, np.array(rows, dtype=np.int64).reshape(-1, 7), parts)
+        one = torch.ones(1, dtype=torch.float32, device=dev)
+        args, ws = [], []
+        for k in range(parts):
+            lo, hi = bounds[k], bounds[k + 1]
+            if k == 0:
+                first, cnt, wk = hp, hi, w[:hi]
+            else:
+                first, cnt = hp + (lo + k - 1) * row, hi - lo + 1
+                wk = torch.cat([one, w[lo:hi]])
+            ws.append(wk)
+            if k < parts - 1:  # an fp32 partial into row hi + k
+                args.append((first, g.stride, cnt, na.MODE_W32_DIV32, wk.data_ptr(), 1.0, 0, g.stride, None,
+                             hp + (hi + k) * row, None))
+            else:
+                args.append((first, g.stride, cnt, nm.mode, wk.data_ptr(), float(nm.denom), 0, g.stride, None,
+                             None if f64 else dout.data_ptr(), dout.data_ptr() if f64 else None))
+        return ("chain", ap, args, ws)
 
     def _small_round(self, plan: BucketPlan, w_local_lst):
         """One small host round with no per-key Python: the uploads are packed natively into the
@@ -779,40 +818,38 @@ class Aggregator:
             if wire_row(lst[0], wsig) is not None:  # decoded by the wire codec into pinned rows of
                 return None                          # this layout: the general path DMAs them as is
         n = len(lst)
-        for nat, *rest in kinds:  # every bucket packed whole, except the split one's second half
-            split = rest[-1]
-            if pack(lst, nat.keys, len(nat.keys), nat.ptr, 0, split[0] if split else n) != 0:
+        for nat, *rest in kinds:  # every bucket packed here, except a chained one (native threads)
+            if rest[-1] is None and pack(lst, nat.keys, len(nat.keys), nat.ptr, 0, n) != 0:
                 return None
-        dev = self.device
-        if dev.index is not None and dev.index != torch.cuda.current_device():
-            with torch.cuda.device(dev):  # launches go to dev's stream from dev's context
-                parts = self._small_launch(kinds, pack, lst, n, dev)
-        else:
-            parts = self._small_launch(kinds, pack, lst, n, dev)
-        return None if parts is None else {k: parts[k] for k in plan.keys}
+        handles = {}
+        try:
+            for i, (nat, *rest) in enumerate(kinds):
+                if rest[-1] is not None:
+                    h = rest[-1][1].start(lst)
+                    if h is None:  # a value off the plan: nothing was copied, nothing launched
+                        return None
+                    handles[i] = h
+            dev = self.device
+            if dev.index is not None and dev.index != torch.cuda.current_device():
+                with torch.cuda.device(dev):  # launches go to dev's stream from dev's context
+                    parts = self._small_launch(kinds, handles, dev)
+            else:
+                parts = self._small_launch(kinds, handles, dev)
+        finally:
+            for i, h in handles.items():  # every copy done (and the values released)
+                kinds[i][-1][1].end(h)
+        return {k: parts[k] for k in plan.keys}
 
-    def _small_launch(self, kinds, pack, lst, n, dev):
-        """The queued part of _small_round: launches (and copies) on dev's current stream, one
-        synchronisation, the results as {key: value}; None when the split bucket's second half
-        cannot be packed natively (nothing left running)."""
+    def _small_launch(self, kinds, handles, dev):
+        """The queued part of _small_round: launches (and copies) on dev's current stream — a
+        chained bucket's launches each right after its part's copies are in — one
+        synchronisation, the results as {key: value}."""
         stream = torch.cuda.current_stream(dev)
         sh = stream.cuda_stream
-        for nat, host, stack, w, dout, hout, hnp, fn, args, out, split in kinds:
-            if split is not None:  # zero-copy in two launches: the second half packed meanwhile
-                h, args_a, args_b, _, nat_b = split
-                na.check(fn(*args_a, sh), fn.__name__)
-                if pack(lst, nat_b.keys, len(nat_b.keys), nat_b.ptr, h, n) != 0:
-                    stream.synchronize()  # the first launch must be done with the staging
-                    return None
-                na.check(fn(*args_b, sh), fn.__name__)
-                continue
-            if stack is host:  # zero-copy record
-                na.check(fn(*args, sh), fn.__name__)
-                continue
-            stack.copy_(host[: stack.shape[0]], non_blocking=True)
-            na.check(fn(*args, sh), fn.__name__)
-            hout.copy_(dout, non_blocking=True)
-        stream.synchronize()  # also: the staging may be rewritten by the next call
+        try:
+            self._small_enqueue(kinds, handles, stream, sh)
+        finally:
+            stream.synchronize()  # also: the staging may be rewritten by the next call
         parts = {}
         for nat, host, stack, w, dout, hout, hnp, fn, args, out, split in kinds:
             fresh = hnp.copy()
@@ -820,6 +857,21 @@ class Aggregator:
                 a = fresh[off : off + m].reshape(shape)
                 parts[k] = a.dtype.type(a[()]) if shape == () else a
         return parts
+
+    def _small_enqueue(self, kinds, handles, stream, sh):
+        for i, (nat, host, stack, w, dout, hout, hnp, fn, args, out, split) in enumerate(kinds):
+            if split is not None:  # chained zero-copy launches, each after its part is packed
+                _, ap, chain, _ws = split
+                for k, a in enumerate(chain):
+                    ap.wait(handles[i], k)
+                    na.check(fn(*a, sh), fn.__name__)
+                continue
+            if stack is host:  # zero-copy record
+                na.check(fn(*args, sh), fn.__name__)
+                continue
+            stack.copy_(host[: stack.shape[0]], non_blocking=True)
+            na.check(fn(*args, sh), fn.__name__)
+            hout.copy_(dout, non_blocking=True)
 
     def _gather_columns(self, plan: BucketPlan, parts):
         """Column-sharded group: every rank's reduced columns -> the whole f32 bucket on every

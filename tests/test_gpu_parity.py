@@ -1212,16 +1212,19 @@ def test_float64_model_with_int64_counters(weights, cuda):
     assert_dict_bitwise(got, want, f"f64 model, weights {type(weights[0]).__name__}")
 
 
-@pytest.mark.parametrize("zero_copy", [False, True])
-def test_small_round_fast_path_reuses_its_record_safely(zero_copy, cuda, monkeypatch):
+@pytest.mark.parametrize("zero_copy,parts", [(False, 4), (True, 1), (True, 2), (True, 4), (True, 5)])
+def test_small_round_fast_path_reuses_its_record_safely(zero_copy, parts, cuda, monkeypatch):
     """Small host rounds (every bucket < 4 MiB: flearn's config 1) take Aggregator._small_round:
     natively packed pinned staging, one H2D / launch / D2H per bucket (or, zero-copy, the kernel
-    reading the pinned staging and writing the pinned result over PCIe), one sync.  Round after
-    round with new values (the record's staging reused) and with a value the native pack refuses
-    (a non-contiguous view: the general path takes over) every result is bit-equal to the oracle."""
+    reading the pinned staging and writing the pinned result over PCIe — the fp32 bucket in
+    `parts` chained launches, each after native threads packed its clients), one sync.  Round
+    after round with new values (the record's staging reused) and with a value the native pack
+    refuses (a non-contiguous view in an early or a late part: the general path takes over,
+    nothing launched) every result is bit-equal to the oracle."""
     from flearn_amd.aggregator import Aggregator
 
     monkeypatch.setattr(Aggregator, "small_zero_copy", zero_copy)
+    monkeypatch.setattr(Aggregator, "small_parts", parts)
     layout = layouts.get("lenet5")
     p = layouts.fp32_elems(layout)
     s = AVG()
@@ -1239,7 +1242,7 @@ def test_small_round_fast_path_reuses_its_record_safely(zero_copy, cuda, monkeyp
         want = oracle.server_ensemble(weights, [{k: v.copy() for k, v in c.items()} for c in clients])
         assert_dict_bitwise(got, want, f"round {r}")
         rec = s.engine.last_plan.memo.get(("small_round", id(s.engine.packer), str(s.engine.device), "reference",
-                                           zero_copy))
+                                           zero_copy, parts))
         assert rec, "the small-round record was not built"
 
 

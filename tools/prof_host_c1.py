@@ -63,6 +63,36 @@ def main(rounds=300):
             name = {False: "copy-engine", True: "zero-copy", "numpy": "reference numpy"}[zc]
             print(f"{name} median us {np.median(res[zc]) * 1e6:.1f} min {min(res[zc]) * 1e6:.1f}")
         Aggregator.small_zero_copy = True
+    if "--parts" in sys.argv:  # zero-copy small rounds in 1 / 2 / 3 / 4 chained launches, alternating
+        from flearn_amd.aggregator import Aggregator
+
+        ups2 = [{"agg_weight": 1.0, "params": layouts.synthetic_state_dict(lay, rng.random(p, dtype=np.float32),
+                                                                            counter=300 + i)} for i in range(10)]
+        sets = (ups, ups2)
+        refs = [{k: np.array(v, copy=True) for k, v in s.server(u, 0)["w_glob"].items()} for u in sets]
+        kinds = (1, 2, 3, 4)
+        res = {k: [] for k in kinds}
+        res["numpy"] = []
+        for rep in range(6):
+            for r in range(rounds // 3):
+                u = sets[r % 2]
+                t = time.perf_counter()
+                reference_avg([c["agg_weight"] for c in u], [c["params"] for c in u])
+                res["numpy"].append(time.perf_counter() - t)
+            for k in kinds:
+                Aggregator.small_parts = k
+                for r in range(20):
+                    s.server(sets[r % 2], r)
+                for r in range(rounds // 3):
+                    t = time.perf_counter()
+                    out = s.server(sets[r % 2], r)["w_glob"]
+                    res[k].append(time.perf_counter() - t)
+                    ref = refs[r % 2]
+                    assert all(np.array_equal(out[kk], ref[kk]) for kk in ref), f"parts={k}: result differs"
+        for k in (*kinds, "numpy"):
+            name = f"{k} launches" if k != "numpy" else "reference numpy"
+            print(f"{name} median us {np.median(res[k]) * 1e6:.1f} min {min(res[k]) * 1e6:.1f}")
+        Aggregator.small_parts = 1
     pr = cProfile.Profile()
     pr.enable()
     for r in range(rounds):
