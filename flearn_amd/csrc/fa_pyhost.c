@@ -357,7 +357,11 @@ void *fa_py_pack_start(PyObject *dicts, PyObject *keys, int64_t npieces, const i
       break;
     }
     PyObject *d = PySequence_Fast_GET_ITEM(seq, src[i]);
-    if (!PyDict_Check(d)) { rc = FA_PY_FALLBACK; break; }
+    // plain dict / OrderedDict only: their item lookup is the C one; a subclass may override it
+    if (!PyDict_CheckExact(d) && strcmp(Py_TYPE(d)->tp_name, "collections.OrderedDict") != 0) {
+      rc = FA_PY_FALLBACK;
+      break;
+    }
     PyObject *v = PyDict_GetItemWithError(d, PyTuple_GET_ITEM(keys, i));  // borrowed
     if (!v) { PyErr_Clear(); rc = FA_PY_FALLBACK; break; }
     if (val_get(v, &vals[held]) != 0) { rc = FA_PY_FALLBACK; break; }

@@ -37,6 +37,7 @@ SHAPES = [(64, 3, 7, 7), (64,), (), (1000, 1000), (3,), (0,), (257, 129), (2048,
 @pytest.mark.parametrize("gdt,with_local,per_chunk", [(np.float64, True, 2), (np.float32, True, 4),
                                                       (np.float64, False, 1), (np.float64, True, 100)])
 def test_chunks_land_like_the_python_pack(gdt, with_local, per_chunk):
+
     chunks, total = _plan(SHAPES, per_chunk)
     lh = np.full(total, -1, np.float32)
     gh = np.full(total, -1, gdt)
@@ -70,7 +71,7 @@ def test_end_without_waits_finishes_every_copy():
             assert np.array_equal(lh[o : o + n], local[k].reshape(-1))
 
 
-@pytest.mark.parametrize("fault", ["dtype", "missing", "shape", "noncontig", "tensor"])
+@pytest.mark.parametrize("fault", ["dtype", "missing", "shape", "noncontig", "tensor", "dict_subclass"])
 def test_values_off_the_plan_fall_back_with_nothing_copied(fault):
     chunks, total = _plan(SHAPES, 2)
     lh, gh = np.zeros(total, np.float32), np.zeros(total)
@@ -85,8 +86,15 @@ def test_values_off_the_plan_fall_back_with_nothing_copied(fault):
         glob[k] = glob[k][:-1]
     elif fault == "noncontig":
         local[k] = np.asfortranarray(local[k])
-    else:
+    elif fault == "tensor":
         glob[k] = torch.from_numpy(glob[k])
+    else:  # a dict subclass may override item lookup: the native pack does not read it
+
+        class D(dict):
+            def __getitem__(self, key):
+                return super().__getitem__(key) * 0
+
+        local = D(local)
     assert ap.start(local, glob) is None
     assert not lh.any() and not gh.any()
 
@@ -204,3 +212,18 @@ def test_server_row_chunks_land_like_the_python_pack(ndev, n, wire):
                 assert (got == -7.0).all()
             else:
                 assert np.array_equal(got, ups[r][s.key].reshape(-1)[a:b]), (r, s.key, sh.index)
+
+
+def test_ordered_dicts_are_packed():
+    import collections
+
+    chunks, total = _plan(SHAPES, 3)
+    lh, gh = np.zeros(total, np.float32), np.zeros(total)
+    ap = _AsyncPack(chunks, lh.ctypes.data, gh.ctypes.data, torch.float64)
+    local, glob = _dicts(SHAPES, np.float64, 11)
+    h = ap.start(collections.OrderedDict(local), collections.OrderedDict(glob))
+    assert h is not None
+    ap.end(h)
+    for _f, _e, _pl, _pg, g in chunks:
+        for k, s, o, n in g:
+            assert np.array_equal(gh[o : o + n], glob[k].reshape(-1)) and np.array_equal(lh[o : o + n], local[k].reshape(-1))
