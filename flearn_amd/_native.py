@@ -17,7 +17,7 @@ from pathlib import Path
 import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 
 LIB_PATH = Path(__file__).resolve().parent / "lib" / "libflearn_amd.so"
-ABI_VERSION = 11
+ABI_VERSION = 12
 
 FA_OK = 0
 FA_ERR_ARG, FA_ERR_ALIGN, FA_ERR_LAUNCH = -1, -2, -3
@@ -48,6 +48,8 @@ EXPORTS = (
     "fa_ipc_close",
     "fa_push",
     "fa_copy_dma",
+    "fa_push_dma",
+    "fa_stream_join",
     "fa_set_reduce_grid",
     "fa_b64_decoded_size",
     "fa_b64_decode",
@@ -200,6 +202,8 @@ def load(require_gpu: bool = False):
                 "fa_ipc_close": ([P], ctypes.c_int),
                 "fa_push": ([P, I64, ctypes.POINTER(P), I32, I32, P], ctypes.c_int),
                 "fa_copy_dma": ([P, P, I64, P], ctypes.c_int),
+                "fa_push_dma": ([P, I64, ctypes.POINTER(P), I32, ctypes.POINTER(P), P], ctypes.c_int),
+                "fa_stream_join": ([P, ctypes.POINTER(P), I32], ctypes.c_int),
                 "fa_set_reduce_grid": ([I32], ctypes.c_int),
                 "fa_b64_decoded_size": ([P, I64], I64),
                 "fa_b64_decode": ([P, I64, P, I64, I32], ctypes.c_int),

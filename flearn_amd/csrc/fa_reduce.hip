@@ -800,6 +800,46 @@ int fa_copy_dma(void* dst, const void* src, int64_t nbytes, void* stream) {
   return FA_OK;
 }
 
+// one event recorded on `from`, waited for by `to` (destroyed at once: HIP releases it when done)
+static int stream_after(hipStream_t to, hipStream_t from) {
+  hipEvent_t ev;
+  hipError_t e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventRecord(ev, from);
+  if (e == hipSuccess) e = hipStreamWaitEvent(to, ev, 0);
+  hipEventDestroy(ev);
+  if (e != hipSuccess) return fail(FA_ERR_LAUNCH, hipGetErrorString(e));
+  return FA_OK;
+}
+
+int fa_push_dma(const void* src, int64_t nbytes, void* const* dsts, int32_t n_dsts, void* const* streams,
+                void* stream) {
+  if (nbytes < 0 || n_dsts < 0 || n_dsts > 8) return fail(FA_ERR_ARG, "bad push size or destination count");
+  if (nbytes == 0 || n_dsts == 0) return FA_OK;
+  if (!src || !dsts || !streams) return fail(FA_ERR_ARG, "null push pointer");
+  for (int i = 0; i < n_dsts; ++i)
+    if (!dsts[i] || !streams[i]) return fail(FA_ERR_ARG, "null push destination or stream");
+  hipEvent_t ev;
+  hipError_t e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventRecord(ev, static_cast<hipStream_t>(stream));
+  for (int i = 0; i < n_dsts && e == hipSuccess; ++i) {
+    hipStream_t s = static_cast<hipStream_t>(streams[i]);
+    e = hipStreamWaitEvent(s, ev, 0);
+    if (e == hipSuccess) e = hipMemcpyAsync(dsts[i], src, (size_t)nbytes, hipMemcpyDeviceToDevice, s);
+  }
+  hipEventDestroy(ev);
+  if (e != hipSuccess) return fail(FA_ERR_LAUNCH, hipGetErrorString(e));
+  return FA_OK;
+}
+
+int fa_stream_join(void* stream, void* const* streams, int32_t n) {
+  if (n < 0 || n > 16 || (n > 0 && !streams)) return fail(FA_ERR_ARG, "bad stream list");
+  for (int i = 0; i < n; ++i) {
+    const int rc = stream_after(static_cast<hipStream_t>(stream), static_cast<hipStream_t>(streams[i]));
+    if (rc) return rc;
+  }
+  return FA_OK;
+}
+
 int fa_fill_uniform_f32(float* dst, int64_t row_stride, int32_t n_rows, int64_t n_cols,
                         uint64_t seed, int64_t row_begin, int64_t col_global_begin, void* stream) {
   if (!dst || n_rows < 0 || n_cols < 0 || row_stride < n_cols) return fail(FA_ERR_ARG, "bad fill");

@@ -131,6 +131,8 @@ class PushGather:
         # one stream would run one after the other, one link at a time
         self.peer_streams = ([torch.cuda.Stream(self.device) for _ in range(self.world - 1)] if mode == "dma"
                              else [])
+        self._peer_handles = (ctypes.c_void_p * max(1, len(self.peer_streams)))(
+            *[s.cuda_stream for s in self.peer_streams]) if self.peer_streams else None
 
     def _all_ok(self, ok: int) -> bool:
         t = torch.tensor([ok], dtype=torch.int32, device=self.device if self.nccl else "cpu")
@@ -165,17 +167,17 @@ class PushGather:
                           "fa_push")
             return
         # copy engines: the peers' legs on their own streams (after the step's barrier and the
-        # stripe's reduce), this rank's own copy by a kernel on the pusher's stream
-        peers = [d for r, d in enumerate(self.dst) if r != self.rank]
-        for s, d in zip(self.peer_streams, peers):
-            s.wait_stream(self.stream)
-            self.na.check(self.L.fa_copy_dma(d + off, src.data_ptr(), n, s.cuda_stream), "fa_copy_dma")
+        # stripe's reduce: one native call), this rank's own copy by a kernel on the pusher's stream
+        peers = (ctypes.c_void_p * (self.world - 1))(*[d + off for r, d in enumerate(self.dst) if r != self.rank])
+        self.na.check(self.L.fa_push_dma(src.data_ptr(), n, peers, self.world - 1, self._peer_handles,
+                                         self.stream.cuda_stream), "fa_push_dma")
         self.na.check(self.L.fa_copy(self.dst[self.rank] + off, src.data_ptr(), n, self.stream.cuda_stream), "fa_copy")
 
     def join(self):
         """The pusher's stream waits for the copy-engine legs (mode "dma")."""
-        for s in self.peer_streams:
-            self.stream.wait_stream(s)
+        if self.peer_streams:
+            self.na.check(self.L.fa_stream_join(self.stream.cuda_stream, self._peer_handles, len(self.peer_streams)),
+                          "fa_stream_join")
 
     def end(self):
         self.join()

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define FA_ABI_VERSION 11
+#define FA_ABI_VERSION 12
 
 /* return codes */
 #define FA_OK 0
@@ -259,6 +259,16 @@ int fa_push(const void* src, int64_t nbytes, void* const* dsts, int32_t n_dsts, 
  * leg costs the reduce no CUs and no memory-pipeline slots (the copy-engine form of the one-shot
  * all-gather: one stream per peer).  ABI 11.                                                  */
 int fa_copy_dma(void* dst, const void* src, int64_t nbytes, void* stream);
+
+/* The copy-engine push leg of one stripe in one call: after the work queued so far on `stream`,
+ * copy nbytes from src to dsts[i] on streams[i] (i < n_dsts <= 8; one copy engine per peer
+ * stream).  What eight Python-level event records / waits / copies cost in host time per stripe
+ * (~80 us) this does in a few; the stripe pipeline is host-bound otherwise.  ABI 12.           */
+int fa_push_dma(const void* src, int64_t nbytes, void* const* dsts, int32_t n_dsts, void* const* streams,
+                void* stream);
+
+/* `stream` waits for the work queued so far on streams[0..n) (n <= 16).  ABI 12.             */
+int fa_stream_join(void* stream, void* const* streams, int32_t n);
 
 /* ---- wire codec (HOST functions: every pointer below is host memory) -------------------------
  * flearn's HTTP mode ships uploads and global models as base64(pickle.dumps(obj))

@@ -173,6 +173,15 @@ def test_push_and_ipc_validation(L):
     assert L.fa_copy_dma(FAKE, FAKE, -1, None) == header_define("FA_ERR_ARG")
     assert L.fa_copy_dma(None, FAKE, 64, None) == header_define("FA_ERR_ARG")
     assert L.fa_copy_dma(None, None, 0, None) == 0
+    sts = (P * 9)(*([FAKE] * 9))
+    assert L.fa_push_dma(FAKE, 64, dsts, 9, sts, None) == header_define("FA_ERR_ARG")
+    assert L.fa_push_dma(FAKE, -1, dsts, 2, sts, None) == header_define("FA_ERR_ARG")
+    assert L.fa_push_dma(FAKE, 0, dsts, 2, sts, None) == 0
+    assert L.fa_push_dma(FAKE, 64, dsts, 2, None, None) == header_define("FA_ERR_ARG")
+    assert L.fa_push_dma(FAKE, 64, bad, 2, sts, None) == header_define("FA_ERR_ARG")
+    assert L.fa_stream_join(None, None, 0) == 0
+    assert L.fa_stream_join(None, None, 2) == header_define("FA_ERR_ARG")
+    assert L.fa_stream_join(None, sts, 17) == header_define("FA_ERR_ARG")
 
 
 def test_piece_struct_layout_matches_c(tmp_path):
