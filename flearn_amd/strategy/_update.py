@@ -409,6 +409,7 @@ class DeviceUpdater:
         # chunk's kernel is launched as soon as its own copies are in
         ap = self._apack(chunks, True) if self.native_pack else None
         h = ap.start(local, glob) if ap is not None else None
+        self.last_pack = "native" if h is not None else "pool"
         futs = None
         if h is None:
             pool = _pool()

@@ -1004,6 +1004,37 @@ def test_client_side_update_large_and_fallback_values(op, mode, cuda, monkeypatc
             prev["c"] = np.asfortranarray(prev["c"])
 
 
+@pytest.mark.parametrize("gdt", [np.float64, np.float32])
+@pytest.mark.parametrize("op", ["avgm", "adagrad", "adam"])
+def test_client_side_update_native_pack(op, gdt, cuda, monkeypatch):
+    """Plain C-contiguous values (what flearn's clients hold): the zero-copy chunks are packed by
+    native threads (bucket.AsyncPack, 1-MiB chunks: many chunks, each launched after its own
+    copies), float64 and float32 global models, bit-exact against the oracle over 3 rounds."""
+    from flearn_amd.strategy._update import DeviceUpdater
+
+    monkeypatch.setattr(DeviceUpdater, "chunk_bytes", 1 << 20)
+    monkeypatch.setattr(DeviceUpdater, "first_chunk_bytes", 256 << 10)
+    rng = np.random.default_rng(33)
+    shapes = {"a": (1024, 3000), "b": (3000,), "c": (700, 900), "d": (), "e": (5, 7), "f": (64, 3, 7, 7)}
+    prev = {k: rng.standard_normal(sh).astype(np.float32) for k, sh in shapes.items()}
+    s = AVGM() if op == "avgm" else OPT()
+    v = None
+    for r in range(3):
+        glob = {k: rng.standard_normal(sh).astype(gdt) for k, sh in shapes.items()}
+        glob["d"] = np.asarray(glob["d"])  # a 0-d array (not a numpy scalar)
+        if op == "avgm":
+            want, v = oracle.mean_momentum(prev, glob, v, 0.9)
+            got = s.mean_momentum(dict(prev), glob, 0.9)
+        else:
+            want, v = oracle.adaptive_opt(prev, glob, v, op)
+            got = s.adaptive_opt(dict(prev), glob, op)
+        up = s._get_updater() if op == "avgm" else s._get_updater(op)
+        assert up.last_pack == "native"
+        assert_dict_bitwise(got, want, f"{op} {gdt.__name__} w{r}")
+        assert_dict_bitwise(s.v_t, v, f"{op} {gdt.__name__} v{r}")
+        prev = {k: np.asarray(got[k]).astype(np.float32) for k in shapes}
+
+
 @pytest.mark.parametrize("transfer", ["dma", "kernel"])
 @pytest.mark.parametrize("op", ["avgm", "adagrad"])
 def test_client_side_update_failure_mid_call_changes_nothing(op, transfer, cuda, monkeypatch):
