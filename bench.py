@@ -270,11 +270,11 @@ def calibrate_push(job: Job, world: int, dev, r_big: float, reps: int = 5, mode:
     big = p.local_cols
     small = max(ALIGN, (big // 8) // ALIGN * ALIGN)
     out = job.red.local_out
-    full = torch.empty(world * big, dtype=torch.float32, device=dev)
-    try:
-        pg = fa_dist.PushGather(full, mode=mode)
+    try:  # a bucket from the receive pool: the jobs and trials after this one map no new buffer
+        pg = fa_dist.PushGather(None, mode=mode, cols=world * big, device=dev)
     except RuntimeError as e:
         return None, {"available": False, "reason": str(e)}
+    full = pg.full
     try:
         pg.gather(out[:big], p.rank * big)
         want = torch.empty_like(full)
@@ -434,8 +434,14 @@ def run_job(cfg, layout, n, args, world, rank, dev, g_eff):
             # every gather's model plan and its neighbours, each timed for a few steps on this job
             # (real collectives; max over ranks, so every rank picks the same plan)
             for g, w_c, r_c in cands:
-                tj = Job(cfg, layout, n, ShardPlan.from_widths(p_real, g_eff, rank, w_c, rep=r_c), dev, world,
-                         args.reorder, push=PUSH_MODE.get(g, False), push_grid=push_grid)
+                try:
+                    tj = Job(cfg, layout, n, ShardPlan.from_widths(p_real, g_eff, rank, w_c, rep=r_c), dev, world,
+                             args.reorder, push=PUSH_MODE.get(g, False), push_grid=push_grid)
+                except RuntimeError as e:  # a push that every rank refused to set up (PushGather)
+                    trials.append({"gather": g, "stripe_widths": list(w_c), "replicated_cols": r_c,
+                                   "measured_ms": float("inf"), "error": str(e)})
+                    torch.cuda.empty_cache()
+                    continue
                 for _ in range(2):
                     tj.red.step()
                 t = _max_over_ranks((_event_time(tj.red.step, 5),), world, dev)[0]
@@ -443,6 +449,9 @@ def run_job(cfg, layout, n, args, world, rank, dev, g_eff):
                 trials.append({"gather": g, "stripe_widths": list(w_c), "replicated_cols": r_c, "predicted_ms":
                                round(models[g].makespan(w_c, r_c)[0] * 1e3, 4), "measured_ms": round(t * 1e3, 4)})
             gather, widths, rep = cands[min(range(len(cands)), key=lambda i: trials[i]["measured_ms"])]
+            for t in trials:  # refused set-ups: no time (the line stays strict JSON)
+                if t["measured_ms"] == float("inf"):
+                    t["measured_ms"] = None
         model = models[gather]
         info["gather"] = gather
         info["push_grid"] = push_grid if gather == "push" else None
@@ -463,8 +472,16 @@ def run_job(cfg, layout, n, args, world, rank, dev, g_eff):
     info["replicated_cols"] = plan.rep
     if world > 1 and args.stripes:
         info["gather"] = args.gather if args.gather != "auto" else "rccl"
-    job = Job(cfg, layout, n, plan, dev, world, args.reorder, push=PUSH_MODE.get(info.get("gather"), False),
-              push_grid=info.get("push_grid") or 0)
+    try:
+        job = Job(cfg, layout, n, plan, dev, world, args.reorder, push=PUSH_MODE.get(info.get("gather"), False),
+                  push_grid=info.get("push_grid") or 0)
+    except RuntimeError as e:  # the chosen push refused on every rank at set-up: RCCL's all-gather
+        if info.get("gather") not in PUSH_MODE:
+            raise
+        info["push_failed_setup"] = {"gather": info["gather"], "error": str(e)}
+        info["gather"] = "rccl"
+        torch.cuda.empty_cache()
+        job = Job(cfg, layout, n, plan, dev, world, args.reorder)
     for _ in range(args.warmup):
         job.red.step()
     torch.cuda.synchronize(dev)

@@ -1514,12 +1514,25 @@ struct PushDsts {
 __global__ __launch_bounds__(kThreads) void push_kernel(const uint8_t* __restrict__ src, int64_t quads, PushDsts d,
                                                         int n_dsts) {
   typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+  constexpr int U = 4;  // quads per lane per round: U loads, then U stores to every destination
   const u4* s = reinterpret_cast<const u4*>(src);
-  for (int64_t q = (int64_t)blockIdx.x * kThreads + threadIdx.x; q < quads; q += (int64_t)gridDim.x * kThreads) {
-    const u4 v = __builtin_nontemporal_load(s + q);
+  const int64_t G = (int64_t)gridDim.x * kThreads;
+  for (int64_t q0 = (int64_t)blockIdx.x * kThreads + threadIdx.x; q0 < quads; q0 += U * G) {
+    u4 v[U];
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
-      if (i < n_dsts) reinterpret_cast<u4*>(d.p[i])[q] = v;
+    for (int u = 0; u < U; ++u) {
+      const int64_t q = q0 + u * G;
+      v[u] = q < quads ? __builtin_nontemporal_load(s + q) : u4{0, 0, 0, 0};
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      if (i >= n_dsts) break;
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t q = q0 + u * G;
+        if (q < quads) reinterpret_cast<u4*>(d.p[i])[q] = v[u];
+      }
+    }
   }
   __threadfence_system();
 }

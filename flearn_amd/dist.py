@@ -63,6 +63,108 @@ def all_gather_into(dst: torch.Tensor, src: torch.Tensor, group=None, async_op: 
     return None
 
 
+def _all_ok(pg, ok: int) -> bool:
+    t = torch.tensor([ok], dtype=torch.int32, device=pg.device if pg.nccl else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=pg.group)
+    return bool(t.item())
+
+
+def _map_peers(pg, full: torch.Tensor):
+    """Collective: register `full` (IPC handle of its allocation + offset) and map every peer's;
+    (opened bases, per-rank device address of each rank's buffer, stale peers).  A token in the
+    buffer's first 16 bytes is read back through every mapping: an import that maps some other
+    allocation (an earlier, since-unmapped buffer whose handle it met again — seen on one GPU with
+    several processes, ~1 set-up in 5 after an unmap) is refused instead of pushed into.  Every
+    rank raises RuntimeError (nothing left mapped) if any rank cannot map or validate a peer."""
+    L = pg.L
+    bases, dsts, stale = [], [], []
+    ok = 1
+    mine = None
+    if pg.world > MAX_PUSH_RANKS or not full.is_cuda or not full.is_contiguous() or full.numel() < 4:
+        ok = 0
+    else:
+        token = torch.randint(-2**31, 2**31 - 1, (4,), dtype=torch.int32)
+        full.view(torch.int32)[:4].copy_(token)
+        torch.cuda.synchronize(full.device)
+        h, off = ctypes.create_string_buffer(64), ctypes.c_int64(0)
+        if L.fa_ipc_handle(full.data_ptr(), h, ctypes.byref(off)) == 0:
+            mine = (bytes(h.raw), int(off.value), token.tolist())
+        else:
+            ok = 0
+    infos = [None] * pg.world
+    dist.all_gather_object(infos, mine, group=pg.group)
+    if ok and all(i is not None for i in infos):
+        probe = torch.empty(4, dtype=torch.int32, device=full.device)
+        for r, (hb, off, tok) in enumerate(infos):
+            if r == pg.rank:
+                dsts.append(full.data_ptr())
+                continue
+            base = ctypes.c_void_p()
+            if L.fa_ipc_open(hb, ctypes.byref(base)) != 0 or not base.value:
+                ok = 0
+                break
+            bases.append(base.value)
+            dsts.append(base.value + off)
+            s = torch.cuda.current_stream(full.device)
+            if L.fa_copy_dma(probe.data_ptr(), base.value + off, 16, s.cuda_stream) != 0:
+                ok = 0
+                break
+            s.synchronize()
+            if probe.tolist() != tok:
+                stale.append(r)
+                ok = 0
+    else:
+        ok = 0
+    if not _all_ok(pg, ok):
+        for b in bases:
+            L.fa_ipc_close(b)
+        err = L.fa_last_error()
+        why = (f" (here: the mappings of ranks {stale} did not hold their tokens)" if stale else
+               f" (here: {err.decode(errors='replace')})" if err and not ok else "")
+        raise RuntimeError("PushGather: a rank could not map its peers' receive buffers" + why)
+    return bases, dsts, stale
+
+
+class _RecvPool:
+    """Receive buffers of the one-shot push, per (device, group), for the process's lifetime:
+    registered and mapped by every peer once, handed out again and again (`take` / `give`) and
+    never freed — re-registering a fresh buffer for every job is what let an import meet an
+    earlier buffer's handle (`_map_peers`).  Every rank takes and gives in the same order, so
+    the slots agree across ranks (checked at each take)."""
+
+    _pools: dict = {}
+
+    def __init__(self, device, group):
+        self.device, self.group = device, group
+        self.slots = []  # [buffer tensor, per-rank device addresses, busy]
+
+    @classmethod
+    def get(cls, device, group):
+        key = (str(device), id(group))
+        p = cls._pools.get(key)
+        if p is None:
+            p = cls._pools[key] = _RecvPool(device, group)
+        return p
+
+    def take(self, pg, cols: int):
+        i = next((j for j, (buf, _d, busy) in enumerate(self.slots) if not busy and buf.numel() >= cols), None)
+        picks = [None] * pg.world
+        dist.all_gather_object(picks, i, group=pg.group)
+        if len(set(picks)) != 1:
+            raise RuntimeError(f"PushGather: the ranks' receive pools disagree ({picks})")
+        if i is None:  # a new buffer: registered and mapped by every peer (collective)
+            buf = torch.empty(max(cols, 4), dtype=torch.float32, device=self.device)
+            pg.full, pg.device = buf, self.device
+            _bases, dsts, _stale = _map_peers(pg, buf)
+            self.slots.append([buf, dsts, False])
+            i = len(self.slots) - 1
+        self.slots[i][2] = True
+        return i, self.slots[i][0], self.slots[i][1]
+
+    def give(self, i: int):
+        self.slots[i][2] = False
+
+
 class PushGather:
     """One-shot all-gather over xGMI by direct peer stores (C ABI fa_ipc_* / fa_push).
 
@@ -82,48 +184,29 @@ class PushGather:
     Construction is collective and all-or-nothing: if any rank cannot map a peer, every rank
     raises RuntimeError (nothing stays mapped) and the caller keeps RCCL's all-gather."""
 
-    def __init__(self, full: torch.Tensor, group=None, mode: str = "kernel"):
+    def __init__(self, full: torch.Tensor | None, group=None, mode: str = "kernel", cols: int = 0, device=None):
+        """full: the receive buffer to register (exported and mapped for this object, unmapped by
+        close()); or None with `cols` / `device`: a buffer of at least `cols` fp32 columns from the
+        process's receive pool (_RecvPool: registered once, mapped once by every peer, reused —
+        buffers are never freed, so no import can meet an earlier buffer's handle again)."""
         from . import _native as na
 
         if mode not in ("kernel", "dma"):
             raise ValueError(f"PushGather mode {mode!r}")
         self.mode = mode
         self.na, self.L = na, na.lib()
-        self.full, self.group = full, group
+        self.group = group
         self.world, self.rank = dist.get_world_size(group), dist.get_rank(group)
-        self.device = full.device
         self.nccl = dist.get_backend(group) == "nccl"
-        self.bases, self.dst = [], []
-        ok = 1
-        mine = None
-        if self.world > MAX_PUSH_RANKS or not full.is_cuda or not full.is_contiguous():
-            ok = 0
+        self.pool_slot = None
+        if full is None:
+            self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+            pool = _RecvPool.get(self.device, group)
+            self.pool_slot, buf, self.dst = pool.take(self, cols)
+            self.full, self.bases, self.stale = buf[:cols], [], []
         else:
-            h, off = ctypes.create_string_buffer(64), ctypes.c_int64(0)
-            if self.L.fa_ipc_handle(full.data_ptr(), h, ctypes.byref(off)) == 0:
-                mine = (bytes(h.raw), int(off.value))
-            else:
-                ok = 0
-        infos = [None] * self.world
-        dist.all_gather_object(infos, mine, group=group)
-        if ok and all(i is not None for i in infos):
-            for r, (hb, off) in enumerate(infos):
-                if r == self.rank:
-                    self.dst.append(full.data_ptr())
-                    continue
-                base = ctypes.c_void_p()
-                if self.L.fa_ipc_open(hb, ctypes.byref(base)) != 0 or not base.value:
-                    ok = 0
-                    break
-                self.bases.append(base.value)
-                self.dst.append(base.value + off)
-        else:
-            ok = 0
-        if not self._all_ok(ok):
-            self._unmap()
-            err = self.L.fa_last_error()
-            raise RuntimeError("PushGather: a rank could not map its peers' receive buffers"
-                               + (f" (here: {err.decode(errors='replace')})" if err and not ok else ""))
+            self.full, self.device = full, full.device
+            self.bases, self.dst, self.stale = _map_peers(self, full)
         self.stream = torch.cuda.Stream(self.device)
         self.flag = torch.zeros(1, dtype=torch.float32, device=self.device)
         self.grid = 0  # fa_push blocks (0: the library's default)
@@ -133,11 +216,6 @@ class PushGather:
                              else [])
         self._peer_handles = (ctypes.c_void_p * max(1, len(self.peer_streams)))(
             *[s.cuda_stream for s in self.peer_streams]) if self.peer_streams else None
-
-    def _all_ok(self, ok: int) -> bool:
-        t = torch.tensor([ok], dtype=torch.int32, device=self.device if self.nccl else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self.group)
-        return bool(t.item())
 
     def _barrier(self):
         if self.nccl:
@@ -196,11 +274,16 @@ class PushGather:
         self.bases, self.dst = [], []
 
     def close(self):
-        """Collective: after every rank's pushes are done, unmap the peers' buffers."""
+        """Collective: after every rank's pushes are done, unmap the peers' buffers (a pool
+        buffer goes back to the pool, mapped)."""
         if self.dst:
             torch.cuda.synchronize(self.device)
             dist.barrier(group=self.group)
-            self._unmap()
+            if self.pool_slot is not None:
+                _RecvPool.get(self.device, self.group).give(self.pool_slot)
+                self.pool_slot, self.dst = None, []
+            else:
+                self._unmap()
 
 
 @dataclass(frozen=True)
@@ -527,13 +610,13 @@ class ShardedReducer:
         # state (a fused optimizer's next prev): then it is reduced locally and copied across
         self._tail_direct = state is None and local_out is None
         # one rank: local columns ARE the global columns, nothing to reassemble
-        self.full = (torch.empty(plan.full_cols, dtype=torch.float32, device=self.device) if self.gather
-                     else None)
-        # push=True: reassemble with direct peer stores (PushGather) instead of RCCL's all-gather;
-        # raises RuntimeError on every rank when some rank cannot map its peers
-        # push: False (RCCL's all-gather), True / "kernel" (fa_push stores) or "dma" (copy engines)
-        self.pusher = (PushGather(self.full, group, mode="dma" if push == "dma" else "kernel")
-                       if self.gather and push else None)
+        # push: False (RCCL's all-gather), True / "kernel" (fa_push stores) or "dma" (copy engines):
+        # reassemble with direct peer stores (PushGather) into a bucket from the process's receive
+        # pool (mapped by the peers once); RuntimeError on every rank if some rank cannot map a peer
+        self.pusher = (PushGather(None, group, mode="dma" if push == "dma" else "kernel", cols=plan.full_cols,
+                                  device=self.device) if self.gather and push else None)
+        self.full = (self.pusher.full if self.pusher is not None else
+                     torch.empty(plan.full_cols, dtype=torch.float32, device=self.device) if self.gather else None)
         if self.pusher is not None:
             self.pusher.grid = push_grid
 

@@ -293,7 +293,13 @@ def case_sharded_reducer_push(rank, world, mode="kernel"):
                 if op != "mean":
                     want = oracle.c_update(op, want_mean, prev_h, v_h)
                     prev_h = want.astype(np.float32)
-                assert full.tobytes() == want.astype(np.float32).tobytes(), (rank, plan.widths, op, step)
+                if full.tobytes() != want.astype(np.float32).tobytes():
+                    bad = np.nonzero(full.view(np.uint32) != want.astype(np.float32).view(np.uint32))[0]
+                    owners = sorted({next((r for r in range(world) for c in range(plan.stripes)
+                                          if plan.global_begin(c, r) <= b < plan.global_begin(c, r) + plan.widths[c]),
+                                          -1) for b in bad[:: max(1, len(bad) // 64)]})
+                    raise AssertionError((rank, mode, plan.widths, op, step, len(bad), int(bad[0]), int(bad[-1]),
+                                          "slices of ranks", owners))
             red.release()
 
 

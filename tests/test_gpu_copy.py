@@ -82,3 +82,25 @@ def test_async_pack_falls_back_for_values_off_the_plan(cuda):
     assert s.engine.packer.last_pack_paths["f32"] == "mixed"
     for key in a:
         assert np.asarray(a[key]).tobytes() == np.asarray(b[key]).tobytes(), key
+
+
+@pytest.mark.parametrize("n_dsts", [1, 2, 3, 8])
+@pytest.mark.parametrize("grid", [0, 1, 7, 64, 1024])
+def test_push_copies_every_destination(n_dsts, grid, cuda):
+    """fa_push (the one-shot all-gather's store kernel) into local buffers: every destination
+    gets the source, byte for byte, for sizes that are not a multiple of the grid's span, and
+    nothing past the end is touched."""
+    import ctypes
+
+    L = na.lib()
+    for nq in (1, 255, 256, 4097, 58_336, 200_003):
+        nbytes = nq * 16
+        src = torch.randint(0, 2**31 - 1, (nq * 4,), dtype=torch.int32, device="cuda")
+        dsts = [torch.full((nq * 4 + 64,), -5, dtype=torch.int32, device="cuda") for _ in range(n_dsts)]
+        ptrs = (ctypes.c_void_p * n_dsts)(*[d.data_ptr() for d in dsts])
+        s = torch.cuda.current_stream()
+        na.check(L.fa_push(src.data_ptr(), nbytes, ptrs, n_dsts, grid, s.cuda_stream), "fa_push")
+        s.synchronize()
+        for d in dsts:
+            assert torch.equal(d[: nq * 4], src), (n_dsts, grid, nq)
+            assert (d[nq * 4 :] == -5).all()

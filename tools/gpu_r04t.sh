@@ -5,5 +5,5 @@ set -e
 R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/${OUT:-r04t}
 mkdir -p $O
-timeout -k 10 300 python3 $R/tools/overlap_probe.py --grids 0 --copy dmahost,pushhost32,pushhost64,wr2 --copy-mb 64 > $O/overlap_push.json 2> $O/overlap_push.err
+timeout -k 10 300 python3 $R/tools/overlap_probe.py --grids 0 --copy pushhost4,pushhost8,pushhost16,pushhost32,pushhost64 --copy-mb 64 > $O/overlap_push.json 2> $O/overlap_push.err
 echo done
