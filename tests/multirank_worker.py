@@ -244,21 +244,6 @@ def case_sharded_reducer_push(rank, world, mode="kernel"):
     from flearn_amd.dist import plan_shards, plan_stripes
 
     cuda = torch.device("cuda", 0)
-    full = torch.full((world * 4096,), -1.0, device=cuda)
-    pg = PushGather(full, None, mode=mode)
-    src = torch.arange(4096, dtype=torch.float32, device=cuda) + 10000.0 * rank
-    pg.gather(src, rank * 4096)
-    want = torch.empty_like(full)
-    all_gather_into(want, src)
-    torch.cuda.synchronize()
-    assert torch.equal(full, want), rank
-    try:
-        pg.push(src, world * 4096 - 64)
-        raise AssertionError("push past the end accepted")
-    except ValueError:
-        pass
-    pg.close()
-
     n, p = 9, 700_001
     lc = -(-p // world)
     widths, rep = plan_shards(p, world, StripeModel(1e-6, 2e-9, 2e-6, 1e-8))
@@ -301,6 +286,27 @@ def case_sharded_reducer_push(rank, world, mode="kernel"):
                     raise AssertionError((rank, mode, plan.widths, op, step, len(bad), int(bad[0]), int(bad[-1]),
                                           "slices of ranks", owners))
             red.release()
+    # kernel mode: an explicitly registered bucket, last — its unmap precedes no further export in
+    # this process (the dma case runs after it: a bucket from the pool, mapped already)
+    if mode == "kernel":
+        full = torch.full((world * 4096,), -1.0, device=cuda)
+        pg = PushGather(full, None, mode=mode)
+    else:
+        pg = PushGather(None, None, mode=mode, cols=world * 4096, device=cuda)
+        full = pg.full
+        full.fill_(-1.0)
+    src = torch.arange(4096, dtype=torch.float32, device=cuda) + 10000.0 * rank
+    pg.gather(src, rank * 4096)
+    want = torch.empty_like(full)
+    all_gather_into(want, src)
+    torch.cuda.synchronize()
+    assert torch.equal(full, want), rank
+    try:
+        pg.push(src, world * 4096 - 64)
+        raise AssertionError("push past the end accepted")
+    except ValueError:
+        pass
+    pg.close()
 
 
 def case_sharded_reducer_push_dma(rank, world):
