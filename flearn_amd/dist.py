@@ -621,7 +621,8 @@ class ShardedReducer:
             self.pusher.grid = push_grid
 
     def release(self):
-        """Collective when pushing: unmap the peers' buffers before any rank frees its own."""
+        """Collective when pushing: after every rank's pushes, the bucket goes back to the receive
+        pool (the next pushing job may reuse it: read `full` before releasing)."""
         if self.pusher is not None:
             self.pusher.close()
             self.pusher = None
