@@ -45,6 +45,7 @@ import json
 import os
 import platform
 import sys
+import threading
 import time
 from pathlib import Path
 
@@ -394,94 +395,127 @@ def _contention(job, full, out, cols, dev, reps: int):
     return float(np.median(r_t)), float(np.median(g_t))
 
 
-def run_job(cfg, layout, n, args, world, rank, dev, g_eff):
-    """Plan (calibrated stripes unless --stripes is given), warm up, time args.steps steps.
-    Returns (job, step_s, wall_s, info)."""
+def _probe_job(cfg, layout, n, args, world, rank, dev, g_eff):
+    """A one-stripe job of this rank's columns, warmed up: what the calibrations run on."""
     p_real = layouts.fp32_elems(layout)
-    info = {}
+    probe = Job(cfg, layout, n, ShardPlan.make(p_real, g_eff, rank, 1), dev, world, args.reorder)
+    for _ in range(2):
+        probe.reduce_only()
+    return probe
+
+
+def _trial(cfg, layout, n, args, world, rank, dev, g_eff, gather, widths, rep, model, push_grid=0) -> dict:
+    """One candidate plan timed for 5 steps on a fresh job (max over ranks: every rank sees the
+    same numbers and picks the same plan)."""
+    p_real = layouts.fp32_elems(layout)
+    rec = {"gather": gather, "stripe_widths": list(widths), "replicated_cols": rep,
+           "predicted_ms": round(model.makespan(widths, rep)[0] * 1e3, 4)}
+    try:
+        tj = Job(cfg, layout, n, ShardPlan.from_widths(p_real, g_eff, rank, widths, rep=rep), dev, world, args.reorder,
+                 push=PUSH_MODE.get(gather, False), push_grid=push_grid)
+    except RuntimeError as e:  # a push that every rank refused to set up (PushGather)
+        torch.cuda.empty_cache()
+        rec.update(measured_ms=None, error=str(e))
+        return rec
+    for _ in range(2):
+        tj.red.step()
+    t = _max_over_ranks((_event_time(tj.red.step, 5),), world, dev)[0]
+    tj.release()
+    rec["measured_ms"] = round(t * 1e3, 4)
+    return rec
+
+
+def _model_info(model, cal, plan):
+    pred, _red, exposed = model.makespan(plan.widths, plan.rep)
+    return dict(model={"a_r_us": round(model.a_r * 1e6, 3), "b_r_ns_per_col": round(model.b_r * 1e9, 5),
+                       "a_g_us": round(model.a_g * 1e6, 3), "b_g_ns_per_col": round(model.b_g * 1e9, 5),
+                       "c_r": round(model.c_r, 4), "c_g": round(model.c_g, 4)},
+                calibration=cal, predicted_ms=round(pred * 1e3, 4), predicted_exposed_gather_ms=round(exposed * 1e3, 4))
+
+
+def plan_rccl(cfg, layout, n, args, world, rank, dev, g_eff):
+    """The reduce/gather plan with RCCL's all-gather: stripes fixed by --stripes, or the fitted
+    model's candidates (flearn_amd.dist.shard_candidates) each timed on the job, the fastest
+    kept.  Returns (plan, info, fastest measured trial in s or None)."""
+    p_real = layouts.fp32_elems(layout)
     if g_eff == 1:
-        plan = ShardPlan.make(p_real, 1, 0, args.stripes or 1)
-    elif args.stripes:
+        return ShardPlan.make(p_real, 1, 0, args.stripes or 1), {}, None
+    if args.stripes:
         sw = (None if args.stripe_weights in (None, "equal") or args.stripes == 1 else
               tuple(float(x) for x in args.stripe_weights.split(",")))
-        plan = ShardPlan.make(p_real, g_eff, rank, args.stripes, weights=sw)
-        info["stripe_choice"] = "fixed by --stripes"
-    else:
-        probe = Job(cfg, layout, n, ShardPlan.make(p_real, g_eff, rank, 1), dev, world, args.reorder)
-        for _ in range(2):
-            probe.reduce_only()
-        model, cal = calibrate(probe, world, dev)
-        push_grid = 0
-        models = {"rccl": model} if args.gather in ("auto", "rccl") else {}
-        if world > 1 and args.gather != "rccl":
-            # the one-shot push, by kernel stores (fa_push) and by copy engines (one per peer)
-            for g_name, mode, key in (("push", "kernel", "push_calibration"), ("push_dma", "dma", "push_dma_calibration")):
-                if args.gather not in ("auto", g_name):
-                    continue
-                m_push, cal_push = calibrate_push(probe, world, dev, cal["reduce_us"][0] * 1e-6, mode=mode)
-                info[key] = cal_push
-                if m_push is not None:
-                    models[g_name] = m_push
-                    if mode == "kernel":
-                        push_grid = cal_push.get("grid", 0)
-        if not models:  # --gather push, but pushing is not available here
-            models = {"rccl": model}
-        probe.release()
-        cands = [(g, w_c, r_c) for g, m in models.items() for w_c, r_c in shard_candidates(p_real, g_eff, m)]
-        gather, widths, rep = min(cands, key=lambda c: models[c[0]].makespan(c[1], c[2])[0])
-        trials = []
-        if world > 1 and len(cands) > 1:
-            # every gather's model plan and its neighbours, each timed for a few steps on this job
-            # (real collectives; max over ranks, so every rank picks the same plan)
-            for g, w_c, r_c in cands:
-                try:
-                    tj = Job(cfg, layout, n, ShardPlan.from_widths(p_real, g_eff, rank, w_c, rep=r_c), dev, world,
-                             args.reorder, push=PUSH_MODE.get(g, False), push_grid=push_grid)
-                except RuntimeError as e:  # a push that every rank refused to set up (PushGather)
-                    trials.append({"gather": g, "stripe_widths": list(w_c), "replicated_cols": r_c,
-                                   "measured_ms": float("inf"), "error": str(e)})
-                    torch.cuda.empty_cache()
-                    continue
-                for _ in range(2):
-                    tj.red.step()
-                t = _max_over_ranks((_event_time(tj.red.step, 5),), world, dev)[0]
-                tj.release()
-                trials.append({"gather": g, "stripe_widths": list(w_c), "replicated_cols": r_c, "predicted_ms":
-                               round(models[g].makespan(w_c, r_c)[0] * 1e3, 4), "measured_ms": round(t * 1e3, 4)})
-            gather, widths, rep = cands[min(range(len(cands)), key=lambda i: trials[i]["measured_ms"])]
-            for t in trials:  # refused set-ups: no time (the line stays strict JSON)
-                if t["measured_ms"] == float("inf"):
-                    t["measured_ms"] = None
-        model = models[gather]
-        info["gather"] = gather
-        info["push_grid"] = push_grid if gather == "push" else None
-        plan = ShardPlan.from_widths(p_real, g_eff, rank, widths, rep=rep)
-        pred, red_s, exposed = model.makespan(plan.widths, plan.rep)
-        info.update(stripe_choice=("model (flearn_amd.dist.plan_shards: stripes + replicated tail), coefficients "
-                                   "fitted on this job" + ("; the fastest of the model's plan and its neighbours "
-                                                           "over 5 measured steps each" if trials else "")),
-                    model={"a_r_us": round(model.a_r * 1e6, 3), "b_r_ns_per_col": round(model.b_r * 1e9, 5),
-                           "a_g_us": round(model.a_g * 1e6, 3), "b_g_ns_per_col": round(model.b_g * 1e9, 5),
-                           "c_r": round(model.c_r, 4), "c_g": round(model.c_g, 4)},
-                    calibration=cal, predicted_ms=round(pred * 1e3, 4),
-                    predicted_exposed_gather_ms=round(exposed * 1e3, 4))
-        if trials:
-            info["plan_trials"] = trials
-    info["stripe_widths"] = list(plan.widths)
-    # columns every rank reduces itself (no gather): redundant work, counted once in `value`
-    info["replicated_cols"] = plan.rep
-    if world > 1 and args.stripes:
-        info["gather"] = args.gather if args.gather != "auto" else "rccl"
+        return ShardPlan.make(p_real, g_eff, rank, args.stripes, weights=sw), {"stripe_choice": "fixed by --stripes"}, None
+    probe = _probe_job(cfg, layout, n, args, world, rank, dev, g_eff)
+    model, cal = calibrate(probe, world, dev)
+    probe.release()
+    cands = shard_candidates(p_real, g_eff, model)
+    widths, rep = min(cands, key=lambda c: model.makespan(c[0], c[1])[0])
+    trials, best_s = [], None
+    if world > 1 and len(cands) > 1:
+        trials = [_trial(cfg, layout, n, args, world, rank, dev, g_eff, "rccl", w_c, r_c, model) for w_c, r_c in cands]
+        i = min(range(len(cands)), key=lambda k: trials[k]["measured_ms"])
+        widths, rep = cands[i]
+        best_s = trials[i]["measured_ms"] * 1e-3
+    plan = ShardPlan.from_widths(p_real, g_eff, rank, widths, rep=rep)
+    info = dict(stripe_choice=("model (flearn_amd.dist.plan_shards: stripes + replicated tail), coefficients fitted "
+                               "on this job" + ("; the fastest of the model's plan and its neighbours over 5 measured "
+                                                "steps each" if trials else "")),
+                **_model_info(model, cal, plan))
+    if trials:
+        info["plan_trials"] = trials
+    return plan, info, best_s
+
+
+def plan_push(cfg, layout, n, args, world, rank, dev, g_eff, r_big_s):
+    """The one-shot push gathers (kernel stores, copy engines): each form set up on a probe job,
+    bit-checked against RCCL's all-gather, calibrated; its model's candidates timed on the job.
+    Returns (plan, gather, info, fastest measured trial in s or None); plan None: no push form
+    available here (the info says why)."""
+    p_real = layouts.fp32_elems(layout)
+    forms = [(g, m, k) for g, m, k in (("push", "kernel", "push_calibration"), ("push_dma", "dma", "push_dma_calibration"))
+             if args.gather in ("auto", g)]
+    info = {}
+    if args.stripes:  # a forced push form on the fixed stripes: no calibration, no trials
+        g = forms[0][0]
+        plan, _i, _b = plan_rccl(cfg, layout, n, args, world, rank, dev, g_eff)
+        return plan, g, {"stripe_choice": "fixed by --stripes", "push_grid": None}, None
+    probe = _probe_job(cfg, layout, n, args, world, rank, dev, g_eff)
+    models, grids = {}, {}
+    if r_big_s <= 0:  # the reduce of the whole local width (the contention terms' reference)
+        big = probe.plan.local_cols
+        r_big_s = _max_over_ranks((_event_time(lambda: probe.fn(0, big, probe.red.local_out[:big]), 5),), world, dev)[0]
     try:
-        job = Job(cfg, layout, n, plan, dev, world, args.reorder, push=PUSH_MODE.get(info.get("gather"), False),
-                  push_grid=info.get("push_grid") or 0)
-    except RuntimeError as e:  # the chosen push refused on every rank at set-up: RCCL's all-gather
-        if info.get("gather") not in PUSH_MODE:
-            raise
-        info["push_failed_setup"] = {"gather": info["gather"], "error": str(e)}
-        info["gather"] = "rccl"
-        torch.cuda.empty_cache()
-        job = Job(cfg, layout, n, plan, dev, world, args.reorder)
+        for g, mode, key in forms:
+            m, c = calibrate_push(probe, world, dev, r_big_s, mode=mode)
+            info[key] = c
+            if m is not None:
+                models[g] = m
+                grids[g] = c.get("grid", 0) if mode == "kernel" else 0
+    finally:
+        probe.release()
+    if not models:
+        return None, None, info, None
+    cands = [(g, w_c, r_c) for g, m in models.items() for w_c, r_c in shard_candidates(p_real, g_eff, m)]
+    trials = [_trial(cfg, layout, n, args, world, rank, dev, g_eff, g, w_c, r_c, models[g], grids[g])
+              for g, w_c, r_c in cands]
+    ok = [k for k in range(len(cands)) if trials[k]["measured_ms"] is not None]
+    if not ok:
+        info["plan_trials"] = trials
+        return None, None, info, None
+    i = min(ok, key=lambda k: trials[k]["measured_ms"])
+    g, widths, rep = cands[i]
+    plan = ShardPlan.from_widths(p_real, g_eff, rank, widths, rep=rep)
+    info.update(_model_info(models[g], info["push_calibration" if g == "push" else "push_dma_calibration"], plan))
+    info.update(plan_trials=trials, push_grid=grids[g] if g == "push" else None,
+                stripe_choice="push gathers' models, the fastest candidate over 5 measured steps each")
+    return plan, g, info, trials[i]["measured_ms"] * 1e-3
+
+
+def timed_job(cfg, layout, n, plan, gather, push_grid, args, world, dev, g_eff):
+    """Build the job on `plan` with `gather`, warm up, time args.steps steps (barrier + sync on
+    both sides, HIP events on the launch stream, max over ranks).  Returns (job, step_s, wall_s,
+    info)."""
+    info = {}
+    job = Job(cfg, layout, n, plan, dev, world, args.reorder, push=PUSH_MODE.get(gather, False), push_grid=push_grid or 0)
     for _ in range(args.warmup):
         job.red.step()
     torch.cuda.synchronize(dev)
@@ -506,6 +540,25 @@ def run_job(cfg, layout, n, args, world, rank, dev, g_eff):
         red_s = _max_over_ranks((_event_time(job.reduce_only, max(3, min(args.steps, 20))),), world, dev)[0]
         info["per_rank_reduce_ms"] = round(red_s * 1e3, 4)
         info["exposed_gather_ms"] = round(max(step_s - red_s, 0.0) * 1e3, 4)
+    info["stripe_widths"] = list(plan.widths)
+    # columns every rank reduces itself (no gather): redundant work, counted once in `value`
+    info["replicated_cols"] = plan.rep
+    info["gather"] = gather if world > 1 else None
+    info["push_grid"] = push_grid if gather == "push" else None
+    return job, step_s, wall, info
+
+
+def run_job(cfg, layout, n, args, world, rank, dev, g_eff, gather: str = "rccl"):
+    """Plan with `gather` ("rccl", or a push form: planned by plan_push) and time it.
+    Returns (job, step_s, wall_s, info)."""
+    if gather == "rccl" or world == 1:
+        plan, info, _best = plan_rccl(cfg, layout, n, args, world, rank, dev, g_eff)
+        push_grid = 0
+    else:
+        plan, gather, info, _best = plan_push(cfg, layout, n, args, world, rank, dev, g_eff, 0.0)
+        push_grid = info.get("push_grid") or 0
+    job, step_s, wall, tinfo = timed_job(cfg, layout, n, plan, gather, push_grid, args, world, dev, g_eff)
+    info.update(tinfo)
     return job, step_s, wall, info
 
 
@@ -670,6 +723,203 @@ def loopback_multi_gpu(devices, rounds: int = 5, config: str = "c2") -> dict:
     return out
 
 
+class HeldLine:
+    """Rank 0's JSON line, built as soon as the RCCL job is timed and verified and refined by
+    the later phases; printed exactly once — at the end, or by the Watchdog when a later phase
+    overruns its budget."""
+
+    def __init__(self, rank: int):
+        self.rank, self.line, self.exit_code = rank, None, 0
+        self._lock = threading.Lock()
+        self._printed = False
+
+    def set(self, line, exit_code: int):
+        with self._lock:
+            self.line, self.exit_code = line, exit_code
+
+    def emit(self) -> bool:
+        with self._lock:
+            if self._printed or self.line is None or self.rank != 0:
+                return False
+            print(json.dumps(self.line), flush=True)
+            self._printed = True
+            return True
+
+
+class Watchdog:
+    """Bounds the phases after the secured RCCL line (the push gathers' set-up, calibration,
+    trials and job; the weak job; the loopback): armed with a budget, it fires if the phase has
+    not been disarmed in time — a hang in a collective or in a GPU wait, on any rank — annotates
+    the held line with what overran, prints it (rank 0) and ends the process with os._exit (every
+    rank has its own watchdog, so every rank ends).  No exec, no restart."""
+
+    def __init__(self, held: HeldLine, rank: int):
+        self.held, self.rank = held, rank
+        self._lock = threading.Lock()
+        self._deadline = None
+        self._what = None
+        self._annotate = None
+        threading.Thread(target=self._run, daemon=True, name="bench-watchdog").start()
+
+    def arm(self, seconds: float, what: str, annotate=None):
+        with self._lock:
+            self._deadline, self._what, self._annotate = time.monotonic() + seconds, what, annotate
+
+    def disarm(self):
+        with self._lock:
+            self._deadline = self._what = self._annotate = None
+
+    def _run(self):
+        while True:
+            time.sleep(0.25)
+            with self._lock:
+                fire = self._deadline is not None and time.monotonic() > self._deadline
+                what, annotate = self._what, self._annotate
+            if not fire:
+                continue
+            log(f"[rank {self.rank}] WATCHDOG: {what} overran its budget; ending with the held line")
+            if self.held.line is not None and annotate is not None:
+                try:
+                    annotate(self.held.line)
+                except Exception:  # noqa: BLE001 - the line goes out whatever the annotation does
+                    pass
+            self.held.emit()
+            sys.stdout.flush()
+            sys.stderr.flush()
+            os._exit(self.held.exit_code)
+
+
+def job_extras(job, step_s, info, args, cfg, world, dev, g_eff, main_n, backend):
+    """The collective measurements around a timed job: the dominant kernel's launch time (the
+    reduce of this rank's whole local width), and at N > 1 the all-gather probe."""
+    plan, cols = job.plan, job.plan.local_cols
+    if g_eff == 1 and plan.stripes == 1:
+        launch_s = step_s  # the step IS one kernel launch
+    else:  # the reduce of this rank's whole local width as one launch (no gather)
+        launch_s = _max_over_ranks((_event_time(lambda: job.fn(0, cols, job.red.local_out), args.steps),), world, dev)[0]
+    if world > 1:
+        info["world_size"] = dist.get_world_size()
+        info["backend"] = dist.get_backend()
+        info["rccl_version"] = rccl_version() if backend == "nccl" else None
+        info["allgather_probe"] = gather_probe(job, world, dev)
+        cal = info.get("calibration")
+        if cal and cal.get("measured_gather"):
+            c_cols, g_us = cal["width_cols"][0], cal["gather_us"][0]
+            info["calibrated_per_link_gbs"] = round(c_cols * 4 / (g_us * 1e-6) / 1e9, 2) if g_us > 0 else None
+    return launch_s
+
+
+def build_line(args, cfg, world, g_eff, emu, main_n, job, step_s, wall, info, check, launch_s, cpu, backend):
+    """Rank 0's JSON line (the driver's contract) for one timed job."""
+    layout_p = job.plan.n_cols
+    plan, cols = job.plan, job.plan.local_cols
+    job_bytes = algorithmic_bytes(main_n, layout_p, cfg["op"]) if not emu else algorithmic_bytes(main_n, cols, cfg["op"])
+    value = job_bytes / GIB / step_s
+    launch_bytes = algorithmic_bytes(main_n, cols, cfg["op"])
+    achieved = launch_bytes / 1e9 / launch_s
+    traffic, traffic_src = load_traffic(args.config) if g_eff == 1 else (None, None)
+    roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "bytes_per_launch": launch_bytes,
+                "launch_us": round(launch_s * 1e6, 2)}
+    if traffic_src:
+        roofline["traffic_source"] = traffic_src
+    weak_main = args.scaling == "weak" and g_eff > 1
+    gather = info.get("gather")
+    line = {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(step_s * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak" if weak_main else "strong",
+        "vs_baseline": None,
+        "dtype": "fp32",
+        "data": "synthetic: device-generated splitmix64 U(-1,1) client uploads, agg_weight 1.0 (flearn default)",
+        "config": {
+            "workload": (f"{cfg['workload']}, weak-scaled: {main_n} clients on {g_eff} GPUs" if weak_main
+                         else cfg["workload"] + (f" on {g_eff} GPUs (fixed problem)" if g_eff > 1 else "")),
+            "config": args.config,
+            "clients": main_n,
+            "params": layout_p,
+            "layout": cfg["layout"],
+            "epilogue": cfg["op"],
+            "order": ("split-N allowed (fixed-order tree of client splits, <= 1e-6 normwise)" if args.reorder
+                      else "reference client order (bit-exact)"),
+            "parallelism": ("single GPU" if g_eff == 1 else
+                            f"element-range shards x{g_eff} + "
+                            + {"push": "one-shot push all-gather over xGMI (peer stores)",
+                               "push_dma": "one-shot push all-gather over xGMI (copy engines, one per peer)"}.get(
+                                   gather, "RCCL all-gather") + f" ({plan.stripes} stripes"
+                            + (f", widths {'/'.join(str(x) for x in plan.widths)}" if plan.stripes > 1 else "")
+                            + (f"; the last {plan.rep} columns reduced by every rank, not gathered" if plan.rep else "")
+                            + ")"
+                            + (f"; EMULATED: rank 0's reduce of a {emu}-GPU job on one GPU, no gather" if emu else "")),
+            # `value` against the HBM peak of the GPUs that produced it (N x 8 TB/s; at N > 1
+            # the step includes the all-gather, so this is the job's, not a kernel's, fraction)
+            "hbm_peak_frac_of_value": round(value * GIB / 1e9 / (HBM_PEAK_GBS * (world if not emu else 1)), 4),
+            "hbm_peak_gbs_all_gpus": HBM_PEAK_GBS * (world if not emu else 1),
+            "wall_s_timed_region": round(wall, 4),
+        },
+        "roofline": roofline,
+        "cpu_baseline": cpu,
+        "verify": check,
+    }
+    if g_eff > 1:
+        line["multi_gpu"] = dict(info)
+        if world > 1 and backend != "nccl":
+            line["multi_gpu"]["backend"] = f"{backend} (rehearsal: host-staged gather, not xGMI)"
+        if check is not None:
+            line["multi_gpu"]["verified"] = check["verified"]
+            line["multi_gpu"]["verified_windows"] = check["windows"]
+    return line
+
+
+def _exit_code(check) -> int:
+    return verify.EXIT_MISMATCH if (check is not None and not check["verified"]) else 0
+
+
+def _install_injections(rank):
+    inject = os.environ.get("FLEARN_BENCH_INJECT", "")
+    if inject == "gather_offset":
+        # rehearsal of a mis-gathering collective (tests/test_gpu_bench.py): every stripe's
+        # gathered range lands ALIGN columns late — the self-check must catch it and fail the run
+        real_gather = fa_dist.all_gather_into
+
+        def late_gather(dst, src, group=None, async_op=False):
+            real_gather(dst, src, group=group, async_op=False)
+            dst.copy_(torch.roll(dst, ALIGN))
+
+        fa_dist.all_gather_into = late_gather
+    if inject == "push_offset":
+        # rehearsal of a mis-placed push (tests/test_gpu_bench.py): every pushed slice lands ALIGN
+        # columns off — the self-check must catch it and the line keep RCCL's all-gather
+        real_push = fa_dist.PushGather.push
+
+        def off_push(self, src, elem_offset):
+            shifted = elem_offset + ALIGN
+            if shifted + src.numel() > self.full.numel():
+                shifted = elem_offset - ALIGN
+            return real_push(self, src, shifted)
+
+        fa_dist.PushGather.push = off_push
+    if inject == "push_stall" and rank == 1:
+        # rehearsal of a rank that never comes back from the push set-up (tests/test_gpu_bench.py):
+        # the watchdog must still print the verified RCCL line within the budget
+        real_init = fa_dist.PushGather.__init__
+
+        def stalled_init(self, *a, **k):
+            log("[rank 1] INJECTED: stalling in the push set-up")
+            while True:
+                time.sleep(1.0)
+
+        fa_dist.PushGather.__init__ = stalled_init
+        del real_init
+    return inject
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -693,7 +943,11 @@ def main():
     ap.add_argument("--gather", choices=("auto", "rccl", "push", "push_dma"), default="auto",
                     help="N>1: how stripes are reassembled — RCCL's all-gather, the one-shot push over "
                          "xGMI by kernel stores or by copy engines (flearn_amd.dist.PushGather), or "
-                         "whichever measures fastest")
+                         "whichever measures fastest.  The RCCL job is always timed and verified first")
+    ap.add_argument("--push-budget-s", type=float, default=float(os.environ.get("FLEARN_BENCH_PUSH_BUDGET_S", 150)),
+                    help="N>1: wall-clock budget of the push phase (set-up, calibration, trials, job)")
+    ap.add_argument("--phase-budget-s", type=float, default=float(os.environ.get("FLEARN_BENCH_PHASE_BUDGET_S", 150)),
+                    help="N>1: budget of the weak job and of the loopback, each")
     ap.add_argument("--no-loopback", action="store_true",
                     help="N>1: skip the single-process AVG(devices=[...]) loopback measurement")
     args = ap.parse_args()
@@ -722,123 +976,142 @@ def main():
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group(backend)
-    if os.environ.get("FLEARN_BENCH_INJECT") == "gather_offset":
-        # rehearsal of a mis-gathering collective (tests/test_gpu_bench.py): every stripe's
-        # gathered range lands ALIGN columns late — the self-check must catch it and fail the run
-        real_gather = fa_dist.all_gather_into
-
-        def late_gather(dst, src, group=None, async_op=False):
-            real_gather(dst, src, group=group, async_op=False)
-            dst.copy_(torch.roll(dst, ALIGN))
-
-        fa_dist.all_gather_into = late_gather
-    if os.environ.get("FLEARN_BENCH_INJECT") == "push_offset":
-        # rehearsal of a mis-placed push (tests/test_gpu_bench.py): every pushed slice lands ALIGN
-        # columns off — the self-check must catch it and the run fall back to RCCL's all-gather
-        real_push = fa_dist.PushGather.push
-
-        def off_push(self, src, elem_offset):
-            shifted = elem_offset + ALIGN
-            if shifted + src.numel() > self.full.numel():
-                shifted = elem_offset - ALIGN
-            return real_push(self, src, shifted)
-
-        fa_dist.PushGather.push = off_push
+    _install_injections(rank)
 
     cfg = CONFIGS[args.config]
     layout = layouts.get(cfg["layout"])
     emu = args.emulate_world
     g_eff = emu or world  # GPUs of the (possibly emulated) job
-    p_real = layouts.fp32_elems(layout)
     strong_n, weak_n = cfg["clients"], cfg["clients"] * g_eff
     main_n = strong_n if args.scaling == "strong" else weak_n
-
-    job, step_s, wall, info = run_job(cfg, layout, main_n, args, world, rank, dev, g_eff)
+    held = HeldLine(rank)
+    dog = Watchdog(held, rank) if world > 1 else None
 
     def self_check(job):
+        if args.no_verify:
+            return None
         log(f"[rank {rank}] verifying the reassembled model ...")
         c = verify_job(job, cfg, world, dev, emulated=bool(emu))
         if rank == 0:
             log(f"[rank 0] verified={c['verified']} windows={c['windows']} mismatched={c['mismatched_windows']}")
         return c
 
-    check = None
-    if not args.no_verify:
-        check = self_check(job)  # the verdict is shared by every rank
-        if not check["verified"] and world > 1 and info.get("gather") in PUSH_MODE:
-            # a push-reassembled bucket that fails its self-check: say so in the line, and time
-            # and verify the job again with RCCL's all-gather (never report the failed one)
-            failed = {"gather": info["gather"], "mismatched_windows": check["mismatched_windows"],
-                      "first_mismatches": check.get("first_mismatches")}
-            log(f"[rank {rank}] the {info['gather']} gather failed the self-check: re-running with RCCL")
-            job.release()
-            job, step_s, wall, info = run_job(cfg, layout, main_n, argparse.Namespace(**{**vars(args), "gather": "rccl"}),
-                                              world, rank, dev, g_eff)
-            info["push_failed_self_check"] = failed
-            check = self_check(job)
-    plan = job.plan
-    cols = plan.local_cols
-    job_bytes = algorithmic_bytes(main_n, p_real, cfg["op"])
-    if emu:  # rank 0's columns only
-        job_bytes = algorithmic_bytes(main_n, cols, cfg["op"])
-    value = job_bytes / GIB / step_s
-
-    # ---- roofline of the dominant kernel: per-launch algorithmic bytes / launch time ----
-    if g_eff == 1 and job.plan.stripes == 1:
-        launch_s = step_s  # the step IS one kernel launch
-    else:  # the reduce of this rank's whole local width as one launch (no gather)
-        launch_s = _max_over_ranks((_event_time(lambda: job.fn(0, cols, job.red.local_out), args.steps),),
-                                   world, dev)[0]
-    launch_bytes = algorithmic_bytes(main_n, cols, cfg["op"])
-    achieved = launch_bytes / 1e9 / launch_s
-    traffic, traffic_src = load_traffic(args.config) if g_eff == 1 else (None, None)
-    roofline = {
-        "bound": "hbm",
-        "achieved": round(achieved, 1),
-        "peak": HBM_PEAK_GBS,
-        "unit": "GB/s",
-        "frac": round(achieved / HBM_PEAK_GBS, 4),
-        "traffic": traffic,
-        "bytes_per_launch": launch_bytes,
-        "launch_us": round(launch_s * 1e6, 2),
-    }
-    if traffic_src:
-        roofline["traffic_source"] = traffic_src
-
-    if world > 1:
-        info["world_size"] = dist.get_world_size()
-        info["backend"] = dist.get_backend()
-        info["rccl_version"] = rccl_version() if backend == "nccl" else None
-        info["allgather_probe"] = gather_probe(job, world, dev)
-        cal = info.get("calibration")
-        if cal and cal.get("measured_gather"):
-            c_cols, g_us = cal["width_cols"][0], cal["gather_us"][0]
-            info["calibrated_per_link_gbs"] = round(c_cols * 4 / (g_us * 1e-6) / 1e9, 2) if g_us > 0 else None
-
+    # ---- phase 1: RCCL's all-gather (one GPU: the kernel alone) — timed, verified, held -------
+    job, step_s, wall, info = run_job(cfg, layout, main_n, args, world, rank, dev, g_eff, gather="rccl")
+    check = self_check(job)
+    launch_s = job_extras(job, step_s, info, args, cfg, world, dev, g_eff, main_n, backend)
     cpu = None
     if rank == 0 and g_eff == 1 and not args.no_cpu_baseline:
         sample = args.cpu_sample or min(main_n, 100)
         log(f"[rank 0] CPU baseline over {sample} clients ...")
         cpu = cpu_baseline(job.stack, layout, sample)
+    line = build_line(args, cfg, world, g_eff, emu, main_n, job, step_s, wall, info, check, launch_s, cpu, backend)
+    held.set(line, _exit_code(check))
+    rccl = {"gather": "rccl", "ms_per_step": round(step_s * 1e3, 4), "value": line["value"],
+            "verified": None if check is None else check["verified"]}
+    if g_eff > 1:
+        line["multi_gpu"]["phases"] = {"rccl": rccl}
+    gather_main = "rccl"
+    if world > 1:
+        dist.barrier()
 
-    other = None
+    # ---- phase 2: the one-shot push gathers, bounded; adopted only if faster AND verified ------
+    if world > 1 and args.gather != "rccl":
+        t_phase = time.perf_counter()
+        ph = {"status": "started", "budget_s": args.push_budget_s}
+        line["multi_gpu"]["phases"]["push"] = ph
+
+        def overran(ln, t_phase=t_phase):
+            p = ln["multi_gpu"]["phases"]["push"]
+            p.update(status="timed_out", elapsed_s=round(time.perf_counter() - t_phase, 1),
+                     note="a rank did not finish the push phase within its budget: the RCCL line stands")
+
+        dog.arm(args.push_budget_s, "push phase", overran)
+        status, pjob, pinfo = "error", None, {}
+        try:
+            r_big = (info.get("calibration") or {}).get("reduce_us", [0.0])[0] * 1e-6
+            pplan, pg_name, pinfo, pbest = plan_push(cfg, layout, main_n, args, world, rank, dev, g_eff, r_big)
+            best_rccl = min((t["measured_ms"] for t in info.get("plan_trials", []) if t["measured_ms"]), default=None)
+            if pplan is None:
+                status = "unavailable"
+            elif args.gather == "auto" and best_rccl is not None and pbest is not None and pbest * 1e3 >= best_rccl:
+                status = "slower_in_trials"
+            else:
+                pjob, pstep, pwall, ptinfo = timed_job(cfg, layout, main_n, pplan, pg_name, pinfo.get("push_grid"),
+                                                       args, world, dev, g_eff)
+                pinfo.update(ptinfo)
+                pcheck = self_check(pjob)
+                if pcheck is not None and not pcheck["verified"]:
+                    status = "failed_self_check"
+                    pinfo["push_failed_self_check"] = {"gather": pg_name, "mismatched_windows": pcheck["mismatched_windows"],
+                                                       "first_mismatches": pcheck.get("first_mismatches")}
+                    log(f"[rank {rank}] the {pg_name} gather failed the self-check: keeping the RCCL line")
+                elif args.gather == "auto" and pstep >= step_s:
+                    status = "slower"
+                else:
+                    status = "adopted"
+                ph.update(ms_per_step=round(pstep * 1e3, 4), gather=pg_name,
+                          verified=None if pcheck is None else pcheck["verified"])
+        except Exception as e:  # noqa: BLE001 - any failure here leaves the RCCL line standing
+            log(f"[rank {rank}] push phase failed: {type(e).__name__}: {e}")
+            ph["error"] = f"{type(e).__name__}: {e}"
+        # every rank's outcome (a rank that raised may not have joined the others' collectives:
+        # if they hang, the watchdog ends the run with the held line)
+        outcomes = [None] * world
+        dist.all_gather_object(outcomes, status)
+        adopt = all(o == "adopted" for o in outcomes)
+        ph["status"] = "adopted" if adopt else next((o for o in outcomes if o != "adopted"), status)
+        ph["rank_outcomes"] = outcomes
+        for k in ("push_calibration", "push_dma_calibration"):
+            if k in pinfo:
+                line["multi_gpu"][k] = pinfo[k]
+        if "plan_trials" in pinfo:
+            line["multi_gpu"]["plan_trials"] = line["multi_gpu"].get("plan_trials", []) + pinfo["plan_trials"]
+        if "push_failed_self_check" in pinfo:
+            line["multi_gpu"]["push_failed_self_check"] = pinfo["push_failed_self_check"]
+        if adopt:
+            job.release()
+            job, step_s, wall, info, check = pjob, pstep, pwall, {**info, **pinfo}, pcheck
+            gather_main = pg_name
+            launch_s = job_extras(job, step_s, info, args, cfg, world, dev, g_eff, main_n, backend)
+            phases = line["multi_gpu"]["phases"]
+            trials = line["multi_gpu"].get("plan_trials")
+            line = build_line(args, cfg, world, g_eff, emu, main_n, job, step_s, wall, info, check, launch_s, cpu, backend)
+            line["multi_gpu"]["phases"] = phases
+            if trials is not None:
+                line["multi_gpu"]["plan_trials"] = trials
+            held.set(line, _exit_code(check))
+        elif pjob is not None:
+            pjob.release()
+        ph["elapsed_s"] = round(time.perf_counter() - t_phase, 1)
+        dist.barrier()
+        dog.disarm()
+
+    # ---- phase 3: the weak job beside it, the loopback drop-in — each bounded -------------------
     if g_eff > 1 and not args.no_weak and emu is None:
+        def weak_overran(ln):
+            ln["weak"] = {"status": "timed_out", "budget_s": args.phase_budget_s}
+
+        dog.arm(args.phase_budget_s, "weak job", weak_overran)
         job.release()
         other_n = weak_n if args.scaling == "strong" else strong_n
-        ojob, ostep, _, oinfo = run_job(cfg, layout, other_n, args, world, rank, dev, g_eff)
-        other = {
+        ojob, ostep, _, oinfo = run_job(cfg, layout, other_n, args, world, rank, dev, g_eff, gather=gather_main)
+        line[("weak" if args.scaling == "strong" else "strong")] = {
             "scaling": "weak" if args.scaling == "strong" else "strong",
             "clients": other_n,
-            "value": round(algorithmic_bytes(other_n, p_real, cfg["op"]) / GIB / ostep, 2),
+            "value": round(algorithmic_bytes(other_n, layouts.fp32_elems(layout), cfg["op"]) / GIB / ostep, 2),
             "unit": "GiB/s",
             "ms_per_step": round(ostep * 1e3, 4),
             **oinfo,
         }
         ojob.release()
+        dist.barrier()
+        dog.disarm()
 
     if world > 1:
         if job is not None and job.red is not None:
-            job.red.release()  # unmap the peers' buffers (push) while the group still exists
+            job.red.release()  # collective: the bucket back to the pool while the group exists
+        fa_dist.shutdown_push()  # every peer unmaps, then the receive buckets are freed
         dist.barrier()
         dist.destroy_process_group()
     loop = None
@@ -849,71 +1122,22 @@ def main():
         devices = [torch.device("cuda", i % ndev) for i in range(world)]
         job.release()
         job = None
+
+        def loop_overran(ln):
+            ln["loopback_multi_gpu"] = {"status": "timed_out", "budget_s": args.phase_budget_s}
+
+        dog.arm(args.phase_budget_s, "loopback", loop_overran)
         log(f"[rank 0] loopback AVG(devices={[str(d) for d in devices]}) ...")
         loop = loopback_multi_gpu(devices)
+        dog.disarm()
+        line["loopback_multi_gpu"] = loop
+        if not loop["verified"]:
+            held.set(line, verify.EXIT_MISMATCH)
 
-    if rank == 0:
-        weak_main = args.scaling == "weak" and g_eff > 1
-        line = {
-            "metric": METRIC,
-            "value": round(value, 2),
-            "unit": "GiB/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(step_s * 1e3, 4),
-            "higher_is_better": True,
-            "scaling": "weak" if weak_main else "strong",
-            "vs_baseline": None,
-            "dtype": "fp32",
-            "data": "synthetic: device-generated splitmix64 U(-1,1) client uploads, agg_weight 1.0 (flearn default)",
-            "config": {
-                "workload": (f"{cfg['workload']}, weak-scaled: {main_n} clients on {g_eff} GPUs" if weak_main
-                             else cfg["workload"] + (f" on {g_eff} GPUs (fixed problem)" if g_eff > 1 else "")),
-                "config": args.config,
-                "clients": main_n,
-                "params": p_real,
-                "layout": cfg["layout"],
-                "epilogue": cfg["op"],
-                "order": ("split-N allowed (fixed-order tree of client splits, <= 1e-6 normwise)" if args.reorder
-                          else "reference client order (bit-exact)"),
-                "parallelism": ("single GPU" if g_eff == 1 else
-                                f"element-range shards x{g_eff} + "
-                                + {"push": "one-shot push all-gather over xGMI (peer stores)",
-                                   "push_dma": "one-shot push all-gather over xGMI (copy engines, one per peer)"}.get(
-                                       info.get("gather"), "RCCL all-gather") + f" ({plan.stripes} stripes"
-                                + (f", widths {'/'.join(str(x) for x in plan.widths)}" if plan.stripes > 1
-                                   else "")
-                                + (f"; the last {plan.rep} columns reduced by every rank, not gathered"
-                                   if plan.rep else "") + ")"
-                                + (f"; EMULATED: rank 0's reduce of a {emu}-GPU job on one GPU, no gather"
-                                   if emu else "")),
-                # `value` against the HBM peak of the GPUs that produced it (N x 8 TB/s; at N > 1
-                # the step includes the all-gather, so this is the job's, not a kernel's, fraction)
-                "hbm_peak_frac_of_value": round(value * GIB / 1e9 / (HBM_PEAK_GBS * (world if not emu else 1)), 4),
-                "hbm_peak_gbs_all_gpus": HBM_PEAK_GBS * (world if not emu else 1),
-                "wall_s_timed_region": round(wall, 4),
-            },
-            "roofline": roofline,
-            "cpu_baseline": cpu,
-            "verify": check,
-        }
-        if g_eff > 1:
-            line["multi_gpu"] = info
-            if world > 1 and backend != "nccl":
-                line["multi_gpu"]["backend"] = f"{backend} (rehearsal: host-staged gather, not xGMI)"
-            if check is not None:
-                line["multi_gpu"]["verified"] = check["verified"]
-                line["multi_gpu"]["verified_windows"] = check["windows"]
-            if other is not None:
-                line[other["scaling"]] = other
-        if loop is not None:
-            line["loopback_multi_gpu"] = loop
-        print(json.dumps(line), flush=True)
-    failed = (check is not None and not check["verified"]) or (loop is not None and not loop["verified"])
-    if failed:
+    held.emit()
+    if held.exit_code:
         log(f"[rank {rank}] SELF-CHECK FAILED: the reassembled global model differs from the unsharded reduce")
-        sys.exit(verify.EXIT_MISMATCH)
+        sys.exit(held.exit_code)
 
 
 if __name__ == "__main__":

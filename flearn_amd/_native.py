@@ -17,7 +17,7 @@ from pathlib import Path
 import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 
 LIB_PATH = Path(__file__).resolve().parent / "lib" / "libflearn_amd.so"
-ABI_VERSION = 12
+ABI_VERSION = 13
 
 FA_OK = 0
 FA_ERR_ARG, FA_ERR_ALIGN, FA_ERR_LAUNCH = -1, -2, -3
@@ -46,6 +46,9 @@ EXPORTS = (
     "fa_ipc_handle",
     "fa_ipc_open",
     "fa_ipc_close",
+    "fa_dev_alloc",
+    "fa_dev_free",
+    "fa_mem_range",
     "fa_push",
     "fa_copy_dma",
     "fa_push_dma",
@@ -200,6 +203,9 @@ def load(require_gpu: bool = False):
                 "fa_ipc_handle": ([P, P, ctypes.POINTER(I64)], ctypes.c_int),
                 "fa_ipc_open": ([P, ctypes.POINTER(P)], ctypes.c_int),
                 "fa_ipc_close": ([P], ctypes.c_int),
+                "fa_dev_alloc": ([I64, ctypes.POINTER(P)], ctypes.c_int),
+                "fa_dev_free": ([P], ctypes.c_int),
+                "fa_mem_range": ([P, ctypes.POINTER(P), ctypes.POINTER(I64)], ctypes.c_int),
                 "fa_push": ([P, I64, ctypes.POINTER(P), I32, I32, P], ctypes.c_int),
                 "fa_copy_dma": ([P, P, I64, P], ctypes.c_int),
                 "fa_push_dma": ([P, I64, ctypes.POINTER(P), I32, ctypes.POINTER(P), P], ctypes.c_int),

@@ -770,6 +770,35 @@ int fa_ipc_close(void* base) {
   return FA_OK;
 }
 
+int fa_dev_alloc(int64_t nbytes, void** ptr) {
+  if (!ptr || nbytes <= 0) return fail(FA_ERR_ARG, "bad device allocation request");
+  *ptr = nullptr;
+  const hipError_t e = hipMalloc(ptr, (size_t)nbytes);
+  if (e != hipSuccess) {
+    *ptr = nullptr;
+    return fail(FA_ERR_LAUNCH, hipGetErrorString(e));
+  }
+  return FA_OK;
+}
+
+int fa_dev_free(void* ptr) {
+  if (!ptr) return FA_OK;
+  const hipError_t e = hipFree(ptr);
+  if (e != hipSuccess) return fail(FA_ERR_LAUNCH, hipGetErrorString(e));
+  return FA_OK;
+}
+
+int fa_mem_range(const void* ptr, void** base, int64_t* size) {
+  if (!ptr || !base || !size) return fail(FA_ERR_ARG, "null range argument");
+  hipDeviceptr_t b = nullptr;
+  size_t n = 0;
+  const hipError_t e = hipMemGetAddressRange(&b, &n, reinterpret_cast<hipDeviceptr_t>(const_cast<void*>(ptr)));
+  if (e != hipSuccess) return fail(FA_ERR_ARG, hipGetErrorString(e));
+  *base = reinterpret_cast<void*>(b);
+  *size = (int64_t)n;
+  return FA_OK;
+}
+
 int fa_push(const void* src, int64_t nbytes, void* const* dsts, int32_t n_dsts, int32_t grid, void* stream) {
   if (nbytes < 0 || n_dsts < 0 || n_dsts > 8 || grid < 0) return fail(FA_ERR_ARG, "bad push size, destination count or grid");
   if (nbytes == 0 || n_dsts == 0) return FA_OK;

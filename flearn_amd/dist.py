@@ -63,6 +63,54 @@ def all_gather_into(dst: torch.Tensor, src: torch.Tensor, group=None, async_op: 
     return None
 
 
+class DeviceBuffer:
+    """A device allocation of its own (C ABI fa_dev_alloc), outside torch's caching allocator:
+    what the push gather exports.  A caching-allocator tensor lives inside a segment that other
+    tensors share and that torch recycles, and hipIpcGetMemHandle exports the whole segment; this
+    is one bucket, one export.  `tensor()` views it (torch keeps this object alive while any view
+    does); the memory is released by `free()` — which the caller orders after every peer has
+    unmapped it — or, failing that, when the last view dies."""
+
+    def __init__(self, nbytes: int, device):
+        from . import _native as na
+
+        self.L, self.na = na.lib(), na
+        self.nbytes, self.device = int(nbytes), torch.device(device)
+        p = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            na.check(self.L.fa_dev_alloc(self.nbytes, ctypes.byref(p)), "fa_dev_alloc")
+        self.ptr = p.value
+        self._typestr = "<f4"
+
+    @property
+    def __cuda_array_interface__(self):
+        if not self.ptr:
+            raise RuntimeError("DeviceBuffer already freed")
+        item = int(self._typestr[-1])
+        return {"shape": (self.nbytes // item,), "typestr": self._typestr, "data": (self.ptr, False),
+                "version": 2, "strides": None}
+
+    def tensor(self, dtype=torch.float32) -> torch.Tensor:
+        """A 1-D view of the whole buffer (float32 or int32)."""
+        self._typestr = {torch.float32: "<f4", torch.int32: "<i4"}[dtype]
+        t = torch.as_tensor(self, device=self.device)
+        if t.data_ptr() != self.ptr or t.device != self.device:
+            raise RuntimeError("DeviceBuffer view does not alias its allocation")
+        return t
+
+    def free(self):
+        if self.ptr:
+            ptr, self.ptr = self.ptr, None
+            with torch.cuda.device(self.device):
+                self.na.check(self.L.fa_dev_free(ptr), "fa_dev_free")
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:  # noqa: BLE001 - interpreter shutdown: nothing left to report to
+            pass
+
+
 def _all_ok(pg, ok: int) -> bool:
     t = torch.tensor([ok], dtype=torch.int32, device=pg.device if pg.nccl else "cpu")
     dist.all_reduce(t, op=dist.ReduceOp.MIN, group=pg.group)
@@ -71,20 +119,23 @@ def _all_ok(pg, ok: int) -> bool:
 
 def _map_peers(pg, full: torch.Tensor):
     """Collective: register `full` (IPC handle of its allocation + offset) and map every peer's;
-    (opened bases, per-rank device address of each rank's buffer, stale peers).  A token in the
-    buffer's first 16 bytes is read back through every mapping: an import that maps some other
-    allocation (an earlier, since-unmapped buffer whose handle it met again — seen on one GPU with
-    several processes, ~1 set-up in 5 after an unmap) is refused instead of pushed into.  Every
+    (opened bases, per-rank device address of each rank's buffer, stale peers).  A token written
+    into the buffer's first 16 bytes (the caller's bytes there are saved and put back) is read
+    back through every mapping: an import that maps some other allocation than the one exported
+    is refused instead of pushed into (the stale imports of round 4).  Every
     rank raises RuntimeError (nothing left mapped) if any rank cannot map or validate a peer."""
     L = pg.L
     bases, dsts, stale = [], [], []
     ok = 1
     mine = None
+    saved = None
     if pg.world > MAX_PUSH_RANKS or not full.is_cuda or not full.is_contiguous() or full.numel() < 4:
         ok = 0
     else:
+        head = full.view(torch.int32)[:4]
+        saved = head.clone()
         token = torch.randint(-2**31, 2**31 - 1, (4,), dtype=torch.int32)
-        full.view(torch.int32)[:4].copy_(token)
+        head.copy_(token)
         torch.cuda.synchronize(full.device)
         h, off = ctypes.create_string_buffer(64), ctypes.c_int64(0)
         if L.fa_ipc_handle(full.data_ptr(), h, ctypes.byref(off)) == 0:
@@ -115,9 +166,13 @@ def _map_peers(pg, full: torch.Tensor):
                 ok = 0
     else:
         ok = 0
-    if not _all_ok(pg, ok):
+    agreed = _all_ok(pg, ok)  # every rank has read every token it reads: the heads may go back
+    if saved is not None:
+        full.view(torch.int32)[:4].copy_(saved)
+    if not agreed:
         for b in bases:
             L.fa_ipc_close(b)
+        dist.barrier(group=pg.group)  # nobody frees or re-exports while a peer still maps it
         err = L.fa_last_error()
         why = (f" (here: the mappings of ranks {stale} did not hold their tokens)" if stale else
                f" (here: {err.decode(errors='replace')})" if err and not ok else "")
@@ -125,44 +180,126 @@ def _map_peers(pg, full: torch.Tensor):
     return bases, dsts, stale
 
 
+def _unmap_all(L, bases, group):
+    """Collective: close this rank's imports, then a barrier — after it no peer maps any bucket
+    that was mapped before, so an owner may free (and later re-export) its memory."""
+    for b in bases:
+        L.fa_ipc_close(b)
+    dist.barrier(group=group)
+
+
+def _resolve_group(group):
+    return group if group is not None else dist.distributed_c10d._get_default_group()
+
+
+def _group_alive(g) -> bool:
+    try:
+        return g in dist.distributed_c10d._world.pg_map
+    except Exception:  # noqa: BLE001 - a torch without the registry: assume alive
+        return True
+
+
 class _RecvPool:
-    """Receive buffers of the one-shot push, per (device, group), for the process's lifetime:
-    registered and mapped by every peer once, handed out again and again (`take` / `give`) and
-    never freed — re-registering a fresh buffer for every job is what let an import meet an
-    earlier buffer's handle (`_map_peers`).  Every rank takes and gives in the same order, so
-    the slots agree across ranks (checked at each take)."""
+    """Receive buckets of the one-shot push, per (device, process group): each an allocation of
+    its own (DeviceBuffer), exported once and mapped once by every peer, handed out to job after
+    job (`take` / `give`: a few ms of collective set-up and token checks saved per job — the
+    bench's plan trials build a dozen jobs), and freed collectively: `shutdown_push(group)`
+    (call it before destroying the group) unmaps every peer's import, barriers, then frees; a
+    `take` that finds no free bucket large enough first retires the free ones (same protocol), so
+    the pool holds at most the buckets in use at once plus one.  Every rank takes and gives in the
+    same order, so the slots agree across ranks (checked at each take).
+
+    Keyed by the group OBJECT (held, so its id cannot be reused by a later group): a destroyed and
+    re-created default group gets a new pool.  A pool whose group was destroyed without
+    shutdown_push is dropped locally the next time any pool is looked up (imports closed, own
+    buckets freed: no barrier is possible any more; the token check guards later imports)."""
 
     _pools: dict = {}
 
-    def __init__(self, device, group):
-        self.device, self.group = device, group
-        self.slots = []  # [buffer tensor, per-rank device addresses, busy]
+    def __init__(self, device, gobj):
+        self.device, self.gobj = device, gobj
+        self.slots = []  # [DeviceBuffer, fp32 view, per-rank device addresses, opened peer bases, busy]
 
     @classmethod
     def get(cls, device, group):
-        key = (str(device), id(group))
+        g = _resolve_group(group)
+        for key in [k for k, p in cls._pools.items() if not _group_alive(p.gobj)]:
+            cls._pools.pop(key)._drop_local()
+        key = (str(device), id(g))
         p = cls._pools.get(key)
         if p is None:
-            p = cls._pools[key] = _RecvPool(device, group)
+            p = cls._pools[key] = _RecvPool(device, g)
         return p
 
+    @classmethod
+    def bytes_held(cls) -> int:
+        return sum(s[0].nbytes for p in cls._pools.values() for s in p.slots)
+
+    def _retire(self, pg, idx):
+        """Collective: unmap and free the slots `idx` (free on every rank, same indices)."""
+        if not idx:
+            return
+        _unmap_all(pg.L, [b for i in idx for b in self.slots[i][3]], pg.group)
+        for i in sorted(idx, reverse=True):
+            buf = self.slots.pop(i)[0]
+            buf.free()
+
     def take(self, pg, cols: int):
-        i = next((j for j, (buf, _d, busy) in enumerate(self.slots) if not busy and buf.numel() >= cols), None)
+        i = next((j for j, s in enumerate(self.slots) if not s[4] and s[1].numel() >= cols), None)
         picks = [None] * pg.world
-        dist.all_gather_object(picks, i, group=pg.group)
+        dist.all_gather_object(picks, (i, len(self.slots)), group=pg.group)
         if len(set(picks)) != 1:
             raise RuntimeError(f"PushGather: the ranks' receive pools disagree ({picks})")
-        if i is None:  # a new buffer: registered and mapped by every peer (collective)
-            buf = torch.empty(max(cols, 4), dtype=torch.float32, device=self.device)
-            pg.full, pg.device = buf, self.device
-            _bases, dsts, _stale = _map_peers(pg, buf)
-            self.slots.append([buf, dsts, False])
+        if i is None:  # retire the free buckets that are too small, then a new one (collective)
+            self._retire(pg, [j for j, s in enumerate(self.slots) if not s[4]])
+            buf = DeviceBuffer(max(cols, 4) * 4, self.device)
+            view = buf.tensor(torch.float32)
+            pg.full, pg.device = view, self.device
+            try:
+                bases, dsts, _stale = _map_peers(pg, view)
+            except RuntimeError:
+                del view
+                buf.free()  # every peer closed its imports before _map_peers raised
+                raise
+            self.slots.append([buf, view, dsts, bases, False])
             i = len(self.slots) - 1
-        self.slots[i][2] = True
-        return i, self.slots[i][0], self.slots[i][1]
+        self.slots[i][4] = True
+        return i, self.slots[i][1], self.slots[i][2]
 
     def give(self, i: int):
-        self.slots[i][2] = False
+        self.slots[i][4] = False
+
+    def shutdown(self, pg):
+        """Collective: unmap every bucket on every rank, barrier, free."""
+        busy = [j for j, s in enumerate(self.slots) if s[4]]
+        if busy:
+            import warnings
+
+            warnings.warn(f"shutdown_push: {len(busy)} receive bucket(s) still in use by a reducer that was "
+                          "not released; their results are freed too", stacklevel=3)
+        self._retire(pg, list(range(len(self.slots))))
+
+    def _drop_local(self):
+        for s in self.slots:
+            for b in s[3]:
+                s[0].L.fa_ipc_close(b)
+            s[0].free()
+        self.slots = []
+
+
+def shutdown_push(group=None, device=None):
+    """Collective over `group`: free the push gather's receive buckets of this process for that
+    group (every peer's mapping closed first, then a barrier, then each rank frees its own).
+    Call it before dist.destroy_process_group; the next push job maps fresh buckets."""
+    from . import _native as na
+
+    g = _resolve_group(group)
+    for key in [k for k, p in _RecvPool._pools.items() if p.gobj is g
+                and (device is None or k[0] == str(torch.device(device)))]:
+        pool = _RecvPool._pools.pop(key)
+        ctx = type("_Ctx", (), {})()
+        ctx.L, ctx.group = na.lib(), group
+        pool.shutdown(ctx)
 
 
 class PushGather:
@@ -186,9 +323,10 @@ class PushGather:
 
     def __init__(self, full: torch.Tensor | None, group=None, mode: str = "kernel", cols: int = 0, device=None):
         """full: the receive buffer to register (exported and mapped for this object, unmapped by
-        close()); or None with `cols` / `device`: a buffer of at least `cols` fp32 columns from the
-        process's receive pool (_RecvPool: registered once, mapped once by every peer, reused —
-        buffers are never freed, so no import can meet an earlier buffer's handle again)."""
+        close(); prefer a DeviceBuffer's view: a caching-allocator tensor exports the whole
+        segment holding it); or None with `cols` / `device`: a bucket of at least `cols` fp32
+        columns from the process's receive pool (_RecvPool: an allocation of its own, mapped
+        once by every peer, reused until shutdown_push)."""
         from . import _native as na
 
         if mode not in ("kernel", "dma"):
@@ -201,8 +339,8 @@ class PushGather:
         self.pool_slot = None
         if full is None:
             self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
-            pool = _RecvPool.get(self.device, group)
-            self.pool_slot, buf, self.dst = pool.take(self, cols)
+            self.pool = _RecvPool.get(self.device, group)
+            self.pool_slot, buf, self.dst = self.pool.take(self, cols)
             self.full, self.bases, self.stale = buf[:cols], [], []
         else:
             self.full, self.device = full, full.device
@@ -268,22 +406,20 @@ class PushGather:
         self.push(src, elem_offset)
         self.end()
 
-    def _unmap(self):
-        for b in self.bases:
-            self.L.fa_ipc_close(b)
-        self.bases, self.dst = [], []
-
     def close(self):
-        """Collective: after every rank's pushes are done, unmap the peers' buffers (a pool
-        buffer goes back to the pool, mapped)."""
+        """Collective: after every rank's pushes are done (a barrier), a pool bucket goes back to
+        the pool, still mapped; an explicitly registered `full` is unmapped by every peer and a
+        second barrier follows, so no rank frees or re-exports its buffer while a peer still maps
+        it."""
         if self.dst:
             torch.cuda.synchronize(self.device)
             dist.barrier(group=self.group)
             if self.pool_slot is not None:
-                _RecvPool.get(self.device, self.group).give(self.pool_slot)
+                self.pool.give(self.pool_slot)
                 self.pool_slot, self.dst = None, []
             else:
-                self._unmap()
+                _unmap_all(self.L, self.bases, self.group)
+                self.bases, self.dst = [], []
 
 
 @dataclass(frozen=True)
@@ -622,10 +758,28 @@ class ShardedReducer:
 
     def release(self):
         """Collective when pushing: after every rank's pushes, the bucket goes back to the receive
-        pool (the next pushing job may reuse it: read `full` before releasing)."""
+        pool.  The tensor step() returned is a view of that bucket: the next pushing job reuses it,
+        and shutdown_push frees it — copy a result out before releasing if it must outlive the
+        job."""
         if self.pusher is not None:
             self.pusher.close()
             self.pusher = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.release()
+        return False
+
+    def __del__(self):
+        if getattr(self, "pusher", None) is not None:
+            import warnings
+
+            # release() is collective: it cannot run here; the bucket stays taken until
+            # shutdown_push frees the pool
+            warnings.warn("ShardedReducer with a push gather dropped without release(): its receive bucket "
+                          "stays in use until shutdown_push", ResourceWarning, stacklevel=2)
 
     @property
     def local_out(self) -> torch.Tensor:

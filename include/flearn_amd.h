@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define FA_ABI_VERSION 12
+#define FA_ABI_VERSION 13
 
 /* return codes */
 #define FA_OK 0
@@ -245,6 +245,18 @@ int fa_ipc_open(const void* handle, void** base);
 
 /* Unmap a base returned by fa_ipc_open.                                                      */
 int fa_ipc_close(void* base);
+
+/* A receive bucket of its own: hipMalloc(nbytes) into *ptr (exceptions to "nothing here
+ * allocates or frees").  An IPC export of a caching-allocator tensor names the whole segment
+ * that holds it, shared with and recycled for other tensors; a bucket from fa_dev_alloc is
+ * exactly one export, freed (fa_dev_free, NULL is a no-op; synchronises the device as hipFree
+ * does) only after every peer has unmapped it (flearn_amd.dist: DESIGN.md section 6).  ABI 13. */
+int fa_dev_alloc(int64_t nbytes, void** ptr);
+int fa_dev_free(void* ptr);
+
+/* The device allocation holding ptr: *base and *size (hipMemGetAddressRange) — what
+ * fa_ipc_handle exports for ptr.  ABI 13.                                                     */
+int fa_mem_range(const void* ptr, void** base, int64_t* size);
 
 /* Copy nbytes from src to each of dsts[0..n_dsts) (n_dsts <= 8; every pointer 16-byte aligned;
  * dsts: a HOST array of device pointers, local or peer-mapped) in one kernel of `grid` blocks

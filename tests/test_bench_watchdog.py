@@ -1,0 +1,60 @@
+"""bench.py's held line and watchdog on CPU (no GPU needed): a phase that hangs after the line was
+secured still ends the process at its budget with exactly one JSON line, annotated with what
+overran, and the held exit code (tests/test_gpu_bench.py rehearses the same with a stalled push
+set-up on the GPU box)."""
+import json
+import subprocess
+import sys
+import time
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parent.parent
+
+PROG = r"""
+import sys, time
+sys.path.insert(0, {repo!r})
+import bench
+held = bench.HeldLine(0)
+held.set({{"metric": "m", "value": 1.5, "multi_gpu": {{}}}}, {code})
+dog = bench.Watchdog(held, 0)
+def note(ln):
+    ln["multi_gpu"]["phases"] = {{"push": {{"status": "timed_out"}}}}
+dog.arm(1.0, "push phase", note)
+time.sleep(60)  # the hang
+print("not reached", flush=True)
+"""
+
+
+def _run(code):
+    t0 = time.monotonic()
+    p = subprocess.run([sys.executable, "-c", PROG.format(repo=str(REPO), code=code)], capture_output=True, text=True,
+                       timeout=120)
+    return p, time.monotonic() - t0
+
+
+def test_watchdog_prints_the_held_line_once_and_exits():
+    p, took = _run(0)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1 and "not reached" not in p.stdout
+    d = json.loads(lines[0])
+    assert d["value"] == 1.5 and d["multi_gpu"]["phases"]["push"]["status"] == "timed_out"
+    assert "WATCHDOG: push phase overran" in p.stderr
+    assert took < 40
+
+
+def test_watchdog_keeps_the_held_exit_code():
+    p, _ = _run(3)
+    assert p.returncode == 3
+    assert len([ln for ln in p.stdout.splitlines() if ln.strip()]) == 1
+
+
+def test_held_line_prints_once():
+    sys.path.insert(0, str(REPO))
+    import bench
+
+    h = bench.HeldLine(1)  # not rank 0: never prints
+    h.set({"v": 1}, 0)
+    assert h.emit() is False
+    h0 = bench.HeldLine(0)
+    assert h0.emit() is False  # nothing held yet

@@ -64,12 +64,18 @@ def test_bench_two_ranks_rehearsal(config, cuda):
     if mg["replicated_cols"]:
         assert sum(mg["stripe_widths"]) * 2 + mg["replicated_cols"] == d["config"]["params"]
     assert mg["per_rank_reduce_ms"] > 0 and mg["exposed_gather_ms"] >= 0
-    # the plan is the fastest of the measured candidates
+    # the plan is the fastest measured candidate of its gather; RCCL's job ran (and was verified)
+    # first, and a push plan replaced it only if its own timed job was faster and verified
     trials = [t for t in mg["plan_trials"] if t["measured_ms"] is not None]  # None: a refused set-up
     assert trials
-    best = min(trials, key=lambda t: t["measured_ms"])
-    assert (best["gather"], best["stripe_widths"], best["replicated_cols"]) == (
-        mg["gather"], mg["stripe_widths"], mg["replicated_cols"])
+    best = min((t for t in trials if t["gather"] == mg["gather"]), key=lambda t: t["measured_ms"])
+    assert (best["stripe_widths"], best["replicated_cols"]) == (mg["stripe_widths"], mg["replicated_cols"])
+    ph = mg["phases"]
+    assert ph["rccl"]["verified"] is True and ph["rccl"]["ms_per_step"] > 0
+    assert ph["push"]["status"] in ("adopted", "slower", "slower_in_trials", "unavailable")
+    assert (mg["gather"] != "rccl") == (ph["push"]["status"] == "adopted")
+    if mg["gather"] != "rccl":
+        assert d["ms_per_step"] < ph["rccl"]["ms_per_step"]
     assert d["weak"]["clients"] == 200 and d["weak"]["value"] > 0
     assert d["roofline"]["bound"] == "hbm" and d["roofline"]["frac"] > 0
     # the reassembled model was checked bit for bit on >= 64 boundary windows, on both ranks
@@ -100,18 +106,41 @@ def test_bench_push_gather_is_verified(cuda):
 
 
 @pytest.mark.timeout(300)
-def test_bench_falls_back_to_rccl_when_a_push_fails_its_check(cuda):
+def test_bench_keeps_rccl_when_a_push_fails_its_check(cuda):
     """FLEARN_BENCH_INJECT=push_offset with --gather push: the pushed bucket fails the self-check,
-    the line records it (`push_failed_self_check`) and the job is timed and verified again with
-    RCCL's all-gather, so the run still ends verified."""
+    the line records it (`push_failed_self_check`) and keeps the RCCL job timed and verified
+    before the push phase, so the run still ends verified."""
     p = _rehearse("c2", ("--no-weak", "--no-loopback", "--stripes", "2", "--gather", "push"), inject="push_offset")
     assert p.returncode == 0, p.stderr[-4000:]
-    assert "failed the self-check: re-running with RCCL" in p.stderr
+    assert "failed the self-check: keeping the RCCL line" in p.stderr
     d = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][0])
     mg = d["multi_gpu"]
     assert mg["gather"] == "rccl" and mg["push_failed_self_check"]["gather"] == "push"
     assert mg["push_failed_self_check"]["mismatched_windows"] > 0
+    assert mg["phases"]["push"]["status"] == "failed_self_check"
     assert d["verify"]["verified"] is True and "RCCL all-gather" in d["config"]["parallelism"]
+
+
+@pytest.mark.timeout(300)
+def test_bench_line_survives_a_stalled_push_setup(cuda):
+    """FLEARN_BENCH_INJECT=push_stall: rank 1 never returns from the push gather's set-up (rank 0
+    then waits in its collective).  The RCCL job was timed and verified before the push phase;
+    the watchdog ends both ranks at the phase budget and rank 0 prints that line, exit 0, long
+    before the driver's limit."""
+    import time
+
+    t0 = time.monotonic()
+    p = _rehearse("c2", ("--no-weak", "--no-loopback", "--push-budget-s", "25"), inject="push_stall")
+    took = time.monotonic() - t0
+    assert p.returncode == 0, p.stderr[-4000:]
+    assert "INJECTED: stalling in the push set-up" in p.stderr and "WATCHDOG: push phase overran" in p.stderr
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    d = json.loads(lines[0])
+    mg = d["multi_gpu"]
+    assert mg["gather"] == "rccl" and mg["phases"]["push"]["status"] == "timed_out"
+    assert mg["phases"]["rccl"]["verified"] is True and d["verify"]["verified"] is True and d["value"] > 0
+    assert took < 240, took
 
 
 @pytest.mark.timeout(300)
