@@ -389,7 +389,10 @@ class Packer:
         # from Python: values off the plan) | "pool"
         self.last_pack_paths = {}
         #: one device: results stored into fresh pinned buffers by fa_copy kernels (zero-copy
-        #: writes) and handed out as views; False: copy-engine D2H into staging + host copy
+        #: writes) and handed out as views; False: copy-engine D2H into staging + host copy into
+        #: pageable memory.  The pinned buffers come from torch's pinned caching allocator, which
+        #: keeps freed pages locked for reuse: a server that retains many rounds' w_glob (history,
+        #: checkpoints) pins one model per retained round — set False there
         self.zero_copy_out = True
 
     def _executor(self) -> concurrent.futures.ThreadPoolExecutor:
@@ -710,7 +713,8 @@ class Packer:
         """One device: fa_copy kernels store each result straight into a fresh pinned buffer per
         kind over PCIe (~53 GB/s; the copy engine's D2H ran at ~30 GB/s)
         and the values handed out are views of it — no staging, no host copy.  The buffer comes
-        from torch's pinned caching allocator and goes back to it when the views die."""
+        from torch's pinned caching allocator and goes back to it when the views die (it stays
+        page-locked in torch's cache: `zero_copy_out`)."""
         L = na.lib()
         fresh, dev = {}, None
         for kind, parts in results.items():

@@ -956,8 +956,26 @@ __global__ __launch_bounds__(64 * W) void reduce_kernel_splitn(const float* __re
 // row-pointer kernel takes 2.4x the UTCL1 translation misses of the stack kernel on per-tensor
 // allocations: profiles/r04/rows_pmc/).  The dword is consumed one row later (xor into a sink
 // kept alive by an empty asm), when it has long arrived.
+// LT > 0 (n <= LT clients, the host's choice): the group's KG x n row pointers are copied into LDS
+// at its claim (one coalesced vector load per wave, one barrier) and every step's pointer comes
+// from there (a ds_read, made wave-uniform with readfirstlane) instead of a scalar load from the
+// rows table in L2: 8 waves x 2 pointer loads per step, each a scalar-cache miss on a table of
+// S x N pointers, left the waves waiting on SMEM before their vector loads (SQ_INSTS_SMEM 9.2x,
+// SQ_WAIT_INST_ANY 3-4x the stack kernel's: profiles/r04/rows_pmc/).
+template <int LT>
+__device__ __forceinline__ const float* srm_row_ptr(const float* const* lds_row, const float* const* g_row, int i) {
+  if constexpr (LT > 0) {
+    const uint64_t p = reinterpret_cast<uint64_t>(lds_row[i]);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)p);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(p >> 32));
+    return reinterpret_cast<const float*>(((uint64_t)hi << 32) | lo);
+  } else {
+    return g_row[i];
+  }
+}
+
 template <class P, typename T, int OP, int V, int W, int KG, int DN, bool NT, bool TR = false, int DS = 1,
-          bool SG = false, int PFA = 0>
+          bool SG = false, int PFA = 0, int LT = 0>
 __global__ __launch_bounds__(64 * W) void reduce_kernel_segrows_rm(const float* const* __restrict__ rows, int n,
                                                                    const typename P::w_t* __restrict__ w,
                                                                    const fa_piece* __restrict__ pieces,
@@ -1003,8 +1021,15 @@ __global__ __launch_bounds__(64 * W) void reduce_kernel_segrows_rm(const float* 
         cols[j] = pc.n_cols;
         bytes[j] = (uint32_t)pc.n_cols * 4u;
       }
+      __shared__ const float* s_tab[KG][LT > 0 ? LT : 1];
+      if constexpr (LT > 0) {  // the previous claim's readers are past the loop-end barriers
+#pragma unroll
+        for (int j = 0; j < KG; ++j)
+          for (int k = (int)threadIdx.x; k < n; k += 64 * W) s_tab[j][k] = rp[j][k];
+        __syncthreads();
+      }
       // row pointer of step (i, j); rows clamped (a step past the end is never loaded)
-#define FA_SRM_PTR(i, j) (reinterpret_cast<const char*>(rp[j][(i) < n ? (i) : n - 1]) + ob[j])
+#define FA_SRM_PTR(i, j) (reinterpret_cast<const char*>(srm_row_ptr<LT>(s_tab[j], rp[j], (i) < n ? (i) : n - 1)) + ob[j])
 #define FA_SRM_LOAD(p, j, slot)                                                                              \
   {                                                                                                          \
     const __amdgpu_buffer_rsrc_t r_ = row_rsrc((p), bytes[j]);                                               \

@@ -264,8 +264,10 @@ def _register(params: dict, row_np: _RowArray, layout: tuple, staged=None):
     key = id(params)
     with _ROWS_LOCK:
         if len(_ROWS) > 4096:
-            for k in [k for k, ent in _ROWS.items() if not _entry_alive(ent)]:
-                del _ROWS[k]
+            # over a snapshot: a weakref callback run by the collector during the scan deletes
+            # from the dict (re-entrantly, under this same lock)
+            for k in [k for k, ent in list(_ROWS.items()) if not _entry_alive(ent)]:
+                _ROWS.pop(k, None)
         # the entry goes when its row dies (a params dict cannot be weakly referenced, so a dict
         # freed while its arrays live on leaves the entry behind: _live_entry drops it on lookup)
         _ROWS[key] = (weakref.ref(row_np, lambda r, k=key: _drop_entry(k, r)), layout, staged, refs)

@@ -313,9 +313,49 @@ def case_sharded_reducer_push_dma(rank, world):
     case_sharded_reducer_push(rank, world, mode="dma")
 
 
+def case_push_lifecycle(rank, world):
+    """The export -> map -> unmap -> free -> re-export sequence that produced round 4's stale
+    imports, driven deterministically 12 times each way: (a) pool buckets (an allocation of their
+    own each) taken, gathered into, released and freed by shutdown_push, then fresh ones; (b) an
+    explicitly registered DeviceBuffer bucket, closed (unmap + barrier) and freed, then the next
+    one, sizes cycling so freed addresses are reused.  Every set-up validates every mapping by its
+    token (`_map_peers` raises on any mismatch: a stale import fails the test), every gathered
+    bucket equals the all-gather's, and the registered bucket's head bytes survive the token."""
+    from flearn_amd import dist as fd
+
+    cuda = torch.device("cuda", 0)
+    for it in range(12):
+        cols = world * (4096 + 1024 * (it % 3))
+        src = torch.arange(cols // world, dtype=torch.float32, device=cuda) + 1e5 * rank + it
+        want = torch.empty(cols, dtype=torch.float32, device=cuda)
+        fd.all_gather_into(want, src)
+        # (a) the pool: a fresh bucket after every shutdown
+        pg = fd.PushGather(None, None, mode="kernel" if it % 2 == 0 else "dma", cols=cols, device=cuda)
+        assert pg.stale == [] and fd._RecvPool.bytes_held() >= cols * 4
+        pg.gather(src, rank * (cols // world))
+        torch.cuda.synchronize()
+        assert torch.equal(pg.full, want), (rank, it, "pool")
+        pg.close()
+        fd.shutdown_push()
+        assert fd._RecvPool.bytes_held() == 0
+        # (b) an explicit DeviceBuffer bucket, its head bytes preserved through registration
+        buf = fd.DeviceBuffer(cols * 4, cuda)
+        full = buf.tensor(torch.float32)
+        full.fill_(-7.0)
+        pe = fd.PushGather(full, None, mode="kernel")
+        assert pe.stale == [] and bool((full[:4] == -7.0).all())
+        pe.gather(src, rank * (cols // world))
+        torch.cuda.synchronize()
+        assert torch.equal(full, want), (rank, it, "explicit")
+        pe.close()  # every peer unmapped (second barrier) before this rank frees
+        del full, pe
+        buf.free()
+
+
 CASES = {f.__name__[5:]: f for f in (case_avg_fixtures, case_setup_strategy, case_fused_rounds,
                                       case_first_round_adopt, case_empty_ranks, case_dyn, case_sharded_reducer,
-                                      case_sharded_reducer_push, case_sharded_reducer_push_dma)}
+                                      case_sharded_reducer_push, case_sharded_reducer_push_dma,
+                                      case_push_lifecycle)}
 
 
 def rank_main(rank, world, port, names):

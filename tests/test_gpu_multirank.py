@@ -80,3 +80,12 @@ def test_sharded_reducer_push_gather(world, cuda):
     per stripe, or one copy-engine copy per peer (here every "peer" is another process on the
     same GPU), bit-exact."""
     _run_ranks(world, ["sharded_reducer_push", "sharded_reducer_push_dma"])
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("world", [2, 3])
+def test_push_setup_lifecycle(world, cuda):
+    """export -> map -> unmap -> free -> re-export, 12 times for pool buckets (shutdown_push) and
+    for explicitly registered DeviceBuffer buckets: every mapping holds its token, every gathered
+    bucket is the all-gather's (the round-4 stale-import sequence)."""
+    _run_ranks(world, ["push_lifecycle"])

@@ -22,3 +22,8 @@ run own_bar_fixed --alloc own --after-unmap barrier --sizes fixed &&
 timeout -k 10 120 rocprofv3 --memory-copy-trace --kernel-trace --stats --output-format csv -d $O/dma/trace -o legs -- \
   python3 tools/probe_dma_legs.py --legs 7 --mib 64 --out $O/dma/legs.json > $O/dma/legs.out 2> $O/dma/legs.err &&
 cat $O/dma/legs.json
+mkdir -p $O/rows &&
+for c in ns c2; do
+  timeout -k 10 300 python3 tools/tune_rows.py --config $c --reps 4 --alloc clones --only lt > $O/rows/${c}_clones.jsonl 2> $O/rows/${c}_clones.err || exit 1
+done
+echo rows-done

@@ -67,20 +67,23 @@ def rank_main(rank, world, port, args):
             buf.view(torch.int32)[:4].copy_(torch.tensor(tok, dtype=torch.int32))
             torch.cuda.synchronize(dev)
             h, off = ctypes.create_string_buffer(64), ctypes.c_int64(0)
-            na.check(L.fa_ipc_handle(buf.data_ptr(), h, ctypes.byref(off)), "fa_ipc_handle")
             base, size = ctypes.c_void_p(), ctypes.c_int64(0)
-            na.check(L.fa_mem_range(buf.data_ptr(), ctypes.byref(base), ctypes.byref(size)), "fa_mem_range")
+            rc_r = L.fa_mem_range(buf.data_ptr(), ctypes.byref(base), ctypes.byref(size))
+            rc_h = L.fa_ipc_handle(buf.data_ptr(), h, ctypes.byref(off))
             hb = bytes(h.raw)
             rec = {"it": it, "cols": cols, "ptr": hex(buf.data_ptr()), "base": hex(base.value or 0),
                    "size": int(size.value), "offset": int(off.value), "handle": hb.hex(),
                    "handle_seen_at": seen.get(hb), "peers": {}}
+            if rc_r or rc_h:  # e.g. hipIpcGetMemHandle refusing a re-allocated address: recorded
+                rec["export_error"] = L.fa_last_error().decode(errors="replace")
             seen.setdefault(hb, it)
             infos = [None] * world
-            dist.all_gather_object(infos, (hb, int(off.value), tok), group=None)
+            dist.all_gather_object(infos, None if rc_h else (hb, int(off.value), tok), group=None)
             opened = []
-            for r, (phb, poff, ptok) in enumerate(infos):
-                if r == rank:
+            for r, info in enumerate(infos):
+                if r == rank or info is None:
                     continue
+                phb, poff, ptok = info
                 pb = ctypes.c_void_p()
                 rc = L.fa_ipc_open(phb, ctypes.byref(pb))
                 if rc != 0 or not pb.value:
@@ -115,14 +118,15 @@ def rank_main(rank, world, port, args):
     finally:
         Path(args.out).mkdir(parents=True, exist_ok=True)
         (Path(args.out) / f"rank{rank}.json").write_text(json.dumps(log, indent=1))
-        stale = sum(1 for rec in log for p in rec["peers"].values() if not p.get("ok"))
+        stale = [sum(1 for rec in log for p in rec["peers"].values() if not p.get("ok")),
+                 sum(1 for rec in log if "export_error" in rec)]
         allr = [None] * world
         try:
             dist.all_gather_object(allr, stale)
         except Exception:  # noqa: BLE001 - the summary is best effort
             pass
         if rank == 0:
-            print(json.dumps({"variant": vars(args), "stale_mappings_per_rank": allr}), flush=True)
+            print(json.dumps({"variant": vars(args), "stale_mappings_and_export_errors_per_rank": allr}), flush=True)
         dist.destroy_process_group()
 
 

@@ -42,6 +42,9 @@ def main():
     ap.add_argument("--config", default="ns", choices=sorted(CONFIGS))
     ap.add_argument("--alloc", default="clones", choices=("clones", "views", "stack"))
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--kernel", default="product", choices=("product", "lt"),
+                    help="lt: the row kernel with the group's row pointers staged in LDS (tools/libtune_rows.so "
+                         "variant 16, the product's V8 W8 KG2 geometry and piece table; mean only)")
     a = ap.parse_args()
     name, n, op = CONFIGS[a.config]
     dev = torch.device("cuda", 0)
@@ -89,10 +92,27 @@ def main():
         v = [torch.zeros(stride, dtype=torch.float64, device=dev) for _ in range(2)]
         vr = [torch.zeros(stride, dtype=torch.float64, device=dev) for _ in range(2)]
 
+    T = None
+    if a.kernel == "lt":
+        import ctypes
+
+        if op != "mean":
+            raise SystemExit("--kernel lt: mean only")
+        T = ctypes.CDLL(str(REPO / "tools" / "libtune_rows.so"))
+        P = ctypes.c_void_p
+        T.tune_rows_rm_launch.argtypes = [ctypes.c_int, P, ctypes.c_int, P, P, ctypes.c_int64, ctypes.c_int, P,
+                                          ctypes.c_double, P, P]
+
     def rows_launch(cur):
         (sh, table), = eng.packer.pack(plan, clients)[KIND_F32]
         assert isinstance(table, RowTable), type(table)
-        if op == "mean":
+        if T is not None:
+            pieces, npieces, grid = table.piece_table(0)
+            rc = T.tune_rows_rm_launch(16, table.ptrs.data_ptr(), n, w.data_ptr(), pieces.data_ptr(), npieces, grid,
+                                       table.work.data_ptr(), float(n), out_rows.data_ptr(), na.stream_handle(dev))
+            assert rc == 0, rc
+            table.release()
+        elif op == "mean":
             agg.reduce_stack(table, w, na.MODE_W32_DIV64, float(n), out32=out_rows)
         else:
             agg.reduce_stack(table, w, na.MODE_W32_DIV64, float(n), out32=pr[1 - cur], prev=pr[cur], v=vr[cur],
@@ -129,7 +149,7 @@ def main():
         t_rows.append(e0.elapsed_time(e1) * 1e3)
         t_stack.append(e1.elapsed_time(e2) * 1e3)
     alg = n * p * 4 + p * 4 + (0 if op == "mean" else p * 4 + 2 * p * 8)
-    print(json.dumps({"config": a.config, "alloc": a.alloc, "clients": n, "params": p, "bit_equal": same,
+    print(json.dumps({"config": a.config, "alloc": a.alloc, "kernel": a.kernel, "clients": n, "params": p, "bit_equal": same,
                       "rows_us_median": round(float(np.median(t_rows)), 1),
                       "stack_kernel_us_median": round(float(np.median(t_stack)), 1),
                       "stack_frac": round(alg / float(np.median(t_stack)) / 8e6, 4),

@@ -206,7 +206,8 @@ def main():
                   "rm_v16w4kg2ds2": (6, 4, 64), "rm_v4w8kg4ds2": (7, 8, 32), "rm_v4w8kg4ds4": (8, 8, 32),
                   "rm_v8w8kg2sg": (9, 8, 64), "rm_v16w4kg2sg": (10, 4, 64), "rm_v8w8kg3sg": (11, 8, 64),
                   "rm_v8w8kg2pf2": (12, 8, 64), "rm_v8w8kg2pf4": (13, 8, 64), "rm_v8w8kg2pf8": (14, 8, 64),
-                  "rm_v16w4kg2pf4": (15, 4, 64)}
+                  "rm_v16w4kg2pf4": (15, 4, 64), "rm_v8w8kg2lt": (16, 8, 64), "rm_v16w4kg2lt": (17, 4, 64),
+                  "rm_v8w8kg2ds2lt": (18, 8, 64), "rm_v8w8kg3lt": (19, 8, 64)}
     for kname, (kid, wv, pchunks) in rm_kernels.items():
         if a.only and not any(o in kname for o in a.only.split(",")):
             continue
