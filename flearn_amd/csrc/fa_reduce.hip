@@ -788,6 +788,32 @@ int fa_dev_free(void* ptr) {
   return FA_OK;
 }
 
+int fa_dev_retire(void* ptr, int64_t nbytes, int32_t* va_kept) {
+  if (!va_kept) return fail(FA_ERR_ARG, "null va_kept");
+  *va_kept = 0;
+  if (!ptr) return FA_OK;
+  hipError_t e = hipFree(ptr);
+  if (e != hipSuccess) return fail(FA_ERR_LAUNCH, hipGetErrorString(e));
+  if (nbytes <= 0) return FA_OK;
+  // the freed range's addresses, reserved with no memory behind them for the process's lifetime:
+  // a later allocation (and so a later IPC export) can never land there again.  2-MiB rounded
+  // first (hipMalloc's fragment), then 4-KiB; a reservation that does not land on ptr is undone
+  for (const int64_t gran : {(int64_t)2 << 20, (int64_t)4 << 10}) {
+    const size_t sz = (size_t)((nbytes + gran - 1) / gran * gran);
+    void* r = nullptr;
+    if (hipMemAddressReserve(&r, sz, 0, ptr, 0) != hipSuccess || !r) {
+      (void)hipGetLastError();
+      continue;
+    }
+    if (r == ptr) {
+      *va_kept = 1;
+      return FA_OK;
+    }
+    (void)hipMemAddressFree(r, sz);
+  }
+  return FA_OK;
+}
+
 int fa_mem_range(const void* ptr, void** base, int64_t* size) {
   if (!ptr || !base || !size) return fail(FA_ERR_ARG, "null range argument");
   hipDeviceptr_t b = nullptr;
@@ -820,11 +846,17 @@ int fa_push(const void* src, int64_t nbytes, void* const* dsts, int32_t n_dsts, 
   return launch_check();
 }
 
+constexpr hipMemcpyKind kCopyEngine = hipMemcpyDeviceToDeviceNoCU;
+
 int fa_copy_dma(void* dst, const void* src, int64_t nbytes, void* stream) {
   if (nbytes < 0) return fail(FA_ERR_ARG, "negative copy size");
   if (nbytes == 0) return FA_OK;
   if (!dst || !src) return fail(FA_ERR_ARG, "null copy pointer");
-  const hipError_t e = hipMemcpyAsync(dst, src, (size_t)nbytes, hipMemcpyDeviceToDevice, static_cast<hipStream_t>(stream));
+  // NoCU: a copy engine, not the runtime's blit kernel.  With hipMemcpyDeviceToDevice the runtime
+  // ran every leg as __amd_rocclr_copyBuffer kernels on the compute queues (rocprofv3, round 5:
+  // profiles/r05/push_dma_trace/) — the CUs and memory pipelines the "copy-engine" push was meant
+  // to leave to the reduce
+  const hipError_t e = hipMemcpyAsync(dst, src, (size_t)nbytes, kCopyEngine, static_cast<hipStream_t>(stream));
   if (e != hipSuccess) return fail(FA_ERR_LAUNCH, hipGetErrorString(e));
   return FA_OK;
 }
@@ -853,7 +885,7 @@ int fa_push_dma(const void* src, int64_t nbytes, void* const* dsts, int32_t n_ds
   for (int i = 0; i < n_dsts && e == hipSuccess; ++i) {
     hipStream_t s = static_cast<hipStream_t>(streams[i]);
     e = hipStreamWaitEvent(s, ev, 0);
-    if (e == hipSuccess) e = hipMemcpyAsync(dsts[i], src, (size_t)nbytes, hipMemcpyDeviceToDevice, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(dsts[i], src, (size_t)nbytes, kCopyEngine, s);
   }
   hipEventDestroy(ev);
   if (e != hipSuccess) return fail(FA_ERR_LAUNCH, hipGetErrorString(e));

@@ -63,24 +63,53 @@ def all_gather_into(dst: torch.Tensor, src: torch.Tensor, group=None, async_op: 
     return None
 
 
+#: exported buckets released by their users: never freed while the process lives (see
+#: DeviceBuffer), handed out again by DeviceBuffer.get
+_PARKED: list = []
+
+
 class DeviceBuffer:
     """A device allocation of its own (C ABI fa_dev_alloc), outside torch's caching allocator:
     what the push gather exports.  A caching-allocator tensor lives inside a segment that other
-    tensors share and that torch recycles, and hipIpcGetMemHandle exports the whole segment; this
-    is one bucket, one export.  `tensor()` views it (torch keeps this object alive while any view
-    does); the memory is released by `free()` — which the caller orders after every peer has
-    unmapped it — or, failing that, when the last view dies."""
+    tensors share and that torch recycles (empty_cache frees it), and hipIpcGetMemHandle exports
+    the whole segment; this is one bucket, one export.
+
+    Once exported (`exported`), a bucket is never freed while the process lives: `free()` parks
+    it and `DeviceBuffer.get` hands it out again (re-exporting the same memory).  On this runtime
+    an exporter that frees imported memory and exports again makes 13-34% of later imports map
+    the wrong allocation — another process's bucket or the importer's own — whether or not the
+    freed address is kept out of reuse; with nothing exported ever freed, and a barrier after
+    every unmap, 0 of 1,920 imports were wrong (tools/ipc_probe.py,
+    profiles/r05/ipc/).  `tensor()` views it (torch keeps this object alive while any view
+    does); an unexported buffer is freed by `free()` or when the last view dies."""
 
     def __init__(self, nbytes: int, device):
         from . import _native as na
 
         self.L, self.na = na.lib(), na
         self.nbytes, self.device = int(nbytes), torch.device(device)
+        self.exported = False  # set when peers may map it: from then on free() parks it
+        self._typestr = "<f4"
         p = ctypes.c_void_p()
         with torch.cuda.device(self.device):
             na.check(self.L.fa_dev_alloc(self.nbytes, ctypes.byref(p)), "fa_dev_alloc")
         self.ptr = p.value
-        self._typestr = "<f4"
+
+    @classmethod
+    def get(cls, nbytes: int, device) -> "DeviceBuffer":
+        """A parked (previously exported, released) buffer of at least nbytes on `device` — the
+        smallest that fits — or a new one."""
+        dev = torch.device(device)
+        fits = [b for b in _PARKED if b.device == dev and b.nbytes >= nbytes]
+        if fits:
+            b = min(fits, key=lambda x: x.nbytes)
+            _PARKED.remove(b)
+            return b
+        return cls(nbytes, dev)
+
+    @staticmethod
+    def parked_bytes() -> int:
+        return sum(b.nbytes for b in _PARKED)
 
     @property
     def __cuda_array_interface__(self):
@@ -99,14 +128,21 @@ class DeviceBuffer:
         return t
 
     def free(self):
-        if self.ptr:
-            ptr, self.ptr = self.ptr, None
-            with torch.cuda.device(self.device):
-                self.na.check(self.L.fa_dev_free(ptr), "fa_dev_free")
+        """Release: an exported buffer is parked for reuse (never freed), any other freed."""
+        if not self.ptr:
+            return
+        if self.exported:
+            if self not in _PARKED:
+                _PARKED.append(self)
+            return
+        ptr, self.ptr = self.ptr, None
+        with torch.cuda.device(self.device):
+            self.na.check(self.L.fa_dev_free(ptr), "fa_dev_free")
 
     def __del__(self):
         try:
-            self.free()
+            if not self.exported:
+                self.free()
         except Exception:  # noqa: BLE001 - interpreter shutdown: nothing left to report to
             pass
 
@@ -203,16 +239,20 @@ class _RecvPool:
     """Receive buckets of the one-shot push, per (device, process group): each an allocation of
     its own (DeviceBuffer), exported once and mapped once by every peer, handed out to job after
     job (`take` / `give`: a few ms of collective set-up and token checks saved per job — the
-    bench's plan trials build a dozen jobs), and freed collectively: `shutdown_push(group)`
-    (call it before destroying the group) unmaps every peer's import, barriers, then frees; a
-    `take` that finds no free bucket large enough first retires the free ones (same protocol), so
-    the pool holds at most the buckets in use at once plus one.  Every rank takes and gives in the
+    bench's plan trials build a dozen jobs).  Released collectively: `shutdown_push(group)`
+    (call it before destroying the group) has every peer close its imports, then a barrier, and
+    the buckets are parked (DeviceBuffer: exported memory is never freed while the process lives
+    — freeing it is what made later imports map the wrong allocation) for
+    the next pool to re-export.  A `take` that finds no free bucket large enough first releases
+    the free ones (same protocol) and takes a parked or new one with 1/8 headroom, so the
+    buckets held stay near the largest set in use at once.  Every rank takes and gives in the
     same order, so the slots agree across ranks (checked at each take).
 
     Keyed by the group OBJECT (held, so its id cannot be reused by a later group): a destroyed and
     re-created default group gets a new pool.  A pool whose group was destroyed without
-    shutdown_push is dropped locally the next time any pool is looked up (imports closed, own
-    buckets freed: no barrier is possible any more; the token check guards later imports)."""
+    shutdown_push is dropped locally the next time any pool is looked up (imports closed with no
+    barrier possible any more — the unordered unmap the token check at the next set-up guards
+    against — buckets parked)."""
 
     _pools: dict = {}
 
@@ -236,13 +276,14 @@ class _RecvPool:
         return sum(s[0].nbytes for p in cls._pools.values() for s in p.slots)
 
     def _retire(self, pg, idx):
-        """Collective: unmap and free the slots `idx` (free on every rank, same indices)."""
+        """Collective: every rank closes its imports of the slots `idx`, a barrier, then the
+        buckets are parked (same indices on every rank)."""
         if not idx:
             return
         _unmap_all(pg.L, [b for i in idx for b in self.slots[i][3]], pg.group)
         for i in sorted(idx, reverse=True):
             buf = self.slots.pop(i)[0]
-            buf.free()
+            buf.free()  # exported: parked for reuse, never freed
 
     def take(self, pg, cols: int):
         i = next((j for j, s in enumerate(self.slots) if not s[4] and s[1].numel() >= cols), None)
@@ -252,14 +293,16 @@ class _RecvPool:
             raise RuntimeError(f"PushGather: the ranks' receive pools disagree ({picks})")
         if i is None:  # retire the free buckets that are too small, then a new one (collective)
             self._retire(pg, [j for j, s in enumerate(self.slots) if not s[4]])
-            buf = DeviceBuffer(max(cols, 4) * 4, self.device)
+            want = max(cols, 4)
+            buf = DeviceBuffer.get((want + want // 8 + ALIGN) // ALIGN * ALIGN * 4, self.device)
             view = buf.tensor(torch.float32)
             pg.full, pg.device = view, self.device
+            buf.exported = True  # from here on never freed: parked when released
             try:
                 bases, dsts, _stale = _map_peers(pg, view)
             except RuntimeError:
                 del view
-                buf.free()  # every peer closed its imports before _map_peers raised
+                buf.free()  # parked; every peer closed its imports (and barriered) before the raise
                 raise
             self.slots.append([buf, view, dsts, bases, False])
             i = len(self.slots) - 1
@@ -270,13 +313,13 @@ class _RecvPool:
         self.slots[i][4] = False
 
     def shutdown(self, pg):
-        """Collective: unmap every bucket on every rank, barrier, free."""
+        """Collective: unmap every bucket on every rank, barrier, park."""
         busy = [j for j, s in enumerate(self.slots) if s[4]]
         if busy:
             import warnings
 
             warnings.warn(f"shutdown_push: {len(busy)} receive bucket(s) still in use by a reducer that was "
-                          "not released; their results are freed too", stacklevel=3)
+                          "not released; their results are overwritten by the next push job", stacklevel=3)
         self._retire(pg, list(range(len(self.slots))))
 
     def _drop_local(self):
@@ -288,9 +331,10 @@ class _RecvPool:
 
 
 def shutdown_push(group=None, device=None):
-    """Collective over `group`: free the push gather's receive buckets of this process for that
-    group (every peer's mapping closed first, then a barrier, then each rank frees its own).
-    Call it before dist.destroy_process_group; the next push job maps fresh buckets."""
+    """Collective over `group`: release the push gather's receive buckets of this process for
+    that group — every peer's mapping closed, then a barrier, then each rank parks its own
+    (DeviceBuffer.get hands them to the next pool; exported memory is never freed).  Call it
+    before dist.destroy_process_group; the next push job maps its buckets afresh."""
     from . import _native as na
 
     g = _resolve_group(group)
@@ -323,10 +367,12 @@ class PushGather:
 
     def __init__(self, full: torch.Tensor | None, group=None, mode: str = "kernel", cols: int = 0, device=None):
         """full: the receive buffer to register (exported and mapped for this object, unmapped by
-        close(); prefer a DeviceBuffer's view: a caching-allocator tensor exports the whole
-        segment holding it); or None with `cols` / `device`: a bucket of at least `cols` fp32
-        columns from the process's receive pool (_RecvPool: an allocation of its own, mapped
-        once by every peer, reused until shutdown_push)."""
+        close()) — a DeviceBuffer (its fp32 view becomes `self.full`; once exported it is never
+        freed: `free()` parks it), or a tensor, whose whole caching-allocator segment is exported
+        (the caller must then keep that memory allocated for the process's lifetime: a freed
+        exported segment makes later imports unreliable); or None with
+        `cols` / `device`: a bucket of at least `cols` fp32 columns from the process's receive
+        pool (_RecvPool: mapped once by every peer, reused until shutdown_push)."""
         from . import _native as na
 
         if mode not in ("kernel", "dma"):
@@ -343,6 +389,9 @@ class PushGather:
             self.pool_slot, buf, self.dst = self.pool.take(self, cols)
             self.full, self.bases, self.stale = buf[:cols], [], []
         else:
+            if isinstance(full, DeviceBuffer):  # exported from here on: never freed (parked)
+                full.exported = True
+                self.owner, full = full, full.tensor(torch.float32)
             self.full, self.device = full, full.device
             self.bases, self.dst, self.stale = _map_peers(self, full)
         self.stream = torch.cuda.Stream(self.device)

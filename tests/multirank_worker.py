@@ -314,42 +314,48 @@ def case_sharded_reducer_push_dma(rank, world):
 
 
 def case_push_lifecycle(rank, world):
-    """The export -> map -> unmap -> free -> re-export sequence that produced round 4's stale
-    imports, driven deterministically 12 times each way: (a) pool buckets (an allocation of their
-    own each) taken, gathered into, released and freed by shutdown_push, then fresh ones; (b) an
-    explicitly registered DeviceBuffer bucket, closed (unmap + barrier) and freed, then the next
-    one, sizes cycling so freed addresses are reused.  Every set-up validates every mapping by its
-    token (`_map_peers` raises on any mismatch: a stale import fails the test), every gathered
-    bucket equals the all-gather's, and the registered bucket's head bytes survive the token."""
+    """The set-up / teardown sequences behind round 4's wrong buckets, driven deterministically 12
+    times each: (a) pool buckets taken, gathered into, released and parked by shutdown_push, then
+    the next pool's; (b) an explicitly registered DeviceBuffer, closed (unmap + barrier) and
+    parked, then the next one, sizes cycling so parked buckets are re-exported.  Every set-up
+    validates every mapping by its token (`_map_peers` raises on a mismatch: a wrong import fails
+    the test), every gathered bucket equals the all-gather's, the registered bucket's head bytes
+    survive the token, and exported memory is re-used, never freed."""
     from flearn_amd import dist as fd
 
     cuda = torch.device("cuda", 0)
+    pool_ptrs, own_ptrs = set(), set()
     for it in range(12):
         cols = world * (4096 + 1024 * (it % 3))
         src = torch.arange(cols // world, dtype=torch.float32, device=cuda) + 1e5 * rank + it
         want = torch.empty(cols, dtype=torch.float32, device=cuda)
         fd.all_gather_into(want, src)
-        # (a) the pool: a fresh bucket after every shutdown
+        # (a) the pool: buckets parked by shutdown_push, re-exported by the next pool
         pg = fd.PushGather(None, None, mode="kernel" if it % 2 == 0 else "dma", cols=cols, device=cuda)
         assert pg.stale == [] and fd._RecvPool.bytes_held() >= cols * 4
+        pool_ptrs.add(pg.full.data_ptr())
         pg.gather(src, rank * (cols // world))
         torch.cuda.synchronize()
         assert torch.equal(pg.full, want), (rank, it, "pool")
         pg.close()
         fd.shutdown_push()
-        assert fd._RecvPool.bytes_held() == 0
+        assert fd._RecvPool.bytes_held() == 0 and fd.DeviceBuffer.parked_bytes() > 0
         # (b) an explicit DeviceBuffer bucket, its head bytes preserved through registration
-        buf = fd.DeviceBuffer(cols * 4, cuda)
-        full = buf.tensor(torch.float32)
-        full.fill_(-7.0)
-        pe = fd.PushGather(full, None, mode="kernel")
+        buf = fd.DeviceBuffer.get(cols * 4, cuda)
+        buf.tensor(torch.float32)[:cols].fill_(-7.0)
+        pe = fd.PushGather(buf, None, mode="kernel")
+        full = pe.full[:cols]
+        assert buf.exported and full.data_ptr() == buf.ptr
+        own_ptrs.add(buf.ptr)
         assert pe.stale == [] and bool((full[:4] == -7.0).all())
         pe.gather(src, rank * (cols // world))
         torch.cuda.synchronize()
         assert torch.equal(full, want), (rank, it, "explicit")
-        pe.close()  # every peer unmapped (second barrier) before this rank frees
+        pe.close()  # every peer unmapped (second barrier) before this rank re-uses the bucket
         del full, pe
-        buf.free()
+        buf.free()  # exported: parked for the next registration, never freed
+    # three sizes cycling: the parked buckets came back instead of new allocations
+    assert len(pool_ptrs | own_ptrs) <= 6, (len(pool_ptrs), len(own_ptrs))
 
 
 CASES = {f.__name__[5:]: f for f in (case_avg_fixtures, case_setup_strategy, case_fused_rounds,

@@ -52,81 +52,104 @@ def rank_main(rank, world, port, args):
     keep = []
     try:
         for it in range(args.iters):
+            # every local step guarded, every collective always reached: one rank's failure is
+            # recorded, never a desynchronised collective
             cols = args.cols + (it % 5) * 65536 if args.sizes == "vary" else args.cols
-            own = None
-            if args.alloc == "own":
-                own = fd.DeviceBuffer(cols * 4, dev)
-                buf = own.tensor(torch.float32)
-            else:
-                buf = torch.empty(cols, dtype=torch.float32, device=dev)
-                if args.neighbours:  # other tensors sharing (and recycling) the segment
-                    keep.append(torch.empty(int(rng.integers(1, 4)) * 65536, dtype=torch.float32, device=dev))
-                    if len(keep) > 3:
-                        keep.pop(0)
-            tok = [rank, it, MAGIC, int(rng.integers(-2**31, 2**31 - 1))]
-            buf.view(torch.int32)[:4].copy_(torch.tensor(tok, dtype=torch.int32))
-            torch.cuda.synchronize(dev)
-            h, off = ctypes.create_string_buffer(64), ctypes.c_int64(0)
-            base, size = ctypes.c_void_p(), ctypes.c_int64(0)
-            rc_r = L.fa_mem_range(buf.data_ptr(), ctypes.byref(base), ctypes.byref(size))
-            rc_h = L.fa_ipc_handle(buf.data_ptr(), h, ctypes.byref(off))
-            hb = bytes(h.raw)
-            rec = {"it": it, "cols": cols, "ptr": hex(buf.data_ptr()), "base": hex(base.value or 0),
-                   "size": int(size.value), "offset": int(off.value), "handle": hb.hex(),
-                   "handle_seen_at": seen.get(hb), "peers": {}}
-            if rc_r or rc_h:  # e.g. hipIpcGetMemHandle refusing a re-allocated address: recorded
-                rec["export_error"] = L.fa_last_error().decode(errors="replace")
-            seen.setdefault(hb, it)
+            rec = {"it": it, "cols": cols, "peers": {}}
+            own = buf = None
+            mine = None
+            try:
+                if args.alloc == "own" and args.free == "reuse":
+                    if len(keep) < 3:
+                        keep.append(fd.DeviceBuffer(cols * 4, dev))
+                    buf = keep[it % 3].tensor(torch.float32)
+                elif args.alloc == "own":
+                    own = fd.DeviceBuffer(cols * 4, dev)
+                    buf = own.tensor(torch.float32)
+                    if args.free == "keep":
+                        keep.append(own)
+                        own = None
+                else:
+                    buf = torch.empty(cols, dtype=torch.float32, device=dev)
+                    if args.neighbours:  # other tensors sharing (and recycling) the segment
+                        keep.append(torch.empty(int(rng.integers(1, 4)) * 65536, dtype=torch.float32, device=dev))
+                        if len(keep) > 3:
+                            keep.pop(0)
+                tok = [rank, it, MAGIC, int(rng.integers(-2**31, 2**31 - 1))]
+                buf.view(torch.int32)[:4].copy_(torch.tensor(tok, dtype=torch.int32))
+                torch.cuda.synchronize(dev)
+                h, off = ctypes.create_string_buffer(64), ctypes.c_int64(0)
+                base, size = ctypes.c_void_p(), ctypes.c_int64(0)
+                rc_r = L.fa_mem_range(buf.data_ptr(), ctypes.byref(base), ctypes.byref(size))
+                rc_h = L.fa_ipc_handle(buf.data_ptr(), h, ctypes.byref(off))
+                hb = bytes(h.raw)
+                rec.update(ptr=hex(buf.data_ptr()), base=hex(base.value or 0), size=int(size.value),
+                           offset=int(off.value), handle=hb.hex(), handle_seen_at=seen.get(hb))
+                if rc_r or rc_h:  # e.g. hipIpcGetMemHandle refusing a re-allocated address
+                    rec["export_error"] = L.fa_last_error().decode(errors="replace")
+                else:
+                    seen.setdefault(hb, it)
+                    mine = (hb, int(off.value), tok)
+            except Exception as e:  # noqa: BLE001
+                rec["local_error"] = f"{type(e).__name__}: {e}"
             infos = [None] * world
-            dist.all_gather_object(infos, None if rc_h else (hb, int(off.value), tok), group=None)
+            dist.all_gather_object(infos, mine)
             opened = []
             for r, info in enumerate(infos):
                 if r == rank or info is None:
                     continue
                 phb, poff, ptok = info
-                pb = ctypes.c_void_p()
-                rc = L.fa_ipc_open(phb, ctypes.byref(pb))
-                if rc != 0 or not pb.value:
-                    rec["peers"][r] = {"open_error": L.fa_last_error().decode(errors="replace")}
-                    continue
-                opened.append(pb.value)
-                na.check(L.fa_copy_dma(probe.data_ptr(), pb.value + poff, 16, stream.cuda_stream), "fa_copy_dma")
-                stream.synchronize()
-                got = probe.tolist()
-                ent = {"mapped": hex(pb.value), "ok": got == ptok}
-                if got != ptok:
-                    ent["read"] = got
-                    if got[0] == r and got[2] == MAGIC:
-                        ent["stale_from_iteration"] = got[1]
-                rec["peers"][r] = ent
+                try:
+                    pb = ctypes.c_void_p()
+                    rc = L.fa_ipc_open(phb, ctypes.byref(pb))
+                    if rc != 0 or not pb.value:
+                        rec["peers"][r] = {"open_error": L.fa_last_error().decode(errors="replace")}
+                        continue
+                    opened.append(pb.value)
+                    na.check(L.fa_copy_dma(probe.data_ptr(), pb.value + poff, 16, stream.cuda_stream), "fa_copy_dma")
+                    stream.synchronize()
+                    got = probe.tolist()
+                    ent = {"mapped": hex(pb.value), "ok": got == ptok}
+                    if got != ptok:
+                        ent["read"] = got
+                        if got[2] == MAGIC:
+                            ent["stale_holds"] = {"rank": got[0], "iteration": got[1]}
+                    rec["peers"][r] = ent
+                except Exception as e:  # noqa: BLE001
+                    rec["peers"][r] = {"error": f"{type(e).__name__}: {e}"}
             dist.barrier()
             for b in opened:
-                na.check(L.fa_ipc_close(b), "fa_ipc_close")
+                if L.fa_ipc_close(b) != 0:
+                    rec.setdefault("close_errors", []).append(L.fa_last_error().decode(errors="replace"))
             if args.after_unmap == "barrier":
                 dist.barrier()
-            if args.alloc == "own":
+            try:
                 del buf
-                own.free()
-                own = None
-            else:
-                del buf
-                if args.free == "empty":
+                if own is not None:
+                    own.exported = args.free == "retire"
+                    own.free()
+                    own = None
+                elif args.free == "empty":
                     torch.cuda.empty_cache()
+            except Exception as e:  # noqa: BLE001
+                rec["free_error"] = f"{type(e).__name__}: {e}"
             log.append(rec)
         torch.cuda.synchronize(dev)
         dist.barrier()
     finally:
         Path(args.out).mkdir(parents=True, exist_ok=True)
         (Path(args.out) / f"rank{rank}.json").write_text(json.dumps(log, indent=1))
-        stale = [sum(1 for rec in log for p in rec["peers"].values() if not p.get("ok")),
-                 sum(1 for rec in log if "export_error" in rec)]
+        stale = {"stale_or_failed_mappings": sum(1 for rec in log for p in rec["peers"].values() if not p.get("ok")),
+                 "export_errors": sum(1 for rec in log if "export_error" in rec),
+                 "local_errors": sum(1 for rec in log if "local_error" in rec or "free_error" in rec),
+                 "iterations": len(log)}
         allr = [None] * world
         try:
             dist.all_gather_object(allr, stale)
         except Exception:  # noqa: BLE001 - the summary is best effort
             pass
         if rank == 0:
-            print(json.dumps({"variant": vars(args), "stale_mappings_and_export_errors_per_rank": allr}), flush=True)
+            print(json.dumps({"variant": vars(args), "per_rank": allr}), flush=True)
         dist.destroy_process_group()
 
 
@@ -137,7 +160,10 @@ def main():
     ap.add_argument("--cols", type=int, default=700_032)
     ap.add_argument("--alloc", choices=("torch", "own"), default="torch")
     ap.add_argument("--after-unmap", choices=("none", "barrier"), default="none")
-    ap.add_argument("--free", choices=("del", "empty"), default="del")
+    ap.add_argument("--free", choices=("del", "empty", "retire", "keep", "reuse"), default="del",
+                    help="retire (own): free with the addresses kept reserved (fa_dev_retire); keep (own): a "
+                         "new bucket each iteration, none ever freed; reuse (own): 3 buckets allocated once, "
+                         "iteration i re-exports bucket i %% 3 (the receive pool's pattern)")
     ap.add_argument("--sizes", choices=("fixed", "vary"), default="vary")
     ap.add_argument("--neighbours", action="store_true", help="torch: other tensors share the segments")
     ap.add_argument("--out", default="gpurun_out/ipc/probe")

@@ -62,30 +62,47 @@ def main():
         else:
             dsts = [torch.empty(n // 4, dtype=torch.float32, device=dev) for _ in range(args.legs)]
         ptrs = (ctypes.c_void_p * args.legs)(*[d.data_ptr() for d in dsts])
+        for path in ("engine", "blit"):
+            # engine: the product's legs (fa_copy_dma / fa_push_dma: hipMemcpyDeviceToDeviceNoCU);
+            # blit: the same copies through torch (hipMemcpyDeviceToDevice-style: a copy kernel)
+            def one(path=path):
+                if path == "engine":
+                    na.check(L.fa_copy_dma(dsts[0].data_ptr(), src.data_ptr(), n, main_s.cuda_stream), "fa_copy_dma")
+                else:
+                    with torch.cuda.stream(main_s):
+                        dsts[0].copy_(src, non_blocking=True)
 
-        def one():
-            na.check(L.fa_copy_dma(dsts[0].data_ptr(), src.data_ptr(), n, main_s.cuda_stream), "fa_copy_dma")
+            def all_legs(k=args.legs, path=path):
+                if path == "engine":
+                    na.check(L.fa_push_dma(src.data_ptr(), n, ptrs, k, handles, main_s.cuda_stream), "fa_push_dma")
+                    na.check(L.fa_stream_join(main_s.cuda_stream, handles, k), "fa_stream_join")
+                else:
+                    for i in range(k):
+                        streams[i].wait_stream(main_s)
+                        with torch.cuda.stream(streams[i]):
+                            dsts[i].copy_(src, non_blocking=True)
+                    for i in range(k):
+                        main_s.wait_stream(streams[i])
 
-        def all_legs(k=args.legs):
-            na.check(L.fa_push_dma(src.data_ptr(), n, ptrs, k, handles, main_s.cuda_stream), "fa_push_dma")
-            na.check(L.fa_stream_join(main_s.cuda_stream, handles, k), "fa_stream_join")
-
-        one()
-        all_legs()
-        t1 = timed(one, args.reps)
-        res = {"one_leg_ms": round(t1 * 1e3, 4), "one_leg_gbs": round(n / t1 / 1e9, 2)}
-        for k in sorted({2, 4, args.legs}):
-            if k > args.legs:
-                continue
-            tk = timed(lambda k=k: all_legs(k), args.reps)
-            res[f"legs{k}_ms"] = round(tk * 1e3, 4)
-            res[f"legs{k}_gbs_total"] = round(k * n / tk / 1e9, 2)
-            # 1.0: the legs took as long as one leg (fully concurrent AND not sharing a bottleneck);
-            # k: they took k times one leg (serial, or concurrent but sharing one link)
-            res[f"legs{k}_over_one"] = round(tk / t1, 3)
-        ok = all(torch.equal(d.to(dev) if kind == "pinned_host" else d, src) for d in dsts)
-        res["copies_correct"] = bool(ok)
-        out[kind] = res
+            one()
+            all_legs()
+            t1 = timed(one, args.reps)
+            res = {"one_leg_ms": round(t1 * 1e3, 4), "one_leg_gbs": round(n / t1 / 1e9, 2)}
+            for k in sorted({2, 4, args.legs}):
+                if k > args.legs:
+                    continue
+                tk = timed(lambda k=k: all_legs(k), args.reps)
+                res[f"legs{k}_ms"] = round(tk * 1e3, 4)
+                res[f"legs{k}_gbs_total"] = round(k * n / tk / 1e9, 2)
+                # 1.0: the legs took as long as one leg (concurrent, no shared bottleneck); k: k
+                # times one leg (serial, or concurrent but sharing one link)
+                res[f"legs{k}_over_one"] = round(tk / t1, 3)
+            torch.cuda.synchronize(dev)
+            ok = all(torch.equal(d.to(dev) if kind == "pinned_host" else d, src) for d in dsts)
+            for d in dsts:
+                d.zero_()
+            res["copies_correct"] = bool(ok)
+            out[f"{kind}_{path}"] = res
         del dsts
         torch.cuda.empty_cache()
     Path(args.out).parent.mkdir(parents=True, exist_ok=True)
