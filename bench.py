@@ -504,7 +504,9 @@ def plan_push(cfg, layout, n, args, world, rank, dev, g_eff, r_big_s):
     i = min(ok, key=lambda k: trials[k]["measured_ms"])
     g, widths, rep = cands[i]
     plan = ShardPlan.from_widths(p_real, g_eff, rank, widths, rep=rep)
-    info.update(_model_info(models[g], info["push_calibration" if g == "push" else "push_dma_calibration"], plan))
+    mi = _model_info(models[g], None, plan)
+    mi.pop("calibration")  # "calibration" stays RCCL's; the push forms' are push(_dma)_calibration
+    info.update(mi)
     info.update(plan_trials=trials, push_grid=grids[g] if g == "push" else None,
                 stripe_choice="push gathers' models, the fastest candidate over 5 measured steps each")
     return plan, g, info, trials[i]["measured_ms"] * 1e-3

@@ -48,7 +48,6 @@ EXPORTS = (
     "fa_ipc_close",
     "fa_dev_alloc",
     "fa_dev_free",
-    "fa_dev_retire",
     "fa_mem_range",
     "fa_push",
     "fa_copy_dma",
@@ -206,7 +205,6 @@ def load(require_gpu: bool = False):
                 "fa_ipc_close": ([P], ctypes.c_int),
                 "fa_dev_alloc": ([I64, ctypes.POINTER(P)], ctypes.c_int),
                 "fa_dev_free": ([P], ctypes.c_int),
-                "fa_dev_retire": ([P, I64, ctypes.POINTER(I32)], ctypes.c_int),
                 "fa_mem_range": ([P, ctypes.POINTER(P), ctypes.POINTER(I64)], ctypes.c_int),
                 "fa_push": ([P, I64, ctypes.POINTER(P), I32, I32, P], ctypes.c_int),
                 "fa_copy_dma": ([P, P, I64, P], ctypes.c_int),

@@ -788,32 +788,6 @@ int fa_dev_free(void* ptr) {
   return FA_OK;
 }
 
-int fa_dev_retire(void* ptr, int64_t nbytes, int32_t* va_kept) {
-  if (!va_kept) return fail(FA_ERR_ARG, "null va_kept");
-  *va_kept = 0;
-  if (!ptr) return FA_OK;
-  hipError_t e = hipFree(ptr);
-  if (e != hipSuccess) return fail(FA_ERR_LAUNCH, hipGetErrorString(e));
-  if (nbytes <= 0) return FA_OK;
-  // the freed range's addresses, reserved with no memory behind them for the process's lifetime:
-  // a later allocation (and so a later IPC export) can never land there again.  2-MiB rounded
-  // first (hipMalloc's fragment), then 4-KiB; a reservation that does not land on ptr is undone
-  for (const int64_t gran : {(int64_t)2 << 20, (int64_t)4 << 10}) {
-    const size_t sz = (size_t)((nbytes + gran - 1) / gran * gran);
-    void* r = nullptr;
-    if (hipMemAddressReserve(&r, sz, 0, ptr, 0) != hipSuccess || !r) {
-      (void)hipGetLastError();
-      continue;
-    }
-    if (r == ptr) {
-      *va_kept = 1;
-      return FA_OK;
-    }
-    (void)hipMemAddressFree(r, sz);
-  }
-  return FA_OK;
-}
-
 int fa_mem_range(const void* ptr, void** base, int64_t* size) {
   if (!ptr || !base || !size) return fail(FA_ERR_ARG, "null range argument");
   hipDeviceptr_t b = nullptr;

@@ -249,19 +249,13 @@ int fa_ipc_close(void* base);
 /* A receive bucket of its own: hipMalloc(nbytes) into *ptr (exceptions to "nothing here
  * allocates or frees").  An IPC export of a caching-allocator tensor names the whole segment
  * that holds it, shared with and recycled for other tensors; a bucket from fa_dev_alloc is
- * exactly one export, freed (fa_dev_free, NULL is a no-op; synchronises the device as hipFree
- * does) only after every peer has unmapped it (flearn_amd.dist: DESIGN.md section 6).  ABI 13. */
+ * exactly one export.  fa_dev_free (NULL is a no-op; synchronises the device as hipFree does) is
+ * for buckets that were never exported: on this runtime, freeing memory a peer has imported
+ * makes 13-34% of later imports map the wrong allocation, so flearn_amd.dist keeps exported
+ * buckets for the process's lifetime and re-exports them.  ABI 13.      */
 int fa_dev_alloc(int64_t nbytes, void** ptr);
 int fa_dev_free(void* ptr);
 
-/* Free an EXPORTED bucket for good: hipFree(ptr), then reserve its address range (no memory
- * behind it) for the process's lifetime, so no later allocation — and no later IPC export — can
- * land at that address again (*va_kept = 1; 0 when the range could not be reserved and the caller
- * must treat the address as burnt).  Why: the runtime's import of a handle whose exporter address
- * an importer has mapped before (after the exporter freed and re-allocated there) can resolve to
- * some other buffer — another process's, or the importer's own (DESIGN.md section 6,
- * tools/ipc_probe.py).  ABI 13.                                                               */
-int fa_dev_retire(void* ptr, int64_t nbytes, int32_t* va_kept);
 
 /* The device allocation holding ptr: *base and *size (hipMemGetAddressRange) — what
  * fa_ipc_handle exports for ptr.  ABI 13.                                                     */

@@ -126,7 +126,6 @@ def rank_main(rank, world, port, args):
             try:
                 del buf
                 if own is not None:
-                    own.exported = args.free == "retire"
                     own.free()
                     own = None
                 elif args.free == "empty":
@@ -160,10 +159,11 @@ def main():
     ap.add_argument("--cols", type=int, default=700_032)
     ap.add_argument("--alloc", choices=("torch", "own"), default="torch")
     ap.add_argument("--after-unmap", choices=("none", "barrier"), default="none")
-    ap.add_argument("--free", choices=("del", "empty", "retire", "keep", "reuse"), default="del",
-                    help="retire (own): free with the addresses kept reserved (fa_dev_retire); keep (own): a "
-                         "new bucket each iteration, none ever freed; reuse (own): 3 buckets allocated once, "
-                         "iteration i re-exports bucket i %% 3 (the receive pool's pattern)")
+    ap.add_argument("--free", choices=("del", "empty", "keep", "reuse"), default="del",
+                    help="keep (own): a new bucket each iteration, none ever freed; reuse (own): 3 buckets "
+                         "allocated once, iteration i re-exports bucket i %% 3 (the receive pool's pattern).  "
+                         "(The r05c 'retire' variants — hipFree, then the freed range reserved with "
+                         "hipMemAddressReserve — ran on commit 10346de's fa_dev_retire, since removed)")
     ap.add_argument("--sizes", choices=("fixed", "vary"), default="vary")
     ap.add_argument("--neighbours", action="store_true", help="torch: other tensors share the segments")
     ap.add_argument("--out", default="gpurun_out/ipc/probe")

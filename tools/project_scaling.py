@@ -96,11 +96,16 @@ def push_contention(ingress_bs: float, path=PUSH_PROBE):
 
 
 def project(cfg: str, g: int, link_bs: float, launch_s=10e-6, collective_s=30e-6, tail=True, contended=False,
-            push=False, barrier_s=15e-6, dma=False):
+            push=False, barrier_s=15e-6, dma=False, dma_egress_bs=None):
     """push: the one-shot push gather (flearn_amd.dist.PushGather) — a launch per stripe instead
     of a collective, two barriers per step, and local HBM traffic of ingress * (1 + 1/(G-1))
-    (received bytes written, the own slice read once) instead of a ring's ~2 x ingress."""
+    (received bytes written, the own slice read once) instead of a ring's ~2 x ingress.
+    dma_egress_bs (with dma): what the copy engines that run at once move out of one GPU in all
+    (round 5, tools/probe_dma_legs.py: ~140 GB/s for 7 legs — 2.3 engines' worth at 60 GB/s
+    each); every leg then gets min(link, egress / (G-1))."""
     n, p = CONFIGS[cfg]
+    if push and dma and dma_egress_bs and g > 1:
+        link_bs = min(link_bs, dma_egress_bs / (g - 1))
     t1 = one_gpu_step(cfg)
     local = -(-p // g)
     local = -(-local // ALIGN) * ALIGN
@@ -135,10 +140,14 @@ def main():
     ap.add_argument("--no-tail", action="store_true", help="stripes only (no replicated tail)")
     ap.add_argument("--push", action="store_true", help="the one-shot push gather instead of RCCL's all-gather")
     ap.add_argument("--dma", action="store_true", help="with --push: its copy-engine form (one leg per peer)")
+    ap.add_argument("--dma-egress-gbs", type=float, default=None,
+                    help="with --push --dma: the copy engines' total egress per GPU (measured: ~140)")
     ap.add_argument("--contended", action="store_true",
                     help="reduce / gather slowed by the measured one-GPU contention (profiles/r04/overlap)")
     a = ap.parse_args()
-    rows = [project(c, g, float(l) * 1e9, tail=not a.no_tail, contended=a.contended, push=a.push, dma=a.dma)
+    egress = a.dma_egress_gbs * 1e9 if a.dma_egress_gbs else None
+    rows = [project(c, g, float(l) * 1e9, tail=not a.no_tail, contended=a.contended, push=a.push, dma=a.dma,
+                    dma_egress_bs=egress)
             for l in a.link_gbs.split(",") for c in CONFIGS for g in (2, 4, 8)]
     if a.json:
         print(json.dumps(rows, indent=1))
