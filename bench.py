@@ -1018,7 +1018,11 @@ def main():
         dist.barrier()
 
     # ---- phase 2: the one-shot push gathers, bounded; adopted only if faster AND verified ------
-    if world > 1 and args.gather != "rccl":
+    # (not when the RCCL job failed its self-check: that line stands, and the run exits non-zero)
+    rccl_failed = check is not None and not check["verified"]
+    if rccl_failed and g_eff > 1:
+        line["multi_gpu"]["phases"]["push"] = {"status": "skipped: the RCCL job failed its self-check"}
+    if world > 1 and args.gather != "rccl" and not rccl_failed:
         t_phase = time.perf_counter()
         ph = {"status": "started", "budget_s": args.push_budget_s}
         line["multi_gpu"]["phases"]["push"] = ph
@@ -1090,7 +1094,7 @@ def main():
         dog.disarm()
 
     # ---- phase 3: the weak job beside it, the loopback drop-in — each bounded -------------------
-    if g_eff > 1 and not args.no_weak and emu is None:
+    if g_eff > 1 and not args.no_weak and emu is None and not rccl_failed:
         def weak_overran(ln):
             ln["weak"] = {"status": "timed_out", "budget_s": args.phase_budget_s}
 
@@ -1117,7 +1121,7 @@ def main():
         dist.barrier()
         dist.destroy_process_group()
     loop = None
-    if world > 1 and rank == 0 and not args.no_loopback:
+    if world > 1 and rank == 0 and not args.no_loopback and not rccl_failed:
         # the single-process multi-GPU drop-in (flearn's Communicator collects every upload in one
         # process): rank 0 alone, after the process group is gone, drives every GPU of the node
         ndev = max(torch.cuda.device_count(), 1)

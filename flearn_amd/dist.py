@@ -208,7 +208,7 @@ def _map_peers(pg, full: torch.Tensor):
     if not agreed:
         for b in bases:
             L.fa_ipc_close(b)
-        dist.barrier(group=pg.group)  # nobody frees or re-exports while a peer still maps it
+        dist.barrier(group=pg.group)  # nobody exports again while a peer is still closing
         err = L.fa_last_error()
         why = (f" (here: the mappings of ranks {stale} did not hold their tokens)" if stale else
                f" (here: {err.decode(errors='replace')})" if err and not ok else "")
@@ -217,8 +217,9 @@ def _map_peers(pg, full: torch.Tensor):
 
 
 def _unmap_all(L, bases, group):
-    """Collective: close this rank's imports, then a barrier — after it no peer maps any bucket
-    that was mapped before, so an owner may free (and later re-export) its memory."""
+    """Collective: close this rank's imports, then a barrier — after it no peer is still closing
+    an import when any rank exports again (exporting while a peer closes made a third of the
+    probe's imports map the wrong allocation: DESIGN.md section 6)."""
     for b in bases:
         L.fa_ipc_close(b)
     dist.barrier(group=group)

@@ -156,7 +156,9 @@ def test_bench_fails_on_a_misplaced_gather(cuda):
     assert len(lines) == 1
     d = json.loads(lines[0])
     assert d["verify"]["verified"] is False and d["verify"]["mismatched_windows"] > 0
-    assert verify.EXIT_MISMATCH == 3
+    # a failed RCCL line is never replaced by a later (push) phase
+    assert d["multi_gpu"]["gather"] == "rccl" and d["multi_gpu"]["phases"]["push"]["status"].startswith("skipped")
+    assert "exitcode  : 3" in p.stderr and verify.EXIT_MISMATCH == 3  # each rank's status (torchrun exits 1)
 
 
 def test_single_gpu_line_is_verified(cuda):

@@ -15,3 +15,5 @@ timeout -k 10 300 python3 bench.py > $O/bench_ns.json 2> $O/bench_ns.err || { ec
 cat $O/bench_ns.json
 FLEARN_BENCH_BACKEND=gloo MASTER_ADDR=127.0.0.1 timeout -k 10 400 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node=2 --master-addr=127.0.0.1 --master-port=29533 bench.py --gpus 2 --steps 5 --warmup 2 --config ns > $O/rehearsal_ns_g2.json 2> $O/rehearsal_ns_g2.err || { echo rehearsal failed; tail $O/rehearsal_ns_g2.err; exit 1; }
 echo rehearsal-ok
+timeout -k 10 300 python3 tools/probe_c5_shape.py --reps 5 > $O/c5_shape.json 2> $O/c5_shape.err || { echo c5 probe failed; tail $O/c5_shape.err; exit 1; }
+cat $O/c5_shape.json
