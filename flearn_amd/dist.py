@@ -294,6 +294,9 @@ class _RecvPool:
             raise RuntimeError(f"PushGather: the ranks' receive pools disagree ({picks})")
         if i is None:  # retire the free buckets that are too small, then a new one (collective)
             self._retire(pg, [j for j, s in enumerate(self.slots) if not s[4]])
+            if torch.device(self.device).type != "cuda":  # refused on every rank together
+                pg.device = torch.device(self.device)
+                _map_peers(pg, torch.empty(4))
             want = max(cols, 4)
             buf = DeviceBuffer.get((want + want // 8 + ALIGN) // ALIGN * ALIGN * 4, self.device)
             view = buf.tensor(torch.float32)
