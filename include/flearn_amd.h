@@ -269,10 +269,10 @@ int fa_mem_range(const void* ptr, void** base, int64_t* size);
  * on 1024 blocks slowed the reduce 1.8x on one GPU).  ABI 10 adds `grid`. */
 int fa_push(const void* src, int64_t nbytes, void* const* dsts, int32_t n_dsts, int32_t grid, void* stream);
 
-/* hipMemcpyAsync(dst, src, nbytes, device-to-device) on `stream`: between two GPUs' memories
- * (a peer bucket mapped with fa_ipc_open) the runtime drives it with a copy engine, so a push
- * leg costs the reduce no CUs and no memory-pipeline slots (the copy-engine form of the one-shot
- * all-gather: one stream per peer).  ABI 11.                                                  */
+/* hipMemcpyAsync(dst, src, nbytes, hipMemcpyDeviceToDeviceNoCU) on `stream`: a copy-engine
+ * transfer, so a push leg costs the reduce no CUs (the copy-engine form of the one-shot
+ * all-gather: one stream per peer).  Round 5: with plain hipMemcpyDeviceToDevice the runtime ran
+ * these copies as blit kernels on the compute queues (rocprofv3).  ABI 11. */
 int fa_copy_dma(void* dst, const void* src, int64_t nbytes, void* stream);
 
 /* The copy-engine push leg of one stripe in one call: after the work queued so far on `stream`,

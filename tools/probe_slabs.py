@@ -35,12 +35,14 @@ def main():
     ap.add_argument("--slabs", default="1,2,3,4,8")
     ap.add_argument("--allocs", type=int, default=2)
     ap.add_argument("--reps", type=int, default=7)
+    ap.add_argument("--windows", action="store_true",
+                    help="keep the [N][P] stack (pitch P) and split only the launches into S column windows")
     a = ap.parse_args()
     L = na.lib()
     dev = torch.device("cuda", 0)
     n, p = a.clients, a.params
     slabs = [int(x) for x in a.slabs.split(",")]
-    res = {"clients": n, "params": p, "op": a.op, "by_slabs": {}}
+    res = {"clients": n, "params": p, "op": a.op, "mode": "windows" if a.windows else "slabs", "by_slabs": {}}
     stride_max = -(-p // 64) * 64
     for alloc in range(a.allocs):
         buf = torch.empty(n * stride_max + 64 * max(slabs) * n, dtype=torch.float32, device=dev)
@@ -48,6 +50,7 @@ def main():
         prev = [torch.empty(stride_max, dtype=torch.float32, device=dev) for _ in range(2)]
         v = [torch.zeros(stride_max, dtype=torch.float64, device=dev) for _ in range(2)]
         agg.fill_uniform(prev[0][None], seed=1)
+        stack = buf[: n * stride_max].view(n, stride_max)  # the plain [N][P] stack (pitch P)
         layouts = {}
         for S in slabs:
             width = -(-(-(-p // S)) // 64) * 64  # columns per slab, ALIGN-rounded
@@ -58,7 +61,10 @@ def main():
                 wc = max(0, min(width, p - c0))
                 if wc == 0:
                     break
-                views.append((buf[off : off + n * width].view(n, width), c0, wc))
+                if a.windows:  # S launches over column windows of the ONE [N][P] stack
+                    views.append((stack[:, c0 : c0 + width] if c0 + width <= stride_max else stack[:, c0:], c0, wc))
+                else:
+                    views.append((buf[off : off + n * width].view(n, width), c0, wc))
                 off += n * width
             layouts[S] = views
 
@@ -90,12 +96,12 @@ def main():
         alg = n * p * 4 + p * 4 + (0 if a.op == "mean" else p * 4 + 2 * p * 8)
         for S in slabs:
             t = float(np.median(times[S]))
-            d = res["by_slabs"].setdefault(str(S), {"pitch_mb": round(layouts[S][0][0].shape[1] * 4 / 1e6, 1), "us": [],
+            d = res["by_slabs"].setdefault(str(S), {"pitch_mb": round(layouts[S][0][0].stride(0) * 4 / 1e6, 1), "us": [],
                                                     "frac": []})
             d["us"].append(round(t, 1))
             d["frac"].append(round(alg / t / 8e6, 4))
         print(json.dumps(res), file=sys.stderr, flush=True)
-        del buf, layouts
+        del buf, layouts, stack
         torch.cuda.empty_cache()
     print(json.dumps(res))
 
