@@ -817,12 +817,16 @@ def build_line(args, cfg, world, g_eff, emu, main_n, job, step_s, wall, info, ch
     plan, cols = job.plan, job.plan.local_cols
     job_bytes = algorithmic_bytes(main_n, layout_p, cfg["op"]) if not emu else algorithmic_bytes(main_n, cols, cfg["op"])
     value = job_bytes / GIB / step_s
-    launch_bytes = algorithmic_bytes(main_n, cols, cfg["op"])
+    # fa_reduce_f32 may run a wide window as several launches of consecutive column windows
+    # (fa_reduce_windows): the per-launch bytes and time are the step's divided by that count
+    launches = max(1, na.lib().fa_reduce_windows(na.OP_BY_NAME[cfg["op"]], cols))
+    launch_bytes = algorithmic_bytes(main_n, cols, cfg["op"]) // launches
+    launch_s = launch_s / launches
     achieved = launch_bytes / 1e9 / launch_s
     traffic, traffic_src = load_traffic(args.config) if g_eff == 1 else (None, None)
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "bytes_per_launch": launch_bytes,
-                "launch_us": round(launch_s * 1e6, 2)}
+                "launch_us": round(launch_s * 1e6, 2), "launches_per_step": launches}
     if traffic_src:
         roofline["traffic_source"] = traffic_src
     weak_main = args.scaling == "weak" and g_eff > 1

@@ -54,6 +54,7 @@ EXPORTS = (
     "fa_push_dma",
     "fa_stream_join",
     "fa_set_reduce_grid",
+    "fa_reduce_windows",
     "fa_b64_decoded_size",
     "fa_b64_decode",
     "fa_b64_decode_ranges",
@@ -211,6 +212,7 @@ def load(require_gpu: bool = False):
                 "fa_push_dma": ([P, I64, ctypes.POINTER(P), I32, ctypes.POINTER(P), P], ctypes.c_int),
                 "fa_stream_join": ([P, ctypes.POINTER(P), I32], ctypes.c_int),
                 "fa_set_reduce_grid": ([I32], ctypes.c_int),
+                "fa_reduce_windows": ([I32, I64], ctypes.c_int),
                 "fa_b64_decoded_size": ([P, I64], I64),
                 "fa_b64_decode": ([P, I64, P, I64, I32], ctypes.c_int),
                 "fa_b64_decode_ranges": ([P, I64, I32, P, P, P, I32], ctypes.c_int),

@@ -181,8 +181,8 @@ int kg_for(int64_t k) {
 }
 
 template <class P, typename T, int OP>
-int launch_reduce(const typename P::x_t* stack, int64_t stride, int n, const void* w, int64_t col0,
-                  int64_t ncols, const Epi<T>& e, hipStream_t s) {
+int launch_reduce_window(const typename P::x_t* stack, int64_t stride, int n, const void* w, int64_t col0,
+                         int64_t ncols, const Epi<T>& e, hipStream_t s) {
   const typename P::w_t* wt = static_cast<const typename P::w_t*>(w);
   const int cus = device_cus();
   const int64_t chunks = ((ncols + 3) / 4 + 63) / 64;  // 1-KiB row pieces
@@ -257,6 +257,49 @@ int launch_reduce(const typename P::x_t* stack, int64_t stride, int n, const voi
                        col0, ncols, e);
     return launch_check();
   }
+}
+
+// Wide fp32 windows as several launches over consecutive column windows of the same stack
+// (round 5, tools/probe_slabs.py --windows, profiles/r05/c5/: same stack, same allocation,
+// interleaved rounds, two allocations each).  Each window gets its own row-major geometry (grid,
+// KG, groups per block), and these splits measured faster than one launch: fused epilogues at
+// 16 M+ columns in 3 windows — FedOPT-Adagrad 100 x 86.6 M 5282/5270 -> 5190/5211 us, FedAVGM
+// 100 x 86.6 M 5260/5249 -> 5177/5183, FedAVGM 100 x 25.6 M 1561/1564 -> 1542/1544 (2 windows:
+// 1574/1572, slower); plain means of 8-16 M columns in 2 — 100 x 11.7 M 666/665 -> 660/661,
+// 1000 x 11.7 M 6481/6486 -> 6441/6437 (3 windows: 6545).  The plain mean of 25.6 M (NS) stays
+// one launch (2 windows 0.2-0.4% slower), as does 86.6 M (no consistent gain).  Per column the
+// sums and epilogue are unchanged: bit-identical results.  Not with a forced grid (ABI 7).
+template <int OP>
+int window_count(int64_t ncols) {
+  if (OP != FA_OP_MEAN) return ncols >= ((int64_t)16 << 20) ? 3 : 1;
+  return (ncols >= ((int64_t)8 << 20) && ncols < ((int64_t)16 << 20)) ? 2 : 1;
+}
+
+template <typename T>
+Epi<T> epi_at(const Epi<T>& e, int64_t c) {  // the epilogue's per-column arrays from column c on
+  Epi<T> o = e;
+  if (o.prev) o.prev += c;
+  if (o.v) o.v += c;
+  if (o.v_out) o.v_out += c;
+  if (o.h) o.h += c;
+  if (o.out32) o.out32 += c;
+  if (o.out64) o.out64 += c;
+  return o;
+}
+
+template <class P, typename T, int OP>
+int launch_reduce(const typename P::x_t* stack, int64_t stride, int n, const void* w, int64_t col0,
+                  int64_t ncols, const Epi<T>& e, hipStream_t s) {
+  int S = 1;
+  if constexpr (sizeof(typename P::x_t) == 4 && sizeof(typename P::acc_t) == 4)
+    if (g_reduce_grid.load(std::memory_order_relaxed) <= 0) S = window_count<OP>(ncols);
+  if (S <= 1) return launch_reduce_window<P, T, OP>(stack, stride, n, w, col0, ncols, e, s);
+  const int64_t width = (ncols + S - 1) / S / 256 * 256 + 256;  // 1-KiB chunks of a row: 16-B aligned
+  for (int64_t c = 0; c < ncols; c += width) {
+    const int64_t wc = ncols - c < width ? ncols - c : width;
+    if (int rc = launch_reduce_window<P, T, OP>(stack, stride, n, w, col0 + c, wc, epi_at(e, c), s)) return rc;
+  }
+  return FA_OK;
 }
 
 // Segmented row-pointer reduce (fa_reduce_f32_rows): reduce_kernel_segrows_rm — blocks claim
@@ -713,6 +756,17 @@ int fa_gather_rows_f64(double* stack, int64_t row_stride, int32_t n_clients, con
     if (int rc = launch_check()) return rc;
   }
   return FA_OK;
+}
+
+int fa_reduce_windows(int32_t op, int64_t n_cols) {
+  if (n_cols < 0) return fail(FA_ERR_ARG, "negative n_cols");
+  if (g_reduce_grid.load(std::memory_order_relaxed) > 0) return 1;
+  switch (op) {
+    case FA_OP_MEAN: return window_count<FA_OP_MEAN>(n_cols);
+    case FA_OP_AVGM: case FA_OP_ADAGRAD: case FA_OP_YOGI: case FA_OP_ADAM: case FA_OP_DYN:
+      return window_count<FA_OP_AVGM>(n_cols);
+    default: return fail(FA_ERR_ARG, "unknown epilogue op");
+  }
 }
 
 int fa_set_reduce_grid(int32_t grid) {

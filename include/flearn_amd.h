@@ -218,6 +218,13 @@ int fa_fill_uniform_f32(float* dst, int64_t row_stride, int32_t n_rows, int64_t 
  * scheduling knob of this engine (the reference has one CPU thread).                         */
 int fa_set_reduce_grid(int32_t grid);
 
+/* How many launches fa_reduce_f32 makes for an fp32-sum window (modes FA_MODE_W32_DIV64 /
+ * _DIV32; FA_MODE_W64 is always one) of n_cols columns with epilogue `op` (FA_OP_*): wide windows run as consecutive column windows, each with its own geometry
+ * (fused epilogues at >= 16 Mi columns in 3, plain means of 8-16 Mi columns in 2; 1 with a
+ * forced grid) — measured faster, bit-identical (DESIGN.md section 4 finding 26).  For callers
+ * that time or profile per launch.  FA_ERR_ARG for an unknown op.  ABI 13.                    */
+int fa_reduce_windows(int32_t op, int64_t n_cols);
+
 /* Copy nbytes from src to dst with a kernel on `stream` (both 16-byte aligned; either may be
  * pinned host memory mapped into the GPU's address space).  For a device result going to a
  * pinned host buffer the kernel's stores cross PCIe at ~53 GB/s where the copy engine's D2H

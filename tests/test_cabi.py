@@ -285,3 +285,24 @@ def test_reduce_grid_knob(L):
     assert L.fa_set_reduce_grid(224) == 160
     assert L.fa_set_reduce_grid(-1) == header_define("FA_ERR_ARG")
     assert L.fa_set_reduce_grid(0) == 224
+
+
+def test_reduce_window_count(L):
+    """fa_reduce_windows (host): how many launches fa_reduce_f32 makes — fused epilogues at
+    >= 16 Mi columns in 3 windows, plain means of 8-16 Mi columns in 2, else 1 (DESIGN.md §4
+    finding 26); one with a forced grid; unknown ops refused."""
+    mean, avgm, adagrad = na.OP_MEAN, na.OP_AVGM, na.OP_ADAGRAD
+    assert L.fa_reduce_windows(mean, 25_610_152) == 1  # NS
+    assert L.fa_reduce_windows(mean, 11_699_112) == 2  # C2 / C4
+    assert L.fa_reduce_windows(mean, 86_567_656) == 1
+    assert L.fa_reduce_windows(mean, 44_426) == 1  # LeNet5
+    assert L.fa_reduce_windows(avgm, 25_610_152) == 3  # C3
+    assert L.fa_reduce_windows(adagrad, 86_567_656) == 3  # C5
+    assert L.fa_reduce_windows(adagrad, (16 << 20) - 64) == 1
+    assert L.fa_reduce_windows(na.OP_DYN, 16 << 20) == 3
+    assert L.fa_reduce_windows(99, 1000) == header_define("FA_ERR_ARG")
+    prev = L.fa_set_reduce_grid(128)
+    try:
+        assert L.fa_reduce_windows(adagrad, 86_567_656) == 1
+    finally:
+        L.fa_set_reduce_grid(prev)
