@@ -30,8 +30,12 @@ CONFIGS = {
 
 
 def one_gpu_step(cfg: str) -> float:
-    d = json.loads((REPO / "profiles" / "r03" / "final" / cfg / f"bench_{cfg}.json").read_text())
-    return d["ms_per_step"] / 1e3
+    """The newest profile pass's 1-GPU step (profiles/r05/final, else r03)."""
+    for rnd in ("r05", "r03"):
+        f = REPO / "profiles" / rnd / "final" / cfg / f"bench_{cfg}.json"
+        if f.exists():
+            return json.loads(f.read_text())["ms_per_step"] / 1e3
+    raise FileNotFoundError(cfg)
 
 
 OVERLAP = (REPO / "profiles" / "r04" / "overlap" / "overlap.json",
