@@ -559,6 +559,10 @@ def run_job(cfg, layout, n, args, world, rank, dev, g_eff, gather: str = "rccl")
     else:
         plan, gather, info, _best = plan_push(cfg, layout, n, args, world, rank, dev, g_eff, 0.0)
         push_grid = info.get("push_grid") or 0
+        if plan is None:  # no push form available for this job: RCCL's all-gather
+            plan, rinfo, _best = plan_rccl(cfg, layout, n, args, world, rank, dev, g_eff)
+            info = {**info, **rinfo, "push_unavailable": True}
+            gather, push_grid = "rccl", 0
     job, step_s, wall, tinfo = timed_job(cfg, layout, n, plan, gather, push_grid, args, world, dev, g_eff)
     info.update(tinfo)
     return job, step_s, wall, info
@@ -1121,7 +1125,7 @@ def main():
     if world > 1:
         if job is not None and job.red is not None:
             job.red.release()  # collective: the bucket back to the pool while the group exists
-        fa_dist.shutdown_push()  # every peer unmaps, then the receive buckets are freed
+        fa_dist.shutdown_push()  # every peer unmaps, then the receive buckets are parked
         dist.barrier()
         dist.destroy_process_group()
     loop = None
