@@ -974,8 +974,10 @@ __device__ __forceinline__ const float* srm_row_ptr(const float* const* lds_row,
   }
 }
 
+// XLS: the epilogue's f64 stores as whole cache lines (buf_store_tquad XL, 2 KiB of LDS per wave),
+// as rowmajor_group does for fused epilogues at KG <= 3 (DESIGN.md §4 finding 22).
 template <class P, typename T, int OP, int V, int W, int KG, int DN, bool NT, bool TR = false, int DS = 1,
-          bool SG = false, int PFA = 0, int LT = 0>
+          bool SG = false, int PFA = 0, int LT = 0, bool XLS = false>
 __global__ __launch_bounds__(64 * W) void reduce_kernel_segrows_rm(const float* const* __restrict__ rows, int n,
                                                                    const typename P::w_t* __restrict__ w,
                                                                    const fa_piece* __restrict__ pieces,
@@ -1089,7 +1091,7 @@ __global__ __launch_bounds__(64 * W) void reduce_kernel_segrows_rm(const float* 
         asm volatile("" ::"v"(sink));
       }
 #pragma unroll
-      for (int j = 0; j < KG; ++j) finish_piece<T, OP, A, V, 64 * W, (V >= 2 ? 2 : V)>(e, col[j] / 4, cols[j], acc[j]);
+      for (int j = 0; j < KG; ++j) finish_piece<T, OP, A, V, 64 * W, (V >= 2 ? 2 : V), XLS>(e, col[j] / 4, cols[j], acc[j]);
     } else {
       const fa_piece pc = pieces[nwide + (t - groups)];
       const float* const* rp = rows + (int64_t)pc.seg * n;
@@ -1098,11 +1100,11 @@ __global__ __launch_bounds__(64 * W) void reduce_kernel_segrows_rm(const float* 
       if (((pc.n_cols + 3) >> 2) > 64 * W) {  // a wide piece the groups did not take
         AV acc[V];
         rows_sweep<P, V, 1, W, NT>(row, bytes, n, w, acc);
-        finish_piece<T, OP, A, V, 64 * W, (V >= 2 ? 2 : V)>(e, pc.col / 4, pc.n_cols, acc);
+        finish_piece<T, OP, A, V, 64 * W, (V >= 2 ? 2 : V), XLS>(e, pc.col / 4, pc.n_cols, acc);
       } else if (pc.n_cols > 0) {
         AV acc[1];
         rows_sweep<P, 1, DN, W, NT>(row, bytes, n, w, acc);
-        finish_piece<T, OP, A, 1, 64 * W, 1>(e, pc.col / 4, pc.n_cols, acc);
+        finish_piece<T, OP, A, 1, 64 * W, 1, XLS>(e, pc.col / 4, pc.n_cols, acc);
       }
     }
     if (threadIdx.x == 0) s_next = claimed;

@@ -159,3 +159,26 @@ extern "C" int tune_rows_rm_trace(const float* const* rows, int n, const float* 
                      dim3(512), 0, s, rows, n, w, pieces, npieces, work, e);
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }
+
+// fused FedAVGM through the product's row-pointer geometry (V8 W8 KG2, DN16), f64 state, with
+// (xl = 1) or without whole-line f64 stores (round 5: tools/probe_rows_xl.py)
+extern "C" int tune_rows_rm_avgm(int xl, const float* const* rows, int n, const float* w, const fa_piece* pieces,
+                                 int64_t npieces, int grid, int* work, double denom, const float* prev, double* v,
+                                 double* v_out, float* out32, void* stream) {
+  Epi<double> e{};
+  e.denom = denom;
+  e.prev = prev;
+  e.v = v;
+  e.v_out = v_out;
+  e.out32 = out32;
+  e.beta = 0.9;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (hipMemsetAsync(work, 0, sizeof(int), s) != hipSuccess) return -3;
+  if (xl)
+    hipLaunchKernelGGL((reduce_kernel_segrows_rm<AccF32, double, FA_OP_AVGM, 8, 8, 2, 16, true, false, 1, false, 0, 0, true>),
+                       dim3((unsigned)grid), dim3(512), 0, s, rows, n, w, pieces, npieces, work, e);
+  else
+    hipLaunchKernelGGL((reduce_kernel_segrows_rm<AccF32, double, FA_OP_AVGM, 8, 8, 2, 16, true, false, 1, false, 0, 0, false>),
+                       dim3((unsigned)grid), dim3(512), 0, s, rows, n, w, pieces, npieces, work, e);
+  return hipGetLastError() == hipSuccess ? 0 : -3;
+}
