@@ -320,8 +320,11 @@ int launch_segrows(const float* const* rows, int n, const void* w, const fa_piec
   const typename P::w_t* wt = static_cast<const typename P::w_t*>(w);
   // f64 sums (np.float64 weights) need twice the accumulator registers: one piece per group
   constexpr int KG = sizeof(typename P::acc_t) == 8 ? 1 : kSegKG;
-  hipLaunchKernelGGL((reduce_kernel_segrows_rm<P, T, OP, kSegV, kSegW, KG, 16, kNT>), dim3((unsigned)grid),
-                     dim3(64 * kSegW), 0, s, rows, n, wt, pieces, npieces, work, e);
+  // fused f64 state: whole-line stores (FedAVGM 100 x ResNet-50 uploads in place 1647.6 -> 1633.8 us,
+  // bit-identical: tools/probe_rows_xl.py, profiles/r05/rows_xl/)
+  constexpr bool XLS = sizeof(T) == 8 && OP != FA_OP_MEAN;
+  hipLaunchKernelGGL((reduce_kernel_segrows_rm<P, T, OP, kSegV, kSegW, KG, 16, kNT, false, 1, false, 0, 0, XLS>),
+                     dim3((unsigned)grid), dim3(64 * kSegW), 0, s, rows, n, wt, pieces, npieces, work, e);
   return launch_check();
 }
 
