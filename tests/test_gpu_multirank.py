@@ -74,11 +74,11 @@ def test_sharded_reducer_hip_ranks(world, cuda):
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("world", [2, 3, 4])
+@pytest.mark.parametrize("world", [2, 3, 4, 8])
 def test_sharded_reducer_push_gather(world, cuda):
     """ShardedReducer reassembled by PushGather: IPC-mapped peer buffers and one fa_push kernel
     per stripe, or one copy-engine copy per peer (here every "peer" is another process on the
-    same GPU), bit-exact."""
+    same GPU), bit-exact; world 8 = MAX_PUSH_RANKS, one MI355X node."""
     _run_ranks(world, ["sharded_reducer_push", "sharded_reducer_push_dma"])
 
 
