@@ -954,13 +954,20 @@ def main():
                     help="N>1: how stripes are reassembled — RCCL's all-gather, the one-shot push over "
                          "xGMI by kernel stores or by copy engines (flearn_amd.dist.PushGather), or "
                          "whichever measures fastest.  The RCCL job is always timed and verified first")
-    ap.add_argument("--push-budget-s", type=float, default=float(os.environ.get("FLEARN_BENCH_PUSH_BUDGET_S", 150)),
+    ap.add_argument("--push-budget-s", type=float, default=float(os.environ.get("FLEARN_BENCH_PUSH_BUDGET_S", 120)),
                     help="N>1: wall-clock budget of the push phase (set-up, calibration, trials, job)")
-    ap.add_argument("--phase-budget-s", type=float, default=float(os.environ.get("FLEARN_BENCH_PHASE_BUDGET_S", 150)),
+    ap.add_argument("--phase-budget-s", type=float, default=float(os.environ.get("FLEARN_BENCH_PHASE_BUDGET_S", 120)),
                     help="N>1: budget of the weak job and of the loopback, each")
+    ap.add_argument("--deadline-s", type=float, default=float(os.environ.get("FLEARN_BENCH_DEADLINE_S", 480)),
+                    help="N>1: an optional phase (push, weak job, loopback) starts only if it can end within "
+                         "this many seconds of the start, budget included (the driver's limit is ~600 s)")
     ap.add_argument("--no-loopback", action="store_true",
                     help="N>1: skip the single-process AVG(devices=[...]) loopback measurement")
     args = ap.parse_args()
+    t_start = time.monotonic()
+
+    def time_for(budget: float) -> bool:  # may an optional phase of this budget still start?
+        return time.monotonic() - t_start + budget <= args.deadline_s
 
     # one process per GPU: with no launcher env, --gpus N > 1 starts the N ranks here, BEFORE any
     # HIP call in this process (na.lib(), torch.cuda.set_device, ...), and exits with their status
@@ -1030,7 +1037,18 @@ def main():
     rccl_failed = check is not None and not check["verified"]
     if rccl_failed and g_eff > 1:
         line["multi_gpu"]["phases"]["push"] = {"status": "skipped: the RCCL job failed its self-check"}
-    if world > 1 and args.gather != "rccl" and not rccl_failed:
+    # every rank decides alike: rank 0's clock, broadcast
+    def agreed(flag: bool) -> bool:
+        if world == 1:
+            return flag
+        box = [flag]
+        dist.broadcast_object_list(box, src=0)
+        return bool(box[0])
+
+    push_time = agreed(time_for(args.push_budget_s)) if world > 1 and args.gather != "rccl" and not rccl_failed else True
+    if not push_time:
+        line["multi_gpu"]["phases"]["push"] = {"status": "skipped: out of time", "deadline_s": args.deadline_s}
+    if world > 1 and args.gather != "rccl" and not rccl_failed and push_time:
         t_phase = time.perf_counter()
         ph = {"status": "started", "budget_s": args.push_budget_s}
         line["multi_gpu"]["phases"]["push"] = ph
@@ -1102,7 +1120,10 @@ def main():
         dog.disarm()
 
     # ---- phase 3: the weak job beside it, the loopback drop-in — each bounded -------------------
-    if g_eff > 1 and not args.no_weak and emu is None and not rccl_failed:
+    weak_time = agreed(time_for(args.phase_budget_s)) if g_eff > 1 and emu is None else True
+    if g_eff > 1 and not args.no_weak and emu is None and not rccl_failed and not weak_time:
+        line["weak"] = {"status": "skipped: out of time", "deadline_s": args.deadline_s}
+    if g_eff > 1 and not args.no_weak and emu is None and not rccl_failed and weak_time:
         def weak_overran(ln):
             ln["weak"] = {"status": "timed_out", "budget_s": args.phase_budget_s}
 
@@ -1129,7 +1150,9 @@ def main():
         dist.barrier()
         dist.destroy_process_group()
     loop = None
-    if world > 1 and rank == 0 and not args.no_loopback and not rccl_failed:
+    if world > 1 and rank == 0 and not args.no_loopback and not rccl_failed and not time_for(args.phase_budget_s):
+        line["loopback_multi_gpu"] = {"status": "skipped: out of time", "deadline_s": args.deadline_s}
+    elif world > 1 and rank == 0 and not args.no_loopback and not rccl_failed:
         # the single-process multi-GPU drop-in (flearn's Communicator collects every upload in one
         # process): rank 0 alone, after the process group is gone, drives every GPU of the node
         ndev = max(torch.cuda.device_count(), 1)
