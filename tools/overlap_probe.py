@@ -59,6 +59,8 @@ def main():
     L.probe_read.restype = ctypes.c_int
     L.probe_write.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_void_p]
     L.probe_write.restype = ctypes.c_int
+    L.probe_blit.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]
+    L.probe_blit.restype = ctypes.c_int
     na.lib()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
@@ -124,6 +126,19 @@ def main():
             def f():
                 assert Lf.fa_push(src.data_ptr(), nbytes, dsts, 1, pgrid, sb.cuda_stream) == 0
             return f
+        if kind.startswith("cphost") or kind == "blithost":  # a plain 16-B copy kernel (probe_copy16,
+            # cphost<B>: B blocks of 256) or the runtime's blit kernel (hipMemcpyDeviceToDevice) into
+            # pinned host memory: which store pattern lets a link-bound copy leave the reduce alone?
+            if host_dst is None:
+                host_dst = torch.empty(nbytes // 4, dtype=torch.float32, pin_memory=True)
+            blocks = int(kind[6:]) if kind.startswith("cphost") else 0
+
+            def f():
+                if blocks:
+                    assert L.probe_copy(host_dst.data_ptr(), src.data_ptr(), nbytes // 16, blocks, sb.cuda_stream) == 0
+                else:
+                    assert L.probe_blit(host_dst.data_ptr(), src.data_ptr(), nbytes, sb.cuda_stream) == 0
+            return f
         if kind == "dmahost":  # a copy engine moving device memory to pinned host memory over PCIe:
             # the sender's side of the copy-engine push (an SDMA leg over a link)
             if host_dst is None:
@@ -132,6 +147,11 @@ def main():
 
             def f():
                 assert Ld.fa_copy_dma(host_dst.data_ptr(), src.data_ptr(), nbytes, sb.cuda_stream) == 0
+            return f
+        if kind == "dmadev":  # a copy engine (fa_copy_dma, NoCU) between two device buffers: the
+            # sender's side of the copy-engine push with an HBM destination standing in for a peer's
+            def f():
+                assert na.lib().fa_copy_dma(dst.data_ptr(), src.data_ptr(), nbytes, sb.cuda_stream) == 0
             return f
         if kind == "dma":
             def f():

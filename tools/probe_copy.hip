@@ -79,3 +79,12 @@ extern "C" int probe_write(void* dst, int64_t n16, int32_t blocks, void* stream)
                      static_cast<uint4*>(dst), n16);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
+
+// the runtime's own copy of a device buffer to another address (hipMemcpyDeviceToDevice): for a
+// pinned-host destination ROCclr runs its blit kernel (__amd_rocclr_copyBuffer) on the stream's
+// queue; the fa_push contention probe compares it with fa_push into the same memory
+extern "C" int probe_blit(void* dst, const void* src, int64_t nbytes, void* stream) {
+  if (!dst || !src || nbytes <= 0) return -1;
+  return hipMemcpyAsync(dst, src, (size_t)nbytes, hipMemcpyDeviceToDevice, static_cast<hipStream_t>(stream)) ==
+                 hipSuccess ? 0 : -2;
+}

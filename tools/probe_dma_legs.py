@@ -10,6 +10,10 @@ answers is whether the copies' INTERVALS overlap — the engines run at once, sh
 follow each other — one engine / one queue at a time), and, second, to `legs` device buffers
 (same-device copies).  Timed with HIP events on the pusher's stream: one leg alone, then all
 legs through fa_push_dma + fa_stream_join.  Measurement infrastructure, not the product.
+
+Time it WITHOUT a profiler: under rocprofv3 the runtime routes these copies differently (kernel
+trace: copy kernels; memory-copy trace: ~60 GB/s per engine), so a traced run says which path
+ran, not how fast ("The copy paths, traced and untraced").
 """
 from __future__ import annotations
 

@@ -100,13 +100,14 @@ def push_contention(ingress_bs: float, path=PUSH_PROBE):
 
 
 def project(cfg: str, g: int, link_bs: float, launch_s=10e-6, collective_s=30e-6, tail=True, contended=False,
-            push=False, barrier_s=15e-6, dma=False, dma_egress_bs=None):
+            push=False, barrier_s=15e-6, dma=False, dma_egress_bs=None, push_probe=PUSH_PROBE):
     """push: the one-shot push gather (flearn_amd.dist.PushGather) — a launch per stripe instead
     of a collective, two barriers per step, and local HBM traffic of ingress * (1 + 1/(G-1))
     (received bytes written, the own slice read once) instead of a ring's ~2 x ingress.
     dma_egress_bs (with dma): what the copy engines that run at once move out of one GPU in all
-    (round 5, tools/probe_dma_legs.py: ~140 GB/s for 7 legs — 2.3 engines' worth at 60 GB/s
-    each); every leg then gets min(link, egress / (G-1))."""
+    (round 5, tools/probe_dma_legs.py untraced: ~955 GB/s for 7 device-to-device legs; the ~140
+    GB/s first read from a profiled run was the profiler's); every leg then gets
+    min(link, egress / (G-1))."""
     n, p = CONFIGS[cfg]
     if push and dma and dma_egress_bs and g > 1:
         link_bs = min(link_bs, dma_egress_bs / (g - 1))
@@ -119,8 +120,10 @@ def project(cfg: str, g: int, link_bs: float, launch_s=10e-6, collective_s=30e-6
     m = StripeModel(launch_s, b_r, a_g, b_g)
     stand_in = None
     if contended and g > 1:
-        c_r, c_g, stand_in = (push_dma_contention((g - 1) * link_bs) if push and dma else
-                              push_contention((g - 1) * link_bs) if push else contention((g - 1) * link_bs))
+        ingress = (g - 1) * link_bs
+        c_r, c_g, stand_in = (push_dma_contention(ingress, PUSH_DMA_PROBE if str(push_probe) == str(PUSH_PROBE)
+                                                  else push_probe, push_probe) if push and dma else
+                              push_contention(ingress, push_probe) if push else contention(ingress))
         m = m.with_contention(c_r, c_g)
     if g == 1:
         widths, rep = (local,), 0
@@ -145,13 +148,15 @@ def main():
     ap.add_argument("--push", action="store_true", help="the one-shot push gather instead of RCCL's all-gather")
     ap.add_argument("--dma", action="store_true", help="with --push: its copy-engine form (one leg per peer)")
     ap.add_argument("--dma-egress-gbs", type=float, default=None,
-                    help="with --push --dma: the copy engines' total egress per GPU (measured: ~140)")
+                    help="with --push --dma: the copy engines' total egress per GPU (measured untraced: ~955)")
+    ap.add_argument("--push-probe", default=str(PUSH_PROBE),
+                    help="the push contention probe (round 5's untraced rerun: profiles/r05/copy_paths/overlap_push_r05.json)")
     ap.add_argument("--contended", action="store_true",
                     help="reduce / gather slowed by the measured one-GPU contention (profiles/r04/overlap)")
     a = ap.parse_args()
     egress = a.dma_egress_gbs * 1e9 if a.dma_egress_gbs else None
     rows = [project(c, g, float(l) * 1e9, tail=not a.no_tail, contended=a.contended, push=a.push, dma=a.dma,
-                    dma_egress_bs=egress)
+                    dma_egress_bs=egress, push_probe=a.push_probe)
             for l in a.link_gbs.split(",") for c in CONFIGS for g in (2, 4, 8)]
     if a.json:
         print(json.dumps(rows, indent=1))
