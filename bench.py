@@ -729,19 +729,55 @@ def loopback_multi_gpu(devices, rounds: int = 5, config: str = "c2") -> dict:
     return out
 
 
+def _load_lastwords():
+    """tools/liblastwords.so (built by __graft_entry__.build()): the held line written to stdout if a
+    signal ends the process (a GPU fault's abort, torchrun's SIGTERM after another rank died)."""
+    import ctypes
+
+    path = Path(__file__).resolve().parent / "tools" / "liblastwords.so"
+    if not path.exists():
+        log(f"[rank 0] {path.name} not built: a crash in the later phases would lose the held line")
+        return None
+    lib = ctypes.CDLL(str(path))
+    lib.lw_set.argtypes = [ctypes.c_char_p, ctypes.c_int64]
+    lib.lw_set.restype = ctypes.c_int
+    lib.lw_clear.argtypes = []
+    lib.lw_clear.restype = ctypes.c_int
+    return lib
+
+
 class HeldLine:
     """Rank 0's JSON line, built as soon as the RCCL job is timed and verified and refined by
     the later phases; printed exactly once — at the end, or by the Watchdog when a later phase
-    overruns its budget."""
+    overruns its budget, or (tools/lastwords.c) by a signal handler if the process is killed or
+    aborts meanwhile: then the line carries `ended_by_signal.during` = the phase that was running."""
 
-    def __init__(self, rank: int):
+    def __init__(self, rank: int, lastwords=False):
         self.rank, self.line, self.exit_code = rank, None, 0
         self._lock = threading.Lock()
         self._printed = False
+        self._phase = "between phases"
+        self._lw = _load_lastwords() if lastwords and rank == 0 else None
 
     def set(self, line, exit_code: int):
         with self._lock:
             self.line, self.exit_code = line, exit_code
+        self.guard(self._phase)
+
+    def guard(self, phase: str):
+        """Hand the current line, marked with `phase`, to the signal handler."""
+        self._phase = phase
+        if self._lw is None or self.line is None:
+            return
+        with self._lock:
+            if self._printed:
+                return
+            data = json.dumps({**self.line, "ended_by_signal": {
+                "during": phase, "note": "the process was ended by a signal (GPU fault, abort, or torchrun's "
+                                         "SIGTERM after another rank died); this is the line held at that point"}})
+            rc = self._lw.lw_set(data.encode(), len(data.encode()))
+            if rc:
+                log(f"[rank 0] lastwords: lw_set returned {rc}")
 
     def emit(self) -> bool:
         with self._lock:
@@ -749,6 +785,8 @@ class HeldLine:
                 return False
             print(json.dumps(self.line), flush=True)
             self._printed = True
+            if self._lw is not None:
+                self._lw.lw_clear()
             return True
 
 
@@ -770,10 +808,12 @@ class Watchdog:
     def arm(self, seconds: float, what: str, annotate=None):
         with self._lock:
             self._deadline, self._what, self._annotate = time.monotonic() + seconds, what, annotate
+        self.held.guard(what)
 
     def disarm(self):
         with self._lock:
             self._deadline = self._what = self._annotate = None
+        self.held.guard("between phases")
 
     def _run(self):
         while True:
@@ -887,6 +927,18 @@ def build_line(args, cfg, world, g_eff, emu, main_n, job, step_s, wall, info, ch
     return line
 
 
+def _end_with_held_line(held, rank, e):
+    """A later phase raised (multi-GPU): print the held line, marked with the phase and the error,
+    and end this rank now — os._exit, since the process group's teardown may wait on dead peers."""
+    log(f"[rank {rank}] a later phase failed: {type(e).__name__}: {e}; ending with the held line")
+    if held.line is not None:
+        held.line["ended_by_error"] = {"during": held._phase, "error": f"{type(e).__name__}: {e}"[:400]}
+    held.emit()
+    sys.stdout.flush()
+    sys.stderr.flush()
+    os._exit(held.exit_code)
+
+
 def _exit_code(check) -> int:
     return verify.EXIT_MISMATCH if (check is not None and not check["verified"]) else 0
 
@@ -927,6 +979,16 @@ def _install_injections(rank):
 
         fa_dist.PushGather.__init__ = stalled_init
         del real_init
+    if inject == "push_crash" and rank == 1:
+        # rehearsal of a rank that dies in the push set-up (a GPU fault's abort, say): torchrun
+        # then ends the others with SIGTERM, or their next collective raises — rank 0 must still
+        # print the verified RCCL line (tools/lastwords.c, _end_with_held_line)
+        def crashing_init(self, *a, **k):
+            log("[rank 1] INJECTED: dying in the push set-up")
+            sys.stderr.flush()
+            os._exit(7)
+
+        fa_dist.PushGather.__init__ = crashing_init
     return inject
 
 
@@ -1001,7 +1063,7 @@ def main():
     g_eff = emu or world  # GPUs of the (possibly emulated) job
     strong_n, weak_n = cfg["clients"], cfg["clients"] * g_eff
     main_n = strong_n if args.scaling == "strong" else weak_n
-    held = HeldLine(rank)
+    held = HeldLine(rank, lastwords=world > 1)  # multi-GPU: a crash in a later phase still prints the line
     dog = Watchdog(held, rank) if world > 1 else None
 
     def self_check(job):
@@ -1032,144 +1094,152 @@ def main():
     if world > 1:
         dist.barrier()
 
-    # ---- phase 2: the one-shot push gathers, bounded; adopted only if faster AND verified ------
-    # (not when the RCCL job failed its self-check: that line stands, and the run exits non-zero)
-    rccl_failed = check is not None and not check["verified"]
-    if rccl_failed and g_eff > 1:
-        line["multi_gpu"]["phases"]["push"] = {"status": "skipped: the RCCL job failed its self-check"}
-    # every rank decides alike: rank 0's clock, broadcast
-    def agreed(flag: bool) -> bool:
-        if world == 1:
-            return flag
-        box = [flag]
-        dist.broadcast_object_list(box, src=0)
-        return bool(box[0])
+    # the phases after the secured line: an exception in any of them (a peer that died mid-collective
+    # raises on gloo) ends every rank with the held line, not a traceback without one
+    try:
+        # ---- phase 2: the one-shot push gathers, bounded; adopted only if faster AND verified ------
+        # (not when the RCCL job failed its self-check: that line stands, and the run exits non-zero)
+        rccl_failed = check is not None and not check["verified"]
+        if rccl_failed and g_eff > 1:
+            line["multi_gpu"]["phases"]["push"] = {"status": "skipped: the RCCL job failed its self-check"}
+        # every rank decides alike: rank 0's clock, broadcast
+        def agreed(flag: bool) -> bool:
+            if world == 1:
+                return flag
+            box = [flag]
+            dist.broadcast_object_list(box, src=0)
+            return bool(box[0])
 
-    push_time = agreed(time_for(args.push_budget_s)) if world > 1 and args.gather != "rccl" and not rccl_failed else True
-    if not push_time:
-        line["multi_gpu"]["phases"]["push"] = {"status": "skipped: out of time", "deadline_s": args.deadline_s}
-    if world > 1 and args.gather != "rccl" and not rccl_failed and push_time:
-        t_phase = time.perf_counter()
-        ph = {"status": "started", "budget_s": args.push_budget_s}
-        line["multi_gpu"]["phases"]["push"] = ph
+        push_time = agreed(time_for(args.push_budget_s)) if world > 1 and args.gather != "rccl" and not rccl_failed else True
+        if not push_time:
+            line["multi_gpu"]["phases"]["push"] = {"status": "skipped: out of time", "deadline_s": args.deadline_s}
+        if world > 1 and args.gather != "rccl" and not rccl_failed and push_time:
+            t_phase = time.perf_counter()
+            ph = {"status": "started", "budget_s": args.push_budget_s}
+            line["multi_gpu"]["phases"]["push"] = ph
 
-        def overran(ln, t_phase=t_phase):
-            p = ln["multi_gpu"]["phases"]["push"]
-            p.update(status="timed_out", elapsed_s=round(time.perf_counter() - t_phase, 1),
-                     note="a rank did not finish the push phase within its budget: the RCCL line stands")
+            def overran(ln, t_phase=t_phase):
+                p = ln["multi_gpu"]["phases"]["push"]
+                p.update(status="timed_out", elapsed_s=round(time.perf_counter() - t_phase, 1),
+                         note="a rank did not finish the push phase within its budget: the RCCL line stands")
 
-        dog.arm(args.push_budget_s, "push phase", overran)
-        status, pjob, pinfo = "error", None, {}
-        try:
-            r_big = (info.get("calibration") or {}).get("reduce_us", [0.0])[0] * 1e-6
-            pplan, pg_name, pinfo, pbest = plan_push(cfg, layout, main_n, args, world, rank, dev, g_eff, r_big)
-            best_rccl = min((t["measured_ms"] for t in info.get("plan_trials", []) if t["measured_ms"]), default=None)
-            if pplan is None:
-                status = "unavailable"
-            elif args.gather == "auto" and best_rccl is not None and pbest is not None and pbest * 1e3 >= best_rccl:
-                status = "slower_in_trials"
-            else:
-                pjob, pstep, pwall, ptinfo = timed_job(cfg, layout, main_n, pplan, pg_name, pinfo.get("push_grid"),
-                                                       args, world, dev, g_eff)
-                pinfo.update(ptinfo)
-                pcheck = self_check(pjob)
-                if pcheck is not None and not pcheck["verified"]:
-                    status = "failed_self_check"
-                    pinfo["push_failed_self_check"] = {"gather": pg_name, "mismatched_windows": pcheck["mismatched_windows"],
-                                                       "first_mismatches": pcheck.get("first_mismatches")}
-                    log(f"[rank {rank}] the {pg_name} gather failed the self-check: keeping the RCCL line")
-                elif args.gather == "auto" and pstep >= step_s:
-                    status = "slower"
+            dog.arm(args.push_budget_s, "push phase", overran)
+            status, pjob, pinfo = "error", None, {}
+            try:
+                r_big = (info.get("calibration") or {}).get("reduce_us", [0.0])[0] * 1e-6
+                pplan, pg_name, pinfo, pbest = plan_push(cfg, layout, main_n, args, world, rank, dev, g_eff, r_big)
+                best_rccl = min((t["measured_ms"] for t in info.get("plan_trials", []) if t["measured_ms"]), default=None)
+                if pplan is None:
+                    status = "unavailable"
+                elif args.gather == "auto" and best_rccl is not None and pbest is not None and pbest * 1e3 >= best_rccl:
+                    status = "slower_in_trials"
                 else:
-                    status = "adopted"
-                ph.update(ms_per_step=round(pstep * 1e3, 4), gather=pg_name,
-                          verified=None if pcheck is None else pcheck["verified"])
-        except Exception as e:  # noqa: BLE001 - any failure here leaves the RCCL line standing
-            log(f"[rank {rank}] push phase failed: {type(e).__name__}: {e}")
-            ph["error"] = f"{type(e).__name__}: {e}"
-        # every rank's outcome (a rank that raised may not have joined the others' collectives:
-        # if they hang, the watchdog ends the run with the held line)
-        outcomes = [None] * world
-        dist.all_gather_object(outcomes, status)
-        adopt = all(o == "adopted" for o in outcomes)
-        ph["status"] = "adopted" if adopt else next((o for o in outcomes if o != "adopted"), status)
-        ph["rank_outcomes"] = outcomes
-        for k in ("push_calibration", "push_dma_calibration"):
-            if k in pinfo:
-                line["multi_gpu"][k] = pinfo[k]
-        if "plan_trials" in pinfo:
-            line["multi_gpu"]["plan_trials"] = line["multi_gpu"].get("plan_trials", []) + pinfo["plan_trials"]
-        if "push_failed_self_check" in pinfo:
-            line["multi_gpu"]["push_failed_self_check"] = pinfo["push_failed_self_check"]
-        if adopt:
+                    pjob, pstep, pwall, ptinfo = timed_job(cfg, layout, main_n, pplan, pg_name, pinfo.get("push_grid"),
+                                                           args, world, dev, g_eff)
+                    pinfo.update(ptinfo)
+                    pcheck = self_check(pjob)
+                    if pcheck is not None and not pcheck["verified"]:
+                        status = "failed_self_check"
+                        pinfo["push_failed_self_check"] = {"gather": pg_name, "mismatched_windows": pcheck["mismatched_windows"],
+                                                           "first_mismatches": pcheck.get("first_mismatches")}
+                        log(f"[rank {rank}] the {pg_name} gather failed the self-check: keeping the RCCL line")
+                    elif args.gather == "auto" and pstep >= step_s:
+                        status = "slower"
+                    else:
+                        status = "adopted"
+                    ph.update(ms_per_step=round(pstep * 1e3, 4), gather=pg_name,
+                              verified=None if pcheck is None else pcheck["verified"])
+            except Exception as e:  # noqa: BLE001 - any failure here leaves the RCCL line standing
+                log(f"[rank {rank}] push phase failed: {type(e).__name__}: {e}")
+                ph["error"] = f"{type(e).__name__}: {e}"
+            # every rank's outcome (a rank that raised may not have joined the others' collectives:
+            # if they hang, the watchdog ends the run with the held line)
+            outcomes = [None] * world
+            dist.all_gather_object(outcomes, status)
+            adopt = all(o == "adopted" for o in outcomes)
+            ph["status"] = "adopted" if adopt else next((o for o in outcomes if o != "adopted"), status)
+            ph["rank_outcomes"] = outcomes
+            for k in ("push_calibration", "push_dma_calibration"):
+                if k in pinfo:
+                    line["multi_gpu"][k] = pinfo[k]
+            if "plan_trials" in pinfo:
+                line["multi_gpu"]["plan_trials"] = line["multi_gpu"].get("plan_trials", []) + pinfo["plan_trials"]
+            if "push_failed_self_check" in pinfo:
+                line["multi_gpu"]["push_failed_self_check"] = pinfo["push_failed_self_check"]
+            if adopt:
+                job.release()
+                job, step_s, wall, info, check = pjob, pstep, pwall, {**info, **pinfo}, pcheck
+                gather_main = pg_name
+                launch_s = job_extras(job, step_s, info, args, cfg, world, dev, g_eff, main_n, backend)
+                phases = line["multi_gpu"]["phases"]
+                trials = line["multi_gpu"].get("plan_trials")
+                line = build_line(args, cfg, world, g_eff, emu, main_n, job, step_s, wall, info, check, launch_s, cpu, backend)
+                line["multi_gpu"]["phases"] = phases
+                if trials is not None:
+                    line["multi_gpu"]["plan_trials"] = trials
+                held.set(line, _exit_code(check))
+            elif pjob is not None:
+                pjob.release()
+            ph["elapsed_s"] = round(time.perf_counter() - t_phase, 1)
+            dist.barrier()
+            dog.disarm()
+
+        # ---- phase 3: the weak job beside it, the loopback drop-in — each bounded -------------------
+        weak_time = agreed(time_for(args.phase_budget_s)) if g_eff > 1 and emu is None else True
+        if g_eff > 1 and not args.no_weak and emu is None and not rccl_failed and not weak_time:
+            line["weak"] = {"status": "skipped: out of time", "deadline_s": args.deadline_s}
+        if g_eff > 1 and not args.no_weak and emu is None and not rccl_failed and weak_time:
+            def weak_overran(ln):
+                ln["weak"] = {"status": "timed_out", "budget_s": args.phase_budget_s}
+
+            dog.arm(args.phase_budget_s, "weak job", weak_overran)
             job.release()
-            job, step_s, wall, info, check = pjob, pstep, pwall, {**info, **pinfo}, pcheck
-            gather_main = pg_name
-            launch_s = job_extras(job, step_s, info, args, cfg, world, dev, g_eff, main_n, backend)
-            phases = line["multi_gpu"]["phases"]
-            trials = line["multi_gpu"].get("plan_trials")
-            line = build_line(args, cfg, world, g_eff, emu, main_n, job, step_s, wall, info, check, launch_s, cpu, backend)
-            line["multi_gpu"]["phases"] = phases
-            if trials is not None:
-                line["multi_gpu"]["plan_trials"] = trials
-            held.set(line, _exit_code(check))
-        elif pjob is not None:
-            pjob.release()
-        ph["elapsed_s"] = round(time.perf_counter() - t_phase, 1)
-        dist.barrier()
-        dog.disarm()
+            other_n = weak_n if args.scaling == "strong" else strong_n
+            ojob, ostep, _, oinfo = run_job(cfg, layout, other_n, args, world, rank, dev, g_eff, gather=gather_main)
+            line[("weak" if args.scaling == "strong" else "strong")] = {
+                "scaling": "weak" if args.scaling == "strong" else "strong",
+                "clients": other_n,
+                "value": round(algorithmic_bytes(other_n, layouts.fp32_elems(layout), cfg["op"]) / GIB / ostep, 2),
+                "unit": "GiB/s",
+                "ms_per_step": round(ostep * 1e3, 4),
+                **oinfo,
+            }
+            ojob.release()
+            dist.barrier()
+            dog.disarm()
 
-    # ---- phase 3: the weak job beside it, the loopback drop-in — each bounded -------------------
-    weak_time = agreed(time_for(args.phase_budget_s)) if g_eff > 1 and emu is None else True
-    if g_eff > 1 and not args.no_weak and emu is None and not rccl_failed and not weak_time:
-        line["weak"] = {"status": "skipped: out of time", "deadline_s": args.deadline_s}
-    if g_eff > 1 and not args.no_weak and emu is None and not rccl_failed and weak_time:
-        def weak_overran(ln):
-            ln["weak"] = {"status": "timed_out", "budget_s": args.phase_budget_s}
+        if world > 1:
+            if job is not None and job.red is not None:
+                job.red.release()  # collective: the bucket back to the pool while the group exists
+            fa_dist.shutdown_push()  # every peer unmaps, then the receive buckets are parked
+            dist.barrier()
+            dist.destroy_process_group()
+        loop = None
+        if world > 1 and rank == 0 and not args.no_loopback and not rccl_failed and not time_for(args.phase_budget_s):
+            line["loopback_multi_gpu"] = {"status": "skipped: out of time", "deadline_s": args.deadline_s}
+        elif world > 1 and rank == 0 and not args.no_loopback and not rccl_failed:
+            # the single-process multi-GPU drop-in (flearn's Communicator collects every upload in one
+            # process): rank 0 alone, after the process group is gone, drives every GPU of the node
+            ndev = max(torch.cuda.device_count(), 1)
+            devices = [torch.device("cuda", i % ndev) for i in range(world)]
+            job.release()
+            job = None
 
-        dog.arm(args.phase_budget_s, "weak job", weak_overran)
-        job.release()
-        other_n = weak_n if args.scaling == "strong" else strong_n
-        ojob, ostep, _, oinfo = run_job(cfg, layout, other_n, args, world, rank, dev, g_eff, gather=gather_main)
-        line[("weak" if args.scaling == "strong" else "strong")] = {
-            "scaling": "weak" if args.scaling == "strong" else "strong",
-            "clients": other_n,
-            "value": round(algorithmic_bytes(other_n, layouts.fp32_elems(layout), cfg["op"]) / GIB / ostep, 2),
-            "unit": "GiB/s",
-            "ms_per_step": round(ostep * 1e3, 4),
-            **oinfo,
-        }
-        ojob.release()
-        dist.barrier()
-        dog.disarm()
+            def loop_overran(ln):
+                ln["loopback_multi_gpu"] = {"status": "timed_out", "budget_s": args.phase_budget_s}
 
-    if world > 1:
-        if job is not None and job.red is not None:
-            job.red.release()  # collective: the bucket back to the pool while the group exists
-        fa_dist.shutdown_push()  # every peer unmaps, then the receive buckets are parked
-        dist.barrier()
-        dist.destroy_process_group()
-    loop = None
-    if world > 1 and rank == 0 and not args.no_loopback and not rccl_failed and not time_for(args.phase_budget_s):
-        line["loopback_multi_gpu"] = {"status": "skipped: out of time", "deadline_s": args.deadline_s}
-    elif world > 1 and rank == 0 and not args.no_loopback and not rccl_failed:
-        # the single-process multi-GPU drop-in (flearn's Communicator collects every upload in one
-        # process): rank 0 alone, after the process group is gone, drives every GPU of the node
-        ndev = max(torch.cuda.device_count(), 1)
-        devices = [torch.device("cuda", i % ndev) for i in range(world)]
-        job.release()
-        job = None
+            dog.arm(args.phase_budget_s, "loopback", loop_overran)
+            log(f"[rank 0] loopback AVG(devices={[str(d) for d in devices]}) ...")
+            loop = loopback_multi_gpu(devices)
+            dog.disarm()
+            line["loopback_multi_gpu"] = loop
+            if not loop["verified"]:
+                held.set(line, verify.EXIT_MISMATCH)
 
-        def loop_overran(ln):
-            ln["loopback_multi_gpu"] = {"status": "timed_out", "budget_s": args.phase_budget_s}
-
-        dog.arm(args.phase_budget_s, "loopback", loop_overran)
-        log(f"[rank 0] loopback AVG(devices={[str(d) for d in devices]}) ...")
-        loop = loopback_multi_gpu(devices)
-        dog.disarm()
-        line["loopback_multi_gpu"] = loop
-        if not loop["verified"]:
-            held.set(line, verify.EXIT_MISMATCH)
+    except Exception as e:  # noqa: BLE001
+        if world == 1:
+            raise
+        _end_with_held_line(held, rank, e)
 
     held.emit()
     if held.exit_code:

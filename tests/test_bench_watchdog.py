@@ -1,8 +1,10 @@
 """bench.py's held line and watchdog on CPU (no GPU needed): a phase that hangs after the line was
 secured still ends the process at its budget with exactly one JSON line, annotated with what
 overran, and the held exit code (tests/test_gpu_bench.py rehearses the same with a stalled push
-set-up on the GPU box)."""
+set-up on the GPU box); a process ended by a signal meanwhile (a GPU fault's abort, torchrun's
+SIGTERM after another rank died) still prints the line, marked with the phase (tools/lastwords.c)."""
 import json
+import signal
 import subprocess
 import sys
 import time
@@ -58,3 +60,53 @@ def test_held_line_prints_once():
     assert h.emit() is False
     h0 = bench.HeldLine(0)
     assert h0.emit() is False  # nothing held yet
+
+
+LW_PROG = r"""
+import os, signal, sys, time
+sys.path.insert(0, {repo!r})
+import bench
+held = bench.HeldLine(0, lastwords=True)
+assert held._lw is not None
+held.set({{"metric": "m", "value": 2.5, "multi_gpu": {{}}}}, 0)
+dog = bench.Watchdog(held, 0)
+dog.arm(60.0, "push phase")
+held.line["multi_gpu"]["phases"] = {{"push": {{"status": "started"}}}}
+held.guard("push phase")
+if {emit}:
+    held.emit()
+sys.stdout.flush()
+{end}
+time.sleep(30)
+print("not reached", flush=True)
+"""
+
+
+def _lastwords_lib():
+    lib = REPO / "tools" / "liblastwords.so"
+    if not lib.exists():
+        subprocess.run(["gcc", "-O2", "-fPIC", "-shared", str(REPO / "tools" / "lastwords.c"), "-o", str(lib)], check=True)
+
+
+def _lw_run(end, emit=False):
+    _lastwords_lib()
+    return subprocess.run([sys.executable, "-c", LW_PROG.format(repo=str(REPO), end=end, emit=emit)],
+                          capture_output=True, text=True, timeout=120)
+
+
+def test_signal_prints_the_held_line_marked_with_its_phase():
+    for end, sig in (("os.kill(os.getpid(), signal.SIGTERM)", signal.SIGTERM), ("os.abort()", signal.SIGABRT)):
+        p = _lw_run(end)
+        assert p.returncode == -sig, (p.returncode, p.stderr[-2000:])  # the process still ends by the signal
+        lines = [ln for ln in p.stdout.splitlines() if ln.strip()]
+        assert len(lines) == 1 and "not reached" not in p.stdout, p.stdout
+        d = json.loads(lines[0])
+        assert d["value"] == 2.5 and d["multi_gpu"]["phases"]["push"]["status"] == "started"
+        assert d["ended_by_signal"]["during"] == "push phase"
+
+
+def test_signal_after_the_line_was_printed_adds_nothing():
+    p = _lw_run("os.kill(os.getpid(), signal.SIGTERM)", emit=True)
+    assert p.returncode == -signal.SIGTERM
+    lines = [ln for ln in p.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1 and "ended_by_signal" not in lines[0]

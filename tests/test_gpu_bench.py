@@ -144,6 +144,24 @@ def test_bench_line_survives_a_stalled_push_setup(cuda):
 
 
 @pytest.mark.timeout(300)
+def test_bench_line_survives_a_rank_dying_in_the_push_phase(cuda):
+    """FLEARN_BENCH_INJECT=push_crash: rank 1 dies in the push gather's set-up (os._exit, standing
+    in for a GPU fault's abort).  Rank 0 is then either ended by torchrun's SIGTERM (tools/lastwords.c
+    writes the held line from the signal handler) or sees its next collective raise (bench's
+    _end_with_held_line): either way exactly one line, the verified RCCL job, marked with the phase."""
+    p = _rehearse("c2", ("--no-weak", "--no-loopback"), inject="push_crash")
+    assert p.returncode != 0  # torchrun reports the dead rank
+    assert "INJECTED: dying in the push set-up" in p.stderr
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, (p.stdout, p.stderr[-3000:])
+    d = json.loads(lines[0])
+    mg = d["multi_gpu"]
+    assert mg["gather"] == "rccl" and mg["phases"]["rccl"]["verified"] is True and d["verify"]["verified"] is True
+    ended = d.get("ended_by_signal") or d.get("ended_by_error")
+    assert ended is not None and ended["during"] == "push phase", d
+
+
+@pytest.mark.timeout(300)
 def test_bench_fails_on_a_misplaced_gather(cuda):
     """FLEARN_BENCH_INJECT=gather_offset: every gathered slice lands ALIGN columns late; the
     self-check must flag it in the line and the run must exit non-zero (EXIT_MISMATCH)."""

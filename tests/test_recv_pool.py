@@ -86,9 +86,11 @@ def _worker(rank, world, init):
     ev = []
     L, FB = _install_stubs(fd, ev)
     try:
+        # the pool's device is named cuda:0 (a CPU device is refused collectively, as the GPU-only
+        # IPC path requires); every GPU call is stubbed, so no GPU is touched
         pg = types.SimpleNamespace(world=world, rank=rank, group=None, nccl=False, device=torch.device("cpu"), L=L)
-        pool = fd._RecvPool.get("cpu", None)
-        assert fd._RecvPool.get(torch.device("cpu"), None) is pool
+        pool = fd._RecvPool.get("cuda:0", None)
+        assert fd._RecvPool.get(torch.device("cuda:0"), None) is pool
         i, buf, dsts = pool.take(pg, 1000)
         assert i == 0 and buf.numel() == _cols(1000) and len(dsts) == world
         j, buf2, _ = pool.take(pg, 500)  # slot 0 is busy: a second bucket
@@ -126,7 +128,7 @@ def _worker(rank, world, init):
         assert fd._RecvPool.bytes_held() == 0 and not fd._RecvPool._pools
         assert FB.parked_bytes() == 4 * (_cols(1000) + _cols(500) + _cols(2000))
         # the next pool re-exports the smallest parked bucket that fits (no new allocation)
-        p2 = fd._RecvPool.get("cpu", None)
+        p2 = fd._RecvPool.get("cuda:0", None)
         ev.clear()
         p2.take(pg, 64)
         assert ev == [("reuse", 2), ("map", _cols(500))], ev
@@ -136,7 +138,7 @@ def _worker(rank, world, init):
         dist.destroy_process_group()
         dist.init_process_group("gloo", init_method=init + "_2", rank=rank, world_size=world)
         ev.clear()
-        p3 = fd._RecvPool.get("cpu", None)
+        p3 = fd._RecvPool.get("cuda:0", None)
         assert id(p3) != old and not p3.slots
         assert ev == [("close", 1000 + _cols(500)), ("park", 2)], ev
         i, _b, _ = p3.take(pg, 64)
