@@ -46,6 +46,12 @@ def main():
     ap.add_argument("--copy", default="16,32,64,dma")
     ap.add_argument("--copy-mb", type=int, default=256, help="bytes of one copy launch")
     ap.add_argument("--reps", type=int, default=7)
+    ap.add_argument("--push-cus", type=int, default=0,
+                    help="run the copy stream on this many CUs only (a CU-masked stream), spread evenly")
+    ap.add_argument("--mask-reduce", action="store_true",
+                    help="with --push-cus: the reduce's stream gets the other CUs (disjoint masks)")
+    ap.add_argument("--push-cu-layout", default="spread", choices=["spread", "low"],
+                    help="which CUs the copy stream gets: every (CUs/K)-th, or the lowest K")
     a = ap.parse_args()
     L = ctypes.CDLL(str(REPO / "tools" / "libprobe_copy.so"))
     L.probe_copy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_void_p]
@@ -74,6 +80,30 @@ def main():
     src = torch.empty(nbytes // 4, dtype=torch.float32, device=dev).fill_(1.0)
     dst = torch.empty_like(src)
     sa, sb = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    masks = None
+    if a.push_cus:
+        ncu = torch.cuda.get_device_properties(0).multi_processor_count
+        words = (ncu + 31) // 32
+        step = ncu // a.push_cus
+        cus = ([i * step for i in range(a.push_cus)] if a.push_cu_layout == "spread" else list(range(a.push_cus)))
+        mb, ma = [0] * words, [0] * words
+        for c in range(ncu):
+            (mb if c in cus else ma)[c // 32] |= 1 << (c % 32)
+        L.probe_stream_cumask.argtypes = [ctypes.POINTER(ctypes.c_uint32), ctypes.c_int32, ctypes.POINTER(ctypes.c_void_p)]
+        L.probe_stream_cumask_get.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.POINTER(ctypes.c_uint32)]
+
+        def masked(m):
+            h = ctypes.c_void_p()
+            assert L.probe_stream_cumask((ctypes.c_uint32 * words)(*m), words, ctypes.byref(h)) == 0
+            got = (ctypes.c_uint32 * words)()
+            assert L.probe_stream_cumask_get(h, words, got) == 0
+            return torch.cuda.ExternalStream(h.value, device=dev), [int(x) for x in got]
+
+        sb, got_b = masked(mb)
+        masks = {"copy_cus": cus, "copy_mask_read_back": [hex(x) for x in got_b]}
+        if a.mask_reduce:
+            sa, got_a = masked(ma)
+            masks["reduce_mask_read_back"] = [hex(x) for x in got_a]
     alg_bytes = n * p * 4 + p * 4
 
     def reduce():
@@ -193,6 +223,7 @@ def main():
         return ea0.elapsed_time(ea1) * 1e3, eb0.elapsed_time(eb1) * 1e3
 
     res = {"config": a.config, "clients": n, "cols": p, "copy_bytes": nbytes, "device": torch.cuda.get_device_name(0),
+           "cu_masks": masks,
            "cus": torch.cuda.get_device_properties(0).multi_processor_count, "rows": []}
     kinds = [k.strip() for k in a.copy.split(",") if k.strip()]
     for g in [int(x) for x in a.grids.split(",")]:

@@ -88,3 +88,22 @@ extern "C" int probe_blit(void* dst, const void* src, int64_t nbytes, void* stre
   return hipMemcpyAsync(dst, src, (size_t)nbytes, hipMemcpyDeviceToDevice, static_cast<hipStream_t>(stream)) ==
                  hipSuccess ? 0 : -2;
 }
+
+// a stream whose kernels may run only on the CUs set in `mask` (words x 32 bits, CU i = bit i):
+// does fencing a link-bound push onto a few CUs, and the reduce onto the others, remove the
+// push's cost to the reduce?  (tools/overlap_probe.py --push-cus)
+extern "C" int probe_stream_cumask(const uint32_t* mask, int32_t words, void** out) {
+  if (!mask || words <= 0 || !out) return -1;
+  hipStream_t s = nullptr;
+  if (hipExtStreamCreateWithCUMask(&s, (uint32_t)words, mask) != hipSuccess) return -2;
+  *out = s;
+  return 0;
+}
+
+extern "C" int probe_stream_cumask_get(void* stream, int32_t words, uint32_t* mask) {
+  return hipExtStreamGetCUMask(static_cast<hipStream_t>(stream), (uint32_t)words, mask) == hipSuccess ? 0 : -2;
+}
+
+extern "C" int probe_stream_destroy(void* stream) {
+  return hipStreamDestroy(static_cast<hipStream_t>(stream)) == hipSuccess ? 0 : -2;
+}
