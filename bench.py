@@ -290,18 +290,22 @@ def calibrate_push(job: Job, world: int, dev, r_big: float, reps: int = 5, mode:
             pg.gather(out[:small], p.rank * small)
         torch.cuda.synchronize(dev)
         dist.barrier()
-        # the push kernel's grid: the smallest within 3% of the fastest whole-width gather (more
-        # blocks keep more stores in flight for the links but take the memory pipeline from the
-        # reduce beside it: DESIGN.md section 6)
-        by_grid = {}
+        # the push kernel's grid: the smallest whose push BESIDE a reduce of the same width ends
+        # both within 3% of the best such pair.  More blocks keep more stores in flight for the
+        # links, but stores backed up behind a link slow the reduce through the data fabric — on
+        # one GPU's PCIe stand-in 3x at the grid that fills the link — so
+        # the gather alone picks the wrong grid.
+        by_grid, pair_by_grid = {}, {}
         for g in (PUSH_GRIDS if mode == "kernel" else ()):
             pg.grid = g
             by_grid[g] = _event_time(lambda: pg.gather(out[:big], p.rank * big), 3)
+            pair_by_grid[g] = _pair_time(job, pg, out, big, dev, 3)
         if by_grid:
-            times = _max_over_ranks(list(by_grid.values()), world, dev)
-            by_grid = dict(zip(PUSH_GRIDS, times))
-            best = min(times)
-            pg.grid = min(g for g, t in by_grid.items() if t <= 1.03 * best)
+            times = _max_over_ranks(list(by_grid.values()) + list(pair_by_grid.values()), world, dev)
+            by_grid = dict(zip(PUSH_GRIDS, times[:len(PUSH_GRIDS)]))
+            pair_by_grid = dict(zip(PUSH_GRIDS, times[len(PUSH_GRIDS):]))
+            best = min(pair_by_grid.values())
+            pg.grid = min(g for g, t in pair_by_grid.items() if t <= 1.03 * best)
         g_big = _event_time(lambda: pg.gather(out[:big], p.rank * big), reps)
         g_small = _event_time(lambda: pg.gather(out[:small], p.rank * small), reps)
         r_conc, g_conc, g_alone = _contention_push(job, pg, out, big, dev, reps)
@@ -314,11 +318,34 @@ def calibrate_push(job: Job, world: int, dev, r_big: float, reps: int = 5, mode:
     c_r, c_g = max(r_conc / r_big - 1.0, 0.0), max(g_conc / max(g_alone, 1e-9) - 1.0, 0.0)
     cal = dict(available=True, mode=mode, checked_against_rccl=True, width_cols=[big, small], grid=grid,
                gather_us_by_grid={str(g): round(t * 1e6, 2) for g, t in by_grid.items()},
+               pair_us_by_grid={str(g): round(t * 1e6, 2) for g, t in pair_by_grid.items()},
                gather_us=[round(g_big * 1e6, 2), round(g_small * 1e6, 2)],
                push_kernel_us=round(g_alone * 1e6, 2), concurrent_reduce_us=round(r_conc * 1e6, 2),
                concurrent_push_us=round(g_conc * 1e6, 2), c_r=round(c_r, 4), c_g=round(c_g, 4),
                per_link_gbs=round(big * 4 / max(g_alone, 1e-9) / 1e9, 2))
     return StripeModel.fit(big, small, r_big, r_small, g_big, g_small, c_r=c_r, c_g=c_g), cal
+
+
+def _pair_time(job, pg, out, cols, dev, reps: int) -> float:
+    """A push of `cols` columns and a reduce of as many, started together: the time until both
+    are done (median of reps) — what a stripe's push beside the next stripe's reduce costs."""
+    out2 = torch.empty_like(out)
+    cur = torch.cuda.current_stream(dev)
+    src, off = out[:cols], job.plan.rank * cols
+    ts = []
+    for _ in range(reps):
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(cur)
+        pg.begin()
+        pg.push(src, off)
+        job.fn(0, cols, out2[:cols])
+        pg.end()
+        e1.record(cur)
+        torch.cuda.synchronize(dev)
+        ts.append(e0.elapsed_time(e1) / 1e3)
+    return float(np.median(ts))
 
 
 def _contention_push(job, pg, out, cols, dev, reps: int):

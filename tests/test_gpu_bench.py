@@ -54,6 +54,9 @@ def test_bench_two_ranks_rehearsal(config, cuda):
     for c in (pc, pd):
         assert c["available"] is True and c["checked_against_rccl"] is True and c["push_kernel_us"] > 0
     assert pc["grid"] in (16, 32, 64, 128, 256) and set(pc["gather_us_by_grid"]) == {"16", "32", "64", "128", "256"}
+    # the grid is chosen by the push-beside-reduce pair, not by the push alone
+    pair = pc["pair_us_by_grid"]
+    assert set(pair) == set(pc["gather_us_by_grid"]) and pair[str(pc["grid"])] <= 1.03 * min(pair.values()) + 1e-6
     assert {t["gather"] for t in mg["plan_trials"]} == {"rccl", "push", "push_dma"}
     used = {"rccl": cal, "push": pc, "push_dma": pd}[mg["gather"]]
     assert mg["model"]["c_r"] == used["c_r"] and mg["model"]["c_g"] == used["c_g"]
