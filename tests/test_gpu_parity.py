@@ -595,6 +595,43 @@ def test_sharded_reducer_rccl_one_rank(op, stripes, weights, cuda, tmp_path):
             dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("push", [True, "dma"])
+def test_sharded_reducer_push_rccl_one_rank(push, cuda, tmp_path):
+    """The push gather's RCCL-specific code on a 1-rank RCCL group: its barriers are 1-element
+    all_reduces ordered on the pusher's stream (gloo, used by every multi-rank test on this box,
+    takes the host-barrier branch instead), the bucket comes from the receive pool (exported,
+    token-checked), three steps, then shutdown_push while the group exists — bit-exact."""
+    import torch.distributed as dist
+
+    from flearn_amd import dist as fd
+    from flearn_amd.dist import ShardedReducer, ShardPlan, hip_reduce_fn
+
+    created = False
+    if not dist.is_initialized():
+        dist.init_process_group("nccl", init_method=f"file://{tmp_path}/pg", rank=0, world_size=1, device_id=cuda)
+        created = True
+    try:
+        n, p = 7, 600_001
+        plan = ShardPlan.make(p, 1, 0, stripes=3)
+        stack = torch.empty((n, plan.local_cols), dtype=torch.float32, device=cuda)
+        for c in range(plan.stripes):
+            agg.fill_uniform(stack[:, plan.local_begin(c):], seed=5, col_begin=plan.global_begin(c),
+                             n_cols=plan.shard_of(c))
+        w = torch.ones(n, dtype=torch.float32, device=cuda)
+        red = ShardedReducer(plan, hip_reduce_fn(stack, w, na.MODE_W32_DIV64, float(n)), cuda, gather=True, push=push)
+        assert red.pusher is not None and red.pusher.nccl
+        want = oracle.c_reduce(oracle.MODE_W32_DIV64, oracle.fill_uniform(n, p, 5), np.ones(n, np.float32), float(n))
+        for _ in range(3):
+            full = red.step()
+            assert bitwise_equal(full[:p].cpu().numpy(), want.astype(np.float32))
+        red.release()
+        fd.shutdown_push()
+        assert fd._RecvPool.bytes_held() == 0
+    finally:
+        if created:
+            dist.destroy_process_group()
+
+
 @pytest.mark.parametrize("op", ["avgm", "adagrad", "yogi", "adam"])
 def test_fused_v_out_equals_in_place(op, cuda):
     """ABI 6 v_out: the double-buffered form (out32 into a fresh buffer, v_t into v_out) gives the
