@@ -42,6 +42,8 @@ from dataclasses import dataclass
 import torch
 import torch.distributed as dist
 
+from .streams import side_stream
+
 ALIGN = 64
 MAX_PUSH_RANKS = 8  # fa_push's destination count: one MI355X node
 
@@ -398,7 +400,13 @@ class PushGather:
                 self.owner, full = full, full.tensor(torch.float32)
             self.full, self.device = full, full.device
             self.bases, self.dst, self.stale = _map_peers(self, full)
-        self.stream = torch.cuda.Stream(self.device)
+        # kernel push: a high-priority stream, whose hardware queue is apart from the compute
+        # stream's — on a shared queue the push kernels run in queue order with the next stripes'
+        # reduces instead of beside them (streams.py).  Copy-engine push: normal priority — its
+        # legs run on the copy engines whatever queue their stream has, and with high-priority
+        # streams the legs were seen to land after the barrier meant to follow them (32 of 576
+        # in-place Adagrad steps wrong at world 8, 0 at normal priority: streams.py)
+        self.stream = side_stream(self.device) if mode == "kernel" else torch.cuda.Stream(self.device)
         self.flag = torch.zeros(1, dtype=torch.float32, device=self.device)
         self.grid = 0  # fa_push blocks (0: the library's default)
         # mode "dma": one stream per peer, each leg a copy-engine copy (fa_copy_dma) — copies on

@@ -322,7 +322,7 @@ class _DeviceStage:
         self.cap = 0
         self.n = 0  # rows staged in the current round
         self.gen = 0
-        self.stream = torch.cuda.Stream(device)
+        self.stream = torch.cuda.Stream(device)  # copies (copy engines): normal priority, streams.py
         self.done = None  # event after the last staged copy
 
     def stage(self, row: torch.Tensor):
