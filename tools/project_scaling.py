@@ -100,7 +100,7 @@ def push_contention(ingress_bs: float, path=PUSH_PROBE):
 
 
 def project(cfg: str, g: int, link_bs: float, launch_s=10e-6, collective_s=30e-6, tail=True, contended=False,
-            push=False, barrier_s=15e-6, dma=False, dma_egress_bs=None, push_probe=PUSH_PROBE):
+            push=False, barrier_s=15e-6, dma=False, dma_egress_bs=None, push_probe=PUSH_PROBE, serial=False):
     """push: the one-shot push gather (flearn_amd.dist.PushGather) — a launch per stripe instead
     of a collective, two barriers per step, and local HBM traffic of ingress * (1 + 1/(G-1))
     (received bytes written, the own slice read once) instead of a ring's ~2 x ingress.
@@ -125,7 +125,7 @@ def project(cfg: str, g: int, link_bs: float, launch_s=10e-6, collective_s=30e-6
                                                   else push_probe, push_probe) if push and dma else
                               push_contention(ingress, push_probe) if push else contention(ingress))
         m = m.with_contention(c_r, c_g)
-    if g == 1:
+    if g == 1 or serial:
         widths, rep = (local,), 0
     elif tail:
         widths, rep = plan_shards(p, g, m)
@@ -151,12 +151,15 @@ def main():
                     help="with --push --dma: the copy engines' total egress per GPU (measured untraced: ~955)")
     ap.add_argument("--push-probe", default=str(PUSH_PROBE),
                     help="the push contention probe (round 5's untraced rerun: profiles/r05/copy_paths/overlap_push_r05.json)")
+    ap.add_argument("--serial", action="store_true",
+                    help="one stripe, no overlap: what a gather whose stream shares the compute stream's hardware "
+                         "queue gets (DESIGN.md section 6, the pipeline's streams)")
     ap.add_argument("--contended", action="store_true",
                     help="reduce / gather slowed by the measured one-GPU contention (profiles/r04/overlap)")
     a = ap.parse_args()
     egress = a.dma_egress_gbs * 1e9 if a.dma_egress_gbs else None
     rows = [project(c, g, float(l) * 1e9, tail=not a.no_tail, contended=a.contended, push=a.push, dma=a.dma,
-                    dma_egress_bs=egress, push_probe=a.push_probe)
+                    dma_egress_bs=egress, push_probe=a.push_probe, serial=a.serial)
             for l in a.link_gbs.split(",") for c in CONFIGS for g in (2, 4, 8)]
     if a.json:
         print(json.dumps(rows, indent=1))
