@@ -404,8 +404,8 @@ class PushGather:
         # stream's — on a shared queue the push kernels run in queue order with the next stripes'
         # reduces instead of beside them (streams.py).  Copy-engine push: normal priority — its
         # legs run on the copy engines whatever queue their stream has, and with high-priority
-        # streams the legs were seen to land after the barrier meant to follow them (32 of 576
-        # in-place Adagrad steps wrong at world 8, 0 at normal priority: streams.py)
+        # streams they gave wrong buckets (32 of 576 in-place Adagrad rank-steps at world 8, 0 at
+        # normal priority: streams.py)
         self.stream = side_stream(self.device) if mode == "kernel" else torch.cuda.Stream(self.device)
         self.flag = torch.zeros(1, dtype=torch.float32, device=self.device)
         self.grid = 0  # fa_push blocks (0: the library's default)

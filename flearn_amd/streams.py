@@ -16,9 +16,10 @@ NoCU) run on the copy engines whatever queue their stream has, and with high-pri
 rank's slice was wrong in the buckets after the step's closing barrier — half of the wrong values
 the previous step's, half the bucket's older contents: tests/push_order_probe.py, eight processes,
 the copy-engine push with in-place Adagrad, 32 of 576 rank-steps wrong with high-priority streams
-and 0 of 576 with normal ones (the kernel push: 0 of 576 either way; profiles/r05/pipeline_queues/).  RCCL's internal stream stays in torch's normal pool (the
-process group's default): a high-priority one would give the all-gather its own queue too, but
-the line bench.py must not lose runs on it, and one GPU cannot test RCCL between ranks.
+and 0 of 576 with normal ones (the kernel push: 0 of 576 either way;
+profiles/r05/pipeline_queues/).  RCCL's internal stream stays in torch's normal pool (the process
+group's default): a high-priority one would give the all-gather its own queue too, but the line
+bench.py must not lose runs on it, and one GPU cannot test RCCL between ranks.
 """
 from __future__ import annotations
 
@@ -28,5 +29,5 @@ HIGH = -1  # torch's high stream priority on ROCm (the only other level is 0)
 
 
 def side_stream(device) -> torch.cuda.Stream:
-    """A stream of its own hardware queue, apart from every normal-priority stream."""
+    """A high-priority stream: its hardware queue is never one a normal-priority stream uses."""
     return torch.cuda.Stream(device, priority=HIGH)
