@@ -258,7 +258,7 @@ def calibrate(job: Job, world: int, dev, reps: int = 5):
     return StripeModel.fit(big, small, r_big, r_small, g_big, g_small, c_r=c_r, c_g=c_g), cal
 
 
-PUSH_GRIDS = (16, 32, 64, 128, 256)
+PUSH_GRIDS = (4, 8, 16, 32, 64, 128, 256)  # the paced push kernel: few blocks can fill a link
 PUSH_MODE = {"push": "kernel", "push_dma": "dma"}  # --gather name -> PushGather mode
 
 

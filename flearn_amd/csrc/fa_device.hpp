@@ -1534,6 +1534,12 @@ __global__ __launch_bounds__(kThreads) void copy_kernel(uint8_t* __restrict__ ds
 // One-shot all-gather leg (fa_push): each lane loads 16 B of the local stripe once and stores it
 // into every destination (the peers' receive buffers over their xGMI links, and the local one);
 // the closing system-scope fence makes the peer stores visible once the kernel has completed.
+// Paced: every wave drains its stores (vmcnt(0): on gfx9 the counter covers stores) before its
+// next round's loads, so at most U x n_dsts KiB per wave is in flight and the grid sets the total.
+// Stores queued beyond a link's bandwidth-delay product back up into the data fabric the reduce
+// beside them streams through: on one GPU's PCIe stand-in, 8 blocks reach 52 GB/s either way and
+// slow the reduce 1.27-1.32x paced, 1.27-2.08x unpaced (2.08 in the same run as the paced 1.27;
+// tools/overlap_probe.py paced<U>x<B> / pushhost<B>).
 struct PushDsts {
   uint8_t* p[8];
 };
@@ -1560,6 +1566,7 @@ __global__ __launch_bounds__(kThreads) void push_kernel(const uint8_t* __restric
         if (q < quads) reinterpret_cast<u4*>(d.p[i])[q] = v[u];
       }
     }
+    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");  // pace: this round's stores done first
   }
   __threadfence_system();
 }

@@ -53,7 +53,8 @@ def test_bench_two_ranks_rehearsal(config, cuda):
     pc, pd = mg["push_calibration"], mg["push_dma_calibration"]
     for c in (pc, pd):
         assert c["available"] is True and c["checked_against_rccl"] is True and c["push_kernel_us"] > 0
-    assert pc["grid"] in (16, 32, 64, 128, 256) and set(pc["gather_us_by_grid"]) == {"16", "32", "64", "128", "256"}
+    assert pc["grid"] in (4, 8, 16, 32, 64, 128, 256)
+    assert set(pc["gather_us_by_grid"]) == {"4", "8", "16", "32", "64", "128", "256"}
     # the grid is chosen by the push-beside-reduce pair, not by the push alone
     pair = pc["pair_us_by_grid"]
     assert set(pair) == set(pc["gather_us_by_grid"]) and pair[str(pc["grid"])] <= 1.03 * min(pair.values()) + 1e-6

@@ -169,6 +169,17 @@ def main():
                 else:
                     assert L.probe_blit(host_dst.data_ptr(), src.data_ptr(), nbytes, sb.cuda_stream) == 0
             return f
+        if kind.startswith("paced"):  # paced<U>x<B>: the paced push stand-in into pinned host memory,
+            # U quads per lane per round, B blocks, each wave's stores drained before its next loads
+            if host_dst is None:
+                host_dst = torch.empty(nbytes // 4, dtype=torch.float32, pin_memory=True)
+            u, b = (int(x) for x in kind[5:].split("x"))
+            L.probe_push_paced.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32,
+                                           ctypes.c_int32, ctypes.c_void_p]
+
+            def f():
+                assert L.probe_push_paced(host_dst.data_ptr(), src.data_ptr(), nbytes // 16, b, u, sb.cuda_stream) == 0
+            return f
         if kind == "dmahost":  # a copy engine moving device memory to pinned host memory over PCIe:
             # the sender's side of the copy-engine push (an SDMA leg over a link)
             if host_dst is None:

@@ -107,3 +107,42 @@ extern "C" int probe_stream_cumask_get(void* stream, int32_t words, uint32_t* ma
 extern "C" int probe_stream_destroy(void* stream) {
   return hipStreamDestroy(static_cast<hipStream_t>(stream)) == hipSuccess ? 0 : -2;
 }
+
+// a paced push stand-in: like fa_push's kernel into ONE destination (U quads per lane per round),
+// but every wave waits for its stores before its next loads (s_waitcnt vmcnt(0): on gfx9 the
+// counter covers stores too), so at most U x 1 KiB per wave is in flight — about the link's
+// bandwidth-delay product on few blocks instead of queues of stores backed up behind it.
+typedef uint32_t pu4 __attribute__((ext_vector_type(4)));
+template <int U>
+__global__ __launch_bounds__(256) void probe_push_paced_k(const pu4* __restrict__ s, int64_t quads,
+                                                          pu4* __restrict__ d) {
+  const int64_t G = (int64_t)gridDim.x * 256;
+  for (int64_t q0 = (int64_t)blockIdx.x * 256 + threadIdx.x; q0 < quads; q0 += U * G) {
+    pu4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t q = q0 + u * G;
+      v[u] = q < quads ? __builtin_nontemporal_load(s + q) : pu4{0, 0, 0, 0};
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t q = q0 + u * G;
+      if (q < quads) d[q] = v[u];
+    }
+    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __threadfence_system();
+}
+
+extern "C" int probe_push_paced(void* dst, const void* src, int64_t n16, int32_t blocks, int32_t u, void* stream) {
+  if (!dst || !src || n16 <= 0 || blocks <= 0) return -1;
+  auto s = static_cast<hipStream_t>(stream);
+  const pu4* a = static_cast<const pu4*>(src);
+  pu4* b = static_cast<pu4*>(dst);
+  if (u == 1) hipLaunchKernelGGL(probe_push_paced_k<1>, dim3((unsigned)blocks), dim3(256), 0, s, a, n16, b);
+  else if (u == 2) hipLaunchKernelGGL(probe_push_paced_k<2>, dim3((unsigned)blocks), dim3(256), 0, s, a, n16, b);
+  else if (u == 4) hipLaunchKernelGGL(probe_push_paced_k<4>, dim3((unsigned)blocks), dim3(256), 0, s, a, n16, b);
+  else if (u == 8) hipLaunchKernelGGL(probe_push_paced_k<8>, dim3((unsigned)blocks), dim3(256), 0, s, a, n16, b);
+  else return -1;
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
