@@ -82,7 +82,7 @@ def push_dma_contention(ingress_bs: float, path=PUSH_DMA_PROBE, push_path=PUSH_P
     return c_r, max(v["copy_slowdown"] - 1.0, 0.0), f"copy engine + writes at {rate / 1e9:.0f} GB/s"
 
 
-def push_contention(ingress_bs: float, path=PUSH_PROBE):
+def push_contention(ingress_bs: float, path=PUSH_PROBE, blocks=None):
     """(c_r, c_g, stand-in) of the one-shot push from the one-GPU probe: the sender's push kernel
     (pushhost<B>: a link-bound fa_push into pinned memory over PCIe, at the smallest grid that
     reaches 95% of its best rate) slows the reduce and is slowed by it; the peers' stores landing
@@ -92,7 +92,8 @@ def push_contention(ingress_bs: float, path=PUSH_PROBE):
     w = next(r for r in d["rows"] if r["grid"] == "default")["with"]
     ph = sorted((int(k[8:]), v) for k, v in w.items() if k.startswith("pushhost") and k[8:])
     top = max(v["copy_alone_gbs"] for _, v in ph)
-    b, v = next((b, v) for b, v in ph if v["copy_alone_gbs"] >= 0.95 * top)
+    b, v = (next((b, v) for b, v in ph if b == blocks) if blocks else
+            next((b, v) for b, v in ph if v["copy_alone_gbs"] >= 0.95 * top))
     wr = sorted((v["copy_alone_gbs"] * 1e9, v) for k, v in w.items() if k.startswith("wr"))
     rate, wv = next(((r, v) for r, v in wr if r >= ingress_bs), wr[-1])
     c_r = (v["reduce_slowdown"] - 1.0) + (wv["reduce_slowdown"] - 1.0)
@@ -100,7 +101,8 @@ def push_contention(ingress_bs: float, path=PUSH_PROBE):
 
 
 def project(cfg: str, g: int, link_bs: float, launch_s=10e-6, collective_s=30e-6, tail=True, contended=False,
-            push=False, barrier_s=15e-6, dma=False, dma_egress_bs=None, push_probe=PUSH_PROBE, serial=False):
+            push=False, barrier_s=15e-6, dma=False, dma_egress_bs=None, push_probe=PUSH_PROBE, serial=False,
+            push_blocks=None):
     """push: the one-shot push gather (flearn_amd.dist.PushGather) — a launch per stripe instead
     of a collective, two barriers per step, and local HBM traffic of ingress * (1 + 1/(G-1))
     (received bytes written, the own slice read once) instead of a ring's ~2 x ingress.
@@ -123,7 +125,7 @@ def project(cfg: str, g: int, link_bs: float, launch_s=10e-6, collective_s=30e-6
         ingress = (g - 1) * link_bs
         c_r, c_g, stand_in = (push_dma_contention(ingress, PUSH_DMA_PROBE if str(push_probe) == str(PUSH_PROBE)
                                                   else push_probe, push_probe) if push and dma else
-                              push_contention(ingress, push_probe) if push else contention(ingress))
+                              push_contention(ingress, push_probe, push_blocks) if push else contention(ingress))
         m = m.with_contention(c_r, c_g)
     if g == 1 or serial:
         widths, rep = (local,), 0
@@ -151,6 +153,8 @@ def main():
                     help="with --push --dma: the copy engines' total egress per GPU (measured untraced: ~955)")
     ap.add_argument("--push-probe", default=str(PUSH_PROBE),
                     help="the push contention probe (round 5's untraced rerun: profiles/r05/copy_paths/overlap_push_r05.json)")
+    ap.add_argument("--push-blocks", type=int, default=None,
+                    help="with --push: the stand-in's block count (default: the fewest within 95%% of its best rate)")
     ap.add_argument("--serial", action="store_true",
                     help="one stripe, no overlap: what a gather whose stream shares the compute stream's hardware "
                          "queue gets (DESIGN.md section 6, the pipeline's streams)")
@@ -159,7 +163,7 @@ def main():
     a = ap.parse_args()
     egress = a.dma_egress_gbs * 1e9 if a.dma_egress_gbs else None
     rows = [project(c, g, float(l) * 1e9, tail=not a.no_tail, contended=a.contended, push=a.push, dma=a.dma,
-                    dma_egress_bs=egress, push_probe=a.push_probe, serial=a.serial)
+                    dma_egress_bs=egress, push_probe=a.push_probe, serial=a.serial, push_blocks=a.push_blocks)
             for l in a.link_gbs.split(",") for c in CONFIGS for g in (2, 4, 8)]
     if a.json:
         print(json.dumps(rows, indent=1))
