@@ -792,9 +792,11 @@ int fa_copy(void* dst, const void* src, int64_t nbytes, void* stream) {
   return launch_check();
 }
 
-// fa_push's default grid: enough 16-B stores in flight for the links (tools/overlap_probe.py
-// pushhost<B> on one GPU: see DESIGN.md section 6), few enough to leave the reduce its CUs
-constexpr int64_t kPushGrid = 64;
+// fa_push's default grid.  The kernel is paced (each wave drains its stores per round): a block
+// keeps 4 waves x 4 quads x 1 KiB = 16 KiB in flight per destination link, so 16 blocks keep
+// ~256 KiB per link — about an xGMI link's bandwidth-delay product (64-153 GB/s x 1-2 us), more
+// only queues in the fabric and slows a reduce beside the push
+constexpr int64_t kPushGrid = 16;
 
 int fa_ipc_handle(const void* ptr, void* handle, int64_t* offset) {
   if (!ptr || !handle || !offset) return fail(FA_ERR_ARG, "null ipc argument");

@@ -271,9 +271,11 @@ int fa_mem_range(const void* ptr, void** base, int64_t* size);
 /* Copy nbytes from src to each of dsts[0..n_dsts) (n_dsts <= 8; every pointer 16-byte aligned;
  * dsts: a HOST array of device pointers, local or peer-mapped) in one kernel of `grid` blocks
  * (0: the library's choice) on `stream`; every lane ends with a system-scope release so the
- * stores are visible to the peers once the kernel has completed.  A small grid suffices to fill
- * the links and leaves the CUs' memory pipelines to a reduce running beside it (a link-bound push
- * on 1024 blocks slowed the reduce 1.8x on one GPU).  ABI 10 adds `grid`. */
+ * stores are visible to the peers once the kernel has completed.  Paced: each wave drains its
+ * stores before its next loads, so a block keeps ~16 KiB in flight per destination and the grid
+ * sets the total; a small grid fills a link, and stores queued beyond a link's bandwidth-delay
+ * product slow a reduce running beside the push (the data fabric backs up: DESIGN.md section 6).
+ * Default (grid 0) 16 blocks; bench.py calibrates it on the node.  ABI 10 adds `grid`. */
 int fa_push(const void* src, int64_t nbytes, void* const* dsts, int32_t n_dsts, int32_t grid, void* stream);
 
 /* hipMemcpyAsync(dst, src, nbytes, hipMemcpyDeviceToDeviceNoCU) on `stream`: a copy-engine
