@@ -644,6 +644,65 @@ def verify_job(job, cfg, world, dev, emulated: bool = False) -> dict:
     return res
 
 
+#: tests/test_gpu_bench.py's fault injection into one audited step (set by _install_injections)
+_AUDIT_FAULT = None
+AUDIT_STEPS = 20
+
+
+def _checksums(t: torch.Tensor, idx: torch.Tensor) -> torch.Tensor:
+    """Two exact integer checksums of an fp32 range's bit patterns: their sum, and their sum
+    weighted by position (a range shifted or permuted changes the second)."""
+    b = t.view(torch.int32).to(torch.int64)
+    return torch.stack([b.sum(), (b * idx[: b.numel()]).sum()])
+
+
+def push_audit(job, world, dev, steps: int = AUDIT_STEPS) -> dict:
+    """After a push job's timed region: `steps` more steps, every one checked end to end.  Each
+    rank checksums its own slice of every stripe on the compute stream right after the stripe's
+    reduce (what it then pushes), and after the step every slice of the reassembled bucket; the
+    senders' checksums are all-gathered and every receiver compares them with what landed — so a
+    gather that corrupted one step in the middle, and not the last, is caught (the windowed
+    bit-check of verify_job covers the last step only).  Collective: every rank runs the same
+    steps and reaches the same verdict."""
+    red, p = job.red, job.plan
+    if red.pusher is None or red.full is None:
+        return {"audited_steps": 0, "verified": True, "note": "no push gather"}
+    idx = (torch.arange(max(p.widths), dtype=torch.int64, device=dev) % 65521) + 1
+    real = red.reduce_fn
+    sent = {}
+
+    def hooked(lo, sc, out):
+        real(lo, sc, out)
+        sent[lo] = _checksums(out, idx)
+
+    red.reduce_fn = hooked
+    bad = []
+    try:
+        for s in range(steps):
+            if _AUDIT_FAULT is not None:
+                _AUDIT_FAULT(s, red)
+            sent.clear()
+            red.step()
+            mine = torch.stack([sent[p.local_begin(c)] for c in range(p.stripes)])  # [stripes, 2]
+            every = torch.empty((world, p.stripes, 2), dtype=torch.int64, device=dev)
+            fa_dist.all_gather_into(every.view(-1), mine.reshape(-1), group=None)
+            got = torch.stack([torch.stack([_checksums(red.full[p.global_begin(c, r): p.global_begin(c, r) + p.widths[c]], idx)
+                                            for c in range(p.stripes)]) for r in range(world)])
+            wrong = (got != every).any(dim=2).nonzero().tolist()
+            if wrong:
+                bad.append({"step": s, "slices": [{"sender": r, "stripe": c} for r, c in wrong][:8]})
+    finally:
+        red.reduce_fn = real
+    # every rank's verdict (a slice may be wrong on one receiver only)
+    flags = torch.tensor([len(bad)], dtype=torch.int64, device=dev)
+    all_flags = torch.empty(world, dtype=torch.int64, device=dev)
+    fa_dist.all_gather_into(all_flags, flags)
+    n_bad = [int(x) for x in all_flags.tolist()]
+    return {"audited_steps": steps, "verified": sum(n_bad) == 0, "bad_steps_by_rank": n_bad,
+            "first_bad": bad[:3], "checksums": "sum and position-weighted sum of the fp32 bit patterns, per "
+                                                "(sender, stripe) slice: sender's after its reduce vs every receiver's bucket"}
+
+
 def gather_probe(job, world, dev, reps: int = 5) -> dict:
     """All-gather rate of this job's local width (RCCL over xGMI at N > 1), outside the timed
     region: every GPU receives (world-1) slices, one over each peer link (one xGMI link per peer
@@ -850,16 +909,22 @@ class Watchdog:
                 what, annotate = self._what, self._annotate
             if not fire:
                 continue
-            log(f"[rank {self.rank}] WATCHDOG: {what} overran its budget; ending with the held line")
-            if self.held.line is not None and annotate is not None:
-                try:
-                    annotate(self.held.line)
-                except Exception:  # noqa: BLE001 - the line goes out whatever the annotation does
-                    pass
-            self.held.emit()
-            sys.stdout.flush()
-            sys.stderr.flush()
-            os._exit(self.held.exit_code)
+            try:
+                log(f"[rank {self.rank}] WATCHDOG: {what} overran its budget; ending with the held line")
+                with self.held._lock:  # a copy: the main thread may still be refining the line
+                    line = None if self.held.line is None else json.loads(json.dumps(self.held.line))
+                if line is not None and annotate is not None:
+                    try:
+                        annotate(line)
+                    except Exception:  # noqa: BLE001 - the line goes out whatever the annotation does
+                        pass
+                    with self.held._lock:
+                        self.held.line = line
+                self.held.emit()
+                sys.stdout.flush()
+                sys.stderr.flush()
+            finally:  # whatever the emit did, the hang it bounds ends here
+                os._exit(self.held.exit_code)
 
 
 def job_extras(job, step_s, info, args, cfg, world, dev, g_eff, main_n, backend):
@@ -966,6 +1031,25 @@ def _end_with_held_line(held, rank, e):
     os._exit(held.exit_code)
 
 
+_OUTCOME_ROUND = [0]
+
+
+def _agree_outcomes(status: str, rank: int, world: int, timeout_s: float):
+    """Every rank's push-phase outcome via the process group's store (no collective); None when
+    some rank has not posted within timeout_s."""
+    from datetime import timedelta
+
+    store = dist.distributed_c10d._get_default_store()
+    _OUTCOME_ROUND[0] += 1
+    keys = [f"flearn_bench/push_outcome/{_OUTCOME_ROUND[0]}/{r}" for r in range(world)]
+    store.set(keys[rank], status)
+    try:
+        store.wait(keys, timedelta(seconds=timeout_s))
+    except Exception:  # noqa: BLE001 - a timeout: a peer is stuck or gone
+        return None
+    return [store.get(k).decode() for k in keys]
+
+
 def _exit_code(check) -> int:
     return verify.EXIT_MISMATCH if (check is not None and not check["verified"]) else 0
 
@@ -994,6 +1078,27 @@ def _install_injections(rank):
             return real_push(self, src, shifted)
 
         fa_dist.PushGather.push = off_push
+    if inject == "push_skip_mid" and rank == 1:
+        # rehearsal of a gather that goes wrong in ONE step that is neither the last timed step nor
+        # the one verify_job bit-checks (tests/test_gpu_bench.py): rank 1 skips its push of the
+        # first stripe in the 8th audited step — the step audit must catch it, the line keep RCCL
+        real_push = fa_dist.PushGather.push
+        skip = {"armed": False}
+
+        def skipping_push(self, src, elem_offset):
+            if skip["armed"]:
+                skip["armed"] = False
+                log("[rank 1] INJECTED: skipping one push in an audited step")
+                return None
+            return real_push(self, src, elem_offset)
+
+        def fault(step, red):
+            if step == 7:
+                skip["armed"] = True
+
+        fa_dist.PushGather.push = skipping_push
+        global _AUDIT_FAULT
+        _AUDIT_FAULT = fault
     if inject == "push_stall" and rank == 1:
         # rehearsal of a rank that never comes back from the push set-up (tests/test_gpu_bench.py):
         # the watchdog must still print the verified RCCL line within the budget
@@ -1164,8 +1269,17 @@ def main():
                     pjob, pstep, pwall, ptinfo = timed_job(cfg, layout, main_n, pplan, pg_name, pinfo.get("push_grid"),
                                                            args, world, dev, g_eff)
                     pinfo.update(ptinfo)
+                    log(f"[rank {rank}] auditing {AUDIT_STEPS} more steps of the {pg_name} gather ...")
+                    paudit = push_audit(pjob, world, dev)
+                    pinfo["push_audit"] = paudit
                     pcheck = self_check(pjob)
-                    if pcheck is not None and not pcheck["verified"]:
+                    if not paudit["verified"]:
+                        status = "failed_self_check"
+                        pinfo["push_failed_self_check"] = {"gather": pg_name, "audit": paudit,
+                                                           "mismatched_windows": None if pcheck is None else
+                                                           pcheck["mismatched_windows"]}
+                        log(f"[rank {rank}] the {pg_name} gather failed its step audit: keeping the RCCL line")
+                    elif pcheck is not None and not pcheck["verified"]:
                         status = "failed_self_check"
                         pinfo["push_failed_self_check"] = {"gather": pg_name, "mismatched_windows": pcheck["mismatched_windows"],
                                                            "first_mismatches": pcheck.get("first_mismatches")}
@@ -1175,14 +1289,19 @@ def main():
                     else:
                         status = "adopted"
                     ph.update(ms_per_step=round(pstep * 1e3, 4), gather=pg_name,
-                              verified=None if pcheck is None else pcheck["verified"])
+                              verified=None if pcheck is None else pcheck["verified"],
+                              audited_steps=paudit["audited_steps"], audit_verified=paudit["verified"])
             except Exception as e:  # noqa: BLE001 - any failure here leaves the RCCL line standing
                 log(f"[rank {rank}] push phase failed: {type(e).__name__}: {e}")
                 ph["error"] = f"{type(e).__name__}: {e}"
-            # every rank's outcome (a rank that raised may not have joined the others' collectives:
-            # if they hang, the watchdog ends the run with the held line)
-            outcomes = [None] * world
-            dist.all_gather_object(outcomes, status)
+            # every rank's outcome, through the store rather than a collective: a rank that raised
+            # may have left its peers inside one of the phase's collectives, and a collective here
+            # could pair with theirs.  Peers that never post theirs are stuck: this rank then ends
+            # with the held line (and their watchdogs end them)
+            outcomes = _agree_outcomes(status, rank, world, max(args.push_budget_s - (time.perf_counter() - t_phase), 5.0))
+            if outcomes is None:
+                ph["status"] = "error"
+                _end_with_held_line(held, rank, RuntimeError("a peer never posted its push-phase outcome"))
             adopt = all(o == "adopted" for o in outcomes)
             ph["status"] = "adopted" if adopt else next((o for o in outcomes if o != "adopted"), status)
             ph["rank_outcomes"] = outcomes
@@ -1208,6 +1327,11 @@ def main():
             elif pjob is not None:
                 pjob.release()
             ph["elapsed_s"] = round(time.perf_counter() - t_phase, 1)
+            # the push gathers' receive buckets on this rank: mapped by the pool, and released ones
+            # parked for reuse (bounded: fa_dist.PARK_CAP x the largest exported)
+            line["multi_gpu"]["push_receive_buckets"] = {
+                "pool_bytes": fa_dist._RecvPool.bytes_held(), "parked_bytes": fa_dist.DeviceBuffer.parked_bytes(dev),
+                "park_cap_bytes": fa_dist.DeviceBuffer.park_cap(dev), "trimmed": fa_dist.DeviceBuffer.trimmed()}
             dist.barrier()
             dog.disarm()
 

@@ -13,6 +13,7 @@ from .strategy import AVG, AVGM, BN, LG, LG_R, OPT, SGD, BaseEncrypt, Distill, D
 from .strategy import convert_to_np, convert_to_tensor
 from .utils import base_strategy_lst, setup_seed, setup_strategy
 from .wire import Encrypt
+from .slab import device_state_dicts
 
 __version__ = "0.1.0"
 
@@ -36,4 +37,5 @@ __all__ = [
     "setup_strategy",
     "setup_seed",
     "base_strategy_lst",
+    "device_state_dicts",
 ]

@@ -17,7 +17,8 @@ from pathlib import Path
 import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 
 LIB_PATH = Path(__file__).resolve().parent / "lib" / "libflearn_amd.so"
-ABI_VERSION = 13
+ABI_VERSION = 14
+FENCE_RELEASE, FENCE_ACQUIRE = 0, 1  # fa_cache_fence kinds
 
 FA_OK = 0
 FA_ERR_ARG, FA_ERR_ALIGN, FA_ERR_LAUNCH = -1, -2, -3
@@ -53,6 +54,7 @@ EXPORTS = (
     "fa_copy_dma",
     "fa_push_dma",
     "fa_stream_join",
+    "fa_cache_fence",
     "fa_set_reduce_grid",
     "fa_reduce_windows",
     "fa_b64_decoded_size",
@@ -211,6 +213,7 @@ def load(require_gpu: bool = False):
                 "fa_copy_dma": ([P, P, I64, P], ctypes.c_int),
                 "fa_push_dma": ([P, I64, ctypes.POINTER(P), I32, ctypes.POINTER(P), P], ctypes.c_int),
                 "fa_stream_join": ([P, ctypes.POINTER(P), I32], ctypes.c_int),
+                "fa_cache_fence": ([I32, P], ctypes.c_int),
                 "fa_set_reduce_grid": ([I32], ctypes.c_int),
                 "fa_reduce_windows": ([I32, I64], ctypes.c_int),
                 "fa_b64_decoded_size": ([P, I64], I64),

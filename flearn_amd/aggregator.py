@@ -318,12 +318,41 @@ class ServerOptimizer:
         self.spare = {}  # shard index -> (prev, v) buffers the next fused step writes into
         self._sig = None
         self._pending_init = None
+        self._pending_v = None
+        self._plan = None  # the bucket plan the state is bound to (the last round's)
         self.group = None  # (process group, world) when bound to a column-sharded Aggregator
 
     def init_global(self, glob: dict):
         """Set the previous global model (dict of arrays/tensors); v_t is reset to zeros."""
-        self._pending_init = {k: np.asarray(v.cpu() if isinstance(v, torch.Tensor) else v) for k, v in glob.items()}
+        self._pending_init = {k: _host_array(v) for k, v in glob.items()}
+        self._pending_v = None
         self.state, self._sig = {}, None
+
+    def set_v_t(self, v_t: dict):
+        """Restore v_t — the dict `v_t()` returns (keyed like w_glob, f64, or fp32 when the
+        weights make w_glob float32) — for the next fused round.  Follows `init_global` (or
+        `load_state`): the state a restarted server needs is the previous global model AND v_t
+        (avgm.py:28-32 / opt.py:45-60 keep v_t across rounds).  Applied when the next round binds
+        the state to its bucket; a key of the model that v_t lacks, or a shape that differs,
+        raises there (KeyError / ValueError)."""
+        if self._pending_init is None:
+            raise RuntimeError("set_v_t restores v_t next to a previous global model: call init_global(w_glob) "
+                               "first (or load_state)")
+        self._pending_v = {k: _host_array(v) for k, v in v_t.items()}
+
+    def load_state(self, state: dict):
+        """Restore what `state_dict()` returned ({"w_glob": previous global, "v_t": v_t}; without
+        "v_t" it is zeros, as after init_global)."""
+        self.init_global(state["w_glob"])
+        if state.get("v_t") is not None:
+            self.set_v_t(state["v_t"])
+
+    def state_dict(self, plan: BucketPlan | None = None) -> dict:
+        """{"w_glob": the fp32 previous global model the next fused round starts from, "v_t":
+        v_t()} as host arrays keyed like w_glob (plan: the last round's by default): what
+        `load_state` restores on a fresh optimizer.  With a column-sharded process group this is a
+        collective (two all-gathers)."""
+        return {"w_glob": self._host_dict(plan, 0), "v_t": self._host_dict(plan, 1)}
 
     @staticmethod
     def _signature(plan: BucketPlan, shards):
@@ -342,20 +371,30 @@ class ServerOptimizer:
         sig = self._signature(plan, shards)
         if self._pending_init is not None:
             prev = np.zeros(g.stride, dtype=np.float32)
+            vdt = np.float32 if self._vdtype(plan) == torch.float32 else np.float64
+            vflat = np.zeros(g.stride, dtype=vdt)
             for s in g.segments:
                 prev[s.offset : s.offset + s.numel] = np.asarray(self._pending_init[s.key], np.float32).reshape(-1)
+                if self._pending_v is not None:
+                    if s.key not in self._pending_v:
+                        raise KeyError(s.key)
+                    v = np.asarray(self._pending_v[s.key])
+                    if tuple(v.shape) != tuple(s.shape):
+                        raise ValueError(f"v_t[{s.key!r}] shape {v.shape} != model shape {tuple(s.shape)}")
+                    vflat[s.offset : s.offset + s.numel] = v.astype(vdt, copy=False).reshape(-1)
             self.state = {
                 sh.index: (torch.from_numpy(prev[sh.c0 : sh.c1].copy()).to(sh.device),
-                           torch.zeros(sh.width, dtype=self._vdtype(plan), device=sh.device))
+                           torch.from_numpy(vflat[sh.c0 : sh.c1].copy()).to(sh.device))
                 for sh in shards
             }
-            self._sig = sig
-            self._pending_init = None
+            self._sig, self._plan = sig, plan
+            self._pending_init = self._pending_v = None
             return True
         if self._sig is None:
             return False
         if sig != self._sig:
             raise ValueError("model layout changed between rounds; call init_global() again")
+        self._plan = plan
         return True
 
     def adopt(self, plan: BucketPlan, shards, means: dict):
@@ -363,7 +402,7 @@ class ServerOptimizer:
         self.state = {sh.index: (means[sh.index][: sh.width].clone(),
                                  torch.zeros(sh.width, dtype=self._vdtype(plan), device=sh.device))
                       for sh in shards}
-        self._sig = self._signature(plan, shards)
+        self._sig, self._plan = self._signature(plan, shards), plan
 
     def swap_buffers(self, sh):
         """(prev, v, prev_out, v_out) of a fused step on shard sh, and the state advanced to the
@@ -381,22 +420,33 @@ class ServerOptimizer:
         pair it had: the spare buffers hold nothing yet)."""
         self.state[sh.index], self.spare[sh.index] = self.spare[sh.index], self.state[sh.index]
 
-    def v_t(self, plan: BucketPlan) -> dict:
-        """The state as the reference exposes it (self.v_t dict of arrays).  With a column-sharded
+    def v_t(self, plan: BucketPlan | None = None) -> dict:
+        """The state as the reference exposes it (self.v_t dict of arrays; plan: the last round's by
+        default).  With a column-sharded
         process group (Aggregator(group=...)) every rank holds only its columns: this is then a
         collective (an all-gather) that every rank must call."""
+        return self._host_dict(plan, 1)
+
+    def _host_dict(self, plan: BucketPlan, i: int) -> dict:
+        """State i (0: prev, 1: v_t) over the whole bucket, keyed like w_glob."""
+        plan = plan if plan is not None else self._plan
+        if not self.state or plan is None:
+            raise RuntimeError("no server optimizer state yet (no fused round has run)")
         if self.group is not None:
             from .bucket import rank_width
             from .dist import gather_columns
 
-            (sh_v,) = [self.state[i][1] for i in sorted(self.state)]
+            (loc,) = [self.state[j][i] for j in sorted(self.state)]
             group, world = self.group
             stride = plan.f32.stride
-            full = gather_columns(sh_v, rank_width(stride, world), stride, group)
-            host = full.cpu().numpy()
-            return {s.key: host[s.offset : s.offset + s.numel].reshape(s.shape).copy() for s in plan.f32.segments}
-        host = np.concatenate([self.state[i][1].cpu().numpy() for i in sorted(self.state)])
+            host = gather_columns(loc, rank_width(stride, world), stride, group).cpu().numpy()
+        else:
+            host = np.concatenate([self.state[j][i].cpu().numpy() for j in sorted(self.state)])
         return {s.key: host[s.offset : s.offset + s.numel].reshape(s.shape).copy() for s in plan.f32.segments}
+
+
+def _host_array(v):
+    return np.asarray(v.detach().cpu() if isinstance(v, torch.Tensor) else v)
 
 
 def _as_host(v):
@@ -687,6 +737,8 @@ class Aggregator:
                         (reduce_stack_f64 if kind == KIND_F64 else reduce_stack_i64)(stack, w, nm.denom, out)
                 res.append((sh, out))
             results[kind] = res
+            if self.packer.last_row_tables.get(kind) == "slab":  # the caller's memory, read in place:
+                self.packer.hold([st for _, st in parts], parts[0][0].device)  # alive until read
         if server_opt is not None and first_means:
             server_opt.adopt(plan, [sh for sh, _ in stacks[KIND_F32]], first_means)
         if self._dist and KIND_F32 in results:

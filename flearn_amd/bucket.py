@@ -467,7 +467,14 @@ class Packer:
             if pieces is None:
                 pieces = plan.memo[pk] = self._pieces(g, shards)
             if plan.input_kind == "torch" and all(w_local_lst[0][s.key].device.type == "cuda" for s in g.segments):
-                table = self.row_table(plan, g, w_local_lst, shards)
+                rp = self._row_ptrs(plan, g, w_local_lst, shards)
+                if rp is not None and kind == KIND_F32:
+                    slab = self._slab_stack(plan, g, w_local_lst, rp)
+                    if slab is not None:  # one allocation laid out as the bucket: the stack itself
+                        out[kind] = [(shards[0], slab)]
+                        self.last_row_tables[kind] = "slab"
+                        continue
+                table = RowTable(self, plan, g, *rp, shards[0].device) if rp is not None else None
                 if table is not None and kind == KIND_F32 and len(shards) == 1 and table.aligned:
                     out[kind] = [(shards[0], table)]  # read in place by fa_reduce_f32_rows
                     self.last_row_tables[kind] = "rows"
@@ -512,6 +519,42 @@ class Packer:
         not a contiguous tensor of an accepted dtype on the bucket's (single, whole-bucket)
         device.  Accepted: the store dtype; for the float64 group also int64 and float32 values
         (BN num_batches_tracked), which fa_gather_rows_f64 converts as numpy's promotion does."""
+        rp = self._row_ptrs(plan, g, w_local_lst, shards)
+        return None if rp is None else RowTable(self, plan, g, *rp, shards[0].device)
+
+    @staticmethod
+    def _slab_stack(plan: BucketPlan, g: Group, w_local_lst, rp):
+        """The uploads as a [N, stride] stack view when every client's fp32 tensors sit in ONE
+        allocation laid out exactly as this bucket — key k of client n at row_base + n * pitch +
+        offset(k), the same pitch for every client (flearn_amd.device_state_dicts makes such
+        uploads) — else None.  The stack kernel then reads them in place: no pointer table, and
+        the translations of one allocation instead of one per (client, tensor) (the row-pointer
+        kernel's 7-8% at NS)."""
+        segs, ptrs, keep, _src = rp
+        n = plan.n_clients
+        if not segs or ptrs.shape[1] != n:
+            return None
+        off = np.array([s.offset for s in segs], dtype=np.int64) * 4
+        base = ptrs[0] - off[0]  # each client's row start
+        if not np.array_equal(ptrs - off[:, None], np.broadcast_to(base, ptrs.shape)):
+            return None
+        pitch = int(base[1] - base[0]) if n > 1 else g.stride * 4
+        if n > 1 and not (np.diff(base) == pitch).all():
+            return None
+        if pitch < g.stride * 4 or pitch % 16 or int(base[0]) % 16:
+            return None
+        t0 = w_local_lst[0][segs[0].key]
+        st = t0.untyped_storage()
+        lo, hi = st.data_ptr(), st.data_ptr() + st.nbytes()
+        first, end = int(base[0]), int(base[0]) + (n - 1) * pitch + g.stride * 4
+        if first < lo or end > hi:  # the rows must lie inside that one allocation
+            return None
+        return torch.empty(0, dtype=torch.float32, device=t0.device).set_(
+            st, (first - lo) // 4, (n, g.stride), (pitch // 4, 1))
+
+    def _row_ptrs(self, plan: BucketPlan, g: Group, w_local_lst, shards):
+        """(segments, pointer table [segments][clients], tensors kept, source kinds) of
+        device-resident uploads — row_table's inputs — or None."""
         if len(shards) != 1 or shards[0].c0 != 0 or shards[0].c1 != g.stride:
             return None
         dev = shards[0].device
@@ -530,7 +573,7 @@ class Packer:
             lst = w_local_lst if type(w_local_lst) is list else list(w_local_lst)
             index = dev.index if dev.index is not None else torch.cuda.current_device()
             if L.fa_tm_tensor_ptrs(lst, tuple(s.key for s in segs), dts, index, ptrs.ctypes.data, keep) == 0:
-                return RowTable(self, plan, g, segs, ptrs, keep, dev, src)
+                return segs, ptrs, keep, src
         keep = []
         for j, s in enumerate(segs):
             row = ptrs[j]
@@ -540,7 +583,7 @@ class Packer:
                     return None
                 row[n] = t.data_ptr()
                 keep.append(t)
-        return RowTable(self, plan, g, segs, ptrs, keep, dev, src)
+        return segs, ptrs, keep, src
 
     def _wire_stack(self, g: Group, w_local_lst, device):
         from .wire import wire_device_stack
@@ -785,7 +828,7 @@ class RowTable:
     recorded after them is checked at the next use of the packer), so the caching allocator
     cannot hand their memory to another stream meanwhile."""
 
-    def __init__(self, packer: Packer, plan: BucketPlan, g: Group, segs, ptrs: np.ndarray, keep, device, src=None):
+    def __init__(self, packer: Packer, plan: BucketPlan, g: Group, segs, ptrs: np.ndarray, keep, src, device):
         self.packer, self.plan, self.group, self.segs = packer, plan, g, segs
         self.src = tuple(src) if src is not None else (na.SRC_F64,) * len(segs)  # per segment
         self.converts = any(k != na.SRC_F64 for k in self.src)  # some segment is not the store dtype

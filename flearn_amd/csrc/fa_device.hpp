@@ -1544,6 +1544,18 @@ struct PushDsts {
   uint8_t* p[8];
 };
 
+// One system-scope cache fence per wave: RELEASE (K = 0) writes the L2 back to HBM, ACQUIRE
+// (K = 1) invalidates it, so that a copy engine (which reads and writes HBM behind the L2) and the
+// kernels around it see each other's data (fa_cache_fence).  Each XCD has its own L2: the launch
+// spreads one wave over every XCD, several times over.
+template <int K>
+__global__ __launch_bounds__(64) void cache_fence_kernel() {
+  if (K == 0)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  else
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+}
+
 __global__ __launch_bounds__(kThreads) void push_kernel(const uint8_t* __restrict__ src, int64_t quads, PushDsts d,
                                                         int n_dsts) {
   typedef uint32_t u4 __attribute__((ext_vector_type(4)));

@@ -925,6 +925,18 @@ int fa_push_dma(const void* src, int64_t nbytes, void* const* dsts, int32_t n_ds
   return FA_OK;
 }
 
+int fa_cache_fence(int32_t kind, void* stream) {
+  // 64 one-wave blocks: workgroups are dealt round-robin over the 8 XCDs, so every XCD's L2 gets
+  // the fence from several waves
+  if (kind == FA_FENCE_RELEASE)
+    hipLaunchKernelGGL(cache_fence_kernel<0>, dim3(64), dim3(64), 0, static_cast<hipStream_t>(stream));
+  else if (kind == FA_FENCE_ACQUIRE)
+    hipLaunchKernelGGL(cache_fence_kernel<1>, dim3(64), dim3(64), 0, static_cast<hipStream_t>(stream));
+  else
+    return fail(FA_ERR_ARG, "unknown cache fence kind");
+  return launch_check();
+}
+
 int fa_stream_join(void* stream, void* const* streams, int32_t n) {
   if (n < 0 || n > 16 || (n > 0 && !streams)) return fail(FA_ERR_ARG, "bad stream list");
   for (int i = 0; i < n; ++i) {

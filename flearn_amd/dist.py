@@ -47,6 +47,16 @@ from .streams import side_stream
 ALIGN = 64
 MAX_PUSH_RANKS = 8  # fa_push's destination count: one MI355X node
 
+#: where the copy-engine push's legs take their start event: "producer" (the stream that ran the
+#: stripe's reduce) or "chain" (round 5: the pusher's stream after its wait on the producer, which
+#: let legs start before the reduce ended; kept only so tests/push_order_probe.py can replay it)
+_DMA_ORDER = "producer"
+
+
+def peer_stream(device) -> torch.cuda.Stream:
+    """A copy-engine leg's stream (normal priority; tests/push_order_probe.py overrides it)."""
+    return torch.cuda.Stream(device)
+
 
 def _host_staged(t: torch.Tensor, group) -> bool:
     """gloo cannot be trusted with device tensors for every collective: stage them on the host."""
@@ -65,9 +75,21 @@ def all_gather_into(dst: torch.Tensor, src: torch.Tensor, group=None, async_op: 
     return None
 
 
-#: exported buckets released by their users: never freed while the process lives (see
-#: DeviceBuffer), handed out again by DeviceBuffer.get
+#: exported buckets released by their users, handed out again by DeviceBuffer.get (see
+#: DeviceBuffer); per device they are kept within PARK_CAP x the largest bucket the device has
+#: exported — beyond that the smallest are freed
 _PARKED: list = []
+PARK_CAP = 2
+_LARGEST: dict = {}  # device -> bytes of the largest bucket it has exported
+_TRIMMED = [0, 0]  # exported buckets freed to keep within the cap: (count, bytes)
+
+
+def size_class(nbytes: int) -> int:
+    """Bucket sizes come in four classes per octave (2^k, 1.25, 1.5, 1.75 x 2^k; at least 4 KiB):
+    requests a few percent apart share one class, so released buckets fit the next job's."""
+    nbytes = max(int(nbytes), 4096)
+    step = 1 << max(nbytes.bit_length() - 3, 0)
+    return -(-nbytes // step) * step
 
 
 class DeviceBuffer:
@@ -76,42 +98,88 @@ class DeviceBuffer:
     tensors share and that torch recycles (empty_cache frees it), and hipIpcGetMemHandle exports
     the whole segment; this is one bucket, one export.
 
-    Once exported (`exported`), a bucket is never freed while the process lives: `free()` parks
-    it and `DeviceBuffer.get` hands it out again (re-exporting the same memory).  On this runtime
-    an exporter that frees imported memory and exports again makes 13-34% of later imports map
-    the wrong allocation — another process's bucket or the importer's own — whether or not the
-    freed address is kept out of reuse; with nothing exported ever freed, and a barrier after
-    every unmap, 0 of 1,920 imports were wrong (tools/ipc_probe.py,
-    profiles/r05/ipc/).  `tensor()` views it (torch keeps this object alive while any view
-    does); an unexported buffer is freed by `free()` or when the last view dies."""
+    Once exported (`exported`), `free()` parks a bucket and `DeviceBuffer.get` hands it out again
+    (re-exporting the same memory).  With several processes on one GPU, an exporter that freed
+    imported memory and exported again made 13-34% of later imports map the wrong allocation;
+    with nothing exported freed, and a barrier after every unmap, 0 of 1,920 imports were wrong
+    (profiles/r05/ipc/).  Parking is bounded: per device the parked bytes
+    stay within PARK_CAP x the largest bucket the device has exported, the smallest parked
+    buckets beyond that are freed (`trimmed()` counts them) — a later import that maps the wrong
+    allocation is still refused by the token check of every mapping (_map_peers), so the cost of
+    a trim is at worst a refused push set-up (RCCL's all-gather then), never a wrong bucket.
+    `tensor()` views it (torch keeps this object alive while any view does); an unexported buffer
+    is freed by `free()` or when the last view dies."""
 
     def __init__(self, nbytes: int, device):
         from . import _native as na
 
         self.L, self.na = na.lib(), na
         self.nbytes, self.device = int(nbytes), torch.device(device)
-        self.exported = False  # set when peers may map it: from then on free() parks it
+        self._exported = False
         self._typestr = "<f4"
+        self.ptr = self._alloc()
+
+    def _alloc(self) -> int:
         p = ctypes.c_void_p()
         with torch.cuda.device(self.device):
-            na.check(self.L.fa_dev_alloc(self.nbytes, ctypes.byref(p)), "fa_dev_alloc")
-        self.ptr = p.value
+            self.na.check(self.L.fa_dev_alloc(self.nbytes, ctypes.byref(p)), "fa_dev_alloc")
+        return p.value
+
+    def _release(self, ptr: int):
+        with torch.cuda.device(self.device):
+            self.na.check(self.L.fa_dev_free(ptr), "fa_dev_free")
+
+    @property
+    def exported(self) -> bool:
+        """Set when peers may map it: from then on free() parks it."""
+        return self._exported
+
+    @exported.setter
+    def exported(self, value: bool):
+        if value and not self._exported:
+            key = str(self.device)
+            _LARGEST[key] = max(_LARGEST.get(key, 0), self.nbytes)
+        self._exported = bool(value)
 
     @classmethod
     def get(cls, nbytes: int, device) -> "DeviceBuffer":
         """A parked (previously exported, released) buffer of at least nbytes on `device` — the
-        smallest that fits — or a new one."""
+        smallest that fits — or a new one of nbytes' size class."""
         dev = torch.device(device)
         fits = [b for b in _PARKED if b.device == dev and b.nbytes >= nbytes]
         if fits:
             b = min(fits, key=lambda x: x.nbytes)
             _PARKED.remove(b)
             return b
-        return cls(nbytes, dev)
+        return cls(size_class(nbytes), dev)
 
     @staticmethod
-    def parked_bytes() -> int:
-        return sum(b.nbytes for b in _PARKED)
+    def parked_bytes(device=None) -> int:
+        return sum(b.nbytes for b in _PARKED if device is None or b.device == torch.device(device))
+
+    @staticmethod
+    def park_cap(device) -> int:
+        return PARK_CAP * _LARGEST.get(str(torch.device(device)), 0)
+
+    @staticmethod
+    def trimmed() -> dict:
+        return {"buckets": _TRIMMED[0], "bytes": _TRIMMED[1]}
+
+    @staticmethod
+    def _trim(device):
+        """Free the smallest parked buckets of `device` until the parked bytes fit the cap."""
+        cap = DeviceBuffer.park_cap(device)
+        parked = sorted((b for b in _PARKED if b.device == device), key=lambda b: b.nbytes)
+        total = sum(b.nbytes for b in parked)
+        for b in parked:
+            if total <= cap:
+                break
+            _PARKED.remove(b)
+            total -= b.nbytes
+            ptr, b.ptr = b.ptr, None
+            b._release(ptr)
+            _TRIMMED[0] += 1
+            _TRIMMED[1] += b.nbytes
 
     @property
     def __cuda_array_interface__(self):
@@ -136,10 +204,10 @@ class DeviceBuffer:
         if self.exported:
             if self not in _PARKED:
                 _PARKED.append(self)
+                DeviceBuffer._trim(self.device)
             return
         ptr, self.ptr = self.ptr, None
-        with torch.cuda.device(self.device):
-            self.na.check(self.L.fa_dev_free(ptr), "fa_dev_free")
+        self._release(ptr)
 
     def __del__(self):
         try:
@@ -155,6 +223,67 @@ def _all_ok(pg, ok: int) -> bool:
     return bool(t.item())
 
 
+class HipIpc:
+    """The IPC transport of the push gather: HIP IPC handles of device allocations (C ABI
+    fa_ipc_*), read back through a copy engine.  `_IPC` is the one in use; the CPU tests put a
+    shared-memory stand-in there to run the pool's collective protocol, token checks included,
+    over gloo (tests/test_recv_pool.py)."""
+
+    @staticmethod
+    def accepts(device) -> bool:
+        return torch.device(device).type == "cuda"
+
+    @staticmethod
+    def sync(device):
+        torch.cuda.synchronize(device)
+
+    @staticmethod
+    def handle(ptr: int):
+        """(handle bytes, byte offset of ptr in its allocation), or None."""
+        from . import _native as na
+
+        h, off = ctypes.create_string_buffer(64), ctypes.c_int64(0)
+        if na.lib().fa_ipc_handle(ptr, h, ctypes.byref(off)) != 0:
+            return None
+        return bytes(h.raw), int(off.value)
+
+    @staticmethod
+    def open(hb: bytes):
+        """The base address a peer's handle maps at here, or None."""
+        from . import _native as na
+
+        base = ctypes.c_void_p()
+        if na.lib().fa_ipc_open(hb, ctypes.byref(base)) != 0 or not base.value:
+            return None
+        return base.value
+
+    @staticmethod
+    def read16(probe: torch.Tensor, addr: int) -> bool:
+        """The 16 bytes at a mapped address into `probe` (4 int32, same device)."""
+        from . import _native as na
+
+        s = torch.cuda.current_stream(probe.device)
+        if na.lib().fa_copy_dma(probe.data_ptr(), addr, 16, s.cuda_stream) != 0:
+            return False
+        s.synchronize()
+        return True
+
+    @staticmethod
+    def close(base: int):
+        from . import _native as na
+
+        na.lib().fa_ipc_close(base)
+
+    @staticmethod
+    def last_error() -> bytes:
+        from . import _native as na
+
+        return na.lib().fa_last_error()
+
+
+_IPC = HipIpc
+
+
 def _map_peers(pg, full: torch.Tensor):
     """Collective: register `full` (IPC handle of its allocation + offset) and map every peer's;
     (opened bases, per-rank device address of each rank's buffer, stale peers).  A token written
@@ -162,22 +291,22 @@ def _map_peers(pg, full: torch.Tensor):
     back through every mapping: an import that maps some other allocation than the one exported
     is refused instead of pushed into (the stale imports of round 4).  Every
     rank raises RuntimeError (nothing left mapped) if any rank cannot map or validate a peer."""
-    L = pg.L
+    ipc = _IPC
     bases, dsts, stale = [], [], []
     ok = 1
     mine = None
     saved = None
-    if pg.world > MAX_PUSH_RANKS or not full.is_cuda or not full.is_contiguous() or full.numel() < 4:
+    if pg.world > MAX_PUSH_RANKS or not ipc.accepts(full.device) or not full.is_contiguous() or full.numel() < 4:
         ok = 0
     else:
         head = full.view(torch.int32)[:4]
         saved = head.clone()
         token = torch.randint(-2**31, 2**31 - 1, (4,), dtype=torch.int32)
         head.copy_(token)
-        torch.cuda.synchronize(full.device)
-        h, off = ctypes.create_string_buffer(64), ctypes.c_int64(0)
-        if L.fa_ipc_handle(full.data_ptr(), h, ctypes.byref(off)) == 0:
-            mine = (bytes(h.raw), int(off.value), token.tolist())
+        ipc.sync(full.device)
+        got = ipc.handle(full.data_ptr())
+        if got is not None:
+            mine = (got[0], got[1], token.tolist())
         else:
             ok = 0
     infos = [None] * pg.world
@@ -188,17 +317,15 @@ def _map_peers(pg, full: torch.Tensor):
             if r == pg.rank:
                 dsts.append(full.data_ptr())
                 continue
-            base = ctypes.c_void_p()
-            if L.fa_ipc_open(hb, ctypes.byref(base)) != 0 or not base.value:
+            base = ipc.open(hb)
+            if base is None:
                 ok = 0
                 break
-            bases.append(base.value)
-            dsts.append(base.value + off)
-            s = torch.cuda.current_stream(full.device)
-            if L.fa_copy_dma(probe.data_ptr(), base.value + off, 16, s.cuda_stream) != 0:
+            bases.append(base)
+            dsts.append(base + off)
+            if not ipc.read16(probe, base + off):
                 ok = 0
                 break
-            s.synchronize()
             if probe.tolist() != tok:
                 stale.append(r)
                 ok = 0
@@ -209,21 +336,21 @@ def _map_peers(pg, full: torch.Tensor):
         full.view(torch.int32)[:4].copy_(saved)
     if not agreed:
         for b in bases:
-            L.fa_ipc_close(b)
+            ipc.close(b)
         dist.barrier(group=pg.group)  # nobody exports again while a peer is still closing
-        err = L.fa_last_error()
+        err = ipc.last_error()
         why = (f" (here: the mappings of ranks {stale} did not hold their tokens)" if stale else
                f" (here: {err.decode(errors='replace')})" if err and not ok else "")
         raise RuntimeError("PushGather: a rank could not map its peers' receive buffers" + why)
     return bases, dsts, stale
 
 
-def _unmap_all(L, bases, group):
+def _unmap_all(bases, group):
     """Collective: close this rank's imports, then a barrier — after it no peer is still closing
     an import when any rank exports again (exporting while a peer closes made a third of the
     probe's imports map the wrong allocation: DESIGN.md section 6)."""
     for b in bases:
-        L.fa_ipc_close(b)
+        _IPC.close(b)
     dist.barrier(group=group)
 
 
@@ -247,8 +374,9 @@ class _RecvPool:
     the buckets are parked (DeviceBuffer: exported memory is never freed while the process lives
     — freeing it is what made later imports map the wrong allocation) for
     the next pool to re-export.  A `take` that finds no free bucket large enough first releases
-    the free ones (same protocol) and takes a parked or new one with 1/8 headroom, so the
-    buckets held stay near the largest set in use at once.  Every rank takes and gives in the
+    the free ones (same protocol) and takes a parked one that fits or a new one of the request's
+    size class (DeviceBuffer.get), so the buckets held stay near the largest set in use at once
+    and the parked ones within DeviceBuffer's cap.  Every rank takes and gives in the
     same order, so the slots agree across ranks (checked at each take).
 
     Keyed by the group OBJECT (held, so its id cannot be reused by a later group): a destroyed and
@@ -283,7 +411,7 @@ class _RecvPool:
         buckets are parked (same indices on every rank)."""
         if not idx:
             return
-        _unmap_all(pg.L, [b for i in idx for b in self.slots[i][3]], pg.group)
+        _unmap_all([b for i in idx for b in self.slots[i][3]], pg.group)
         for i in sorted(idx, reverse=True):
             buf = self.slots.pop(i)[0]
             buf.free()  # exported: parked for reuse, never freed
@@ -296,11 +424,11 @@ class _RecvPool:
             raise RuntimeError(f"PushGather: the ranks' receive pools disagree ({picks})")
         if i is None:  # retire the free buckets that are too small, then a new one (collective)
             self._retire(pg, [j for j, s in enumerate(self.slots) if not s[4]])
-            if torch.device(self.device).type != "cuda":  # refused on every rank together
+            if not _IPC.accepts(self.device):  # refused on every rank together
                 pg.device = torch.device(self.device)
                 _map_peers(pg, torch.empty(4))
             want = max(cols, 4)
-            buf = DeviceBuffer.get((want + want // 8 + ALIGN) // ALIGN * ALIGN * 4, self.device)
+            buf = DeviceBuffer.get(-(-want // ALIGN) * ALIGN * 4, self.device)
             view = buf.tensor(torch.float32)
             pg.full, pg.device = view, self.device
             buf.exported = True  # from here on never freed: parked when released
@@ -331,7 +459,7 @@ class _RecvPool:
     def _drop_local(self):
         for s in self.slots:
             for b in s[3]:
-                s[0].L.fa_ipc_close(b)
+                _IPC.close(b)
             s[0].free()
         self.slots = []
 
@@ -341,15 +469,11 @@ def shutdown_push(group=None, device=None):
     that group — every peer's mapping closed, then a barrier, then each rank parks its own
     (DeviceBuffer.get hands them to the next pool; exported memory is never freed).  Call it
     before dist.destroy_process_group; the next push job maps its buckets afresh."""
-    from . import _native as na
-
     g = _resolve_group(group)
     for key in [k for k, p in _RecvPool._pools.items() if p.gobj is g
                 and (device is None or k[0] == str(torch.device(device)))]:
         pool = _RecvPool._pools.pop(key)
-        ctx = type("_Ctx", (), {})()
-        ctx.L, ctx.group = na.lib(), group
-        pool.shutdown(ctx)
+        pool.shutdown(type("_Ctx", (), {"group": group})())
 
 
 class PushGather:
@@ -400,19 +524,15 @@ class PushGather:
                 self.owner, full = full, full.tensor(torch.float32)
             self.full, self.device = full, full.device
             self.bases, self.dst, self.stale = _map_peers(self, full)
-        # kernel push: a high-priority stream, whose hardware queue is apart from the compute
-        # stream's — on a shared queue the push kernels run in queue order with the next stripes'
-        # reduces instead of beside them (streams.py).  Copy-engine push: normal priority — its
-        # legs run on the copy engines whatever queue their stream has, and with high-priority
-        # streams they gave wrong buckets (32 of 576 in-place Adagrad rank-steps at world 8, 0 at
-        # normal priority: streams.py)
-        self.stream = side_stream(self.device) if mode == "kernel" else torch.cuda.Stream(self.device)
+        # a high-priority stream, whose hardware queue is apart from the compute stream's — on a
+        # shared queue the push kernels run in queue order with the next stripes' reduces instead
+        # of beside them (streams.py)
+        self.stream = side_stream(self.device)
         self.flag = torch.zeros(1, dtype=torch.float32, device=self.device)
         self.grid = 0  # fa_push blocks (0: the library's default)
         # mode "dma": one stream per peer, each leg a copy-engine copy (fa_copy_dma) — copies on
         # one stream would run one after the other, one link at a time
-        self.peer_streams = ([torch.cuda.Stream(self.device) for _ in range(self.world - 1)] if mode == "dma"
-                             else [])
+        self.peer_streams = [peer_stream(self.device) for _ in range(self.world - 1)] if mode == "dma" else []
         self._peer_handles = (ctypes.c_void_p * max(1, len(self.peer_streams)))(
             *[s.cuda_stream for s in self.peer_streams]) if self.peer_streams else None
 
@@ -443,11 +563,17 @@ class PushGather:
             self.na.check(self.L.fa_push(src.data_ptr(), n, dsts, self.world, self.grid, self.stream.cuda_stream),
                           "fa_push")
             return
-        # copy engines: the peers' legs on their own streams (after the step's barrier and the
-        # stripe's reduce: one native call), this rank's own copy by a kernel on the pusher's stream
+        # copy engines: the peers' legs on their own streams, each after an event recorded on the
+        # stream that RAN the stripe's reduce (one native call), this rank's own copy by a kernel on
+        # the pusher's stream.  The legs' event must come from the producer itself: recorded on the
+        # pusher's stream, whose only work queued since is a wait on the producer, it did not carry
+        # that wait — the legs then copied half-written slices (the round-5
+        # wrong buckets, tools/probe_event_chain.hip).  `_DMA_ORDER = "chain"` replays that order
+        # for tests/push_order_probe.py.
+        after = self.stream if _DMA_ORDER == "chain" else cur
         peers = (ctypes.c_void_p * (self.world - 1))(*[d + off for r, d in enumerate(self.dst) if r != self.rank])
         self.na.check(self.L.fa_push_dma(src.data_ptr(), n, peers, self.world - 1, self._peer_handles,
-                                         self.stream.cuda_stream), "fa_push_dma")
+                                         after.cuda_stream), "fa_push_dma")
         self.na.check(self.L.fa_copy(self.dst[self.rank] + off, src.data_ptr(), n, self.stream.cuda_stream), "fa_copy")
 
     def join(self):
@@ -479,7 +605,7 @@ class PushGather:
                 self.pool.give(self.pool_slot)
                 self.pool_slot, self.dst = None, []
             else:
-                _unmap_all(self.L, self.bases, self.group)
+                _unmap_all(self.bases, self.group)
                 self.bases, self.dst = [], []
 
 

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define FA_ABI_VERSION 13
+#define FA_ABI_VERSION 14
 
 /* return codes */
 #define FA_OK 0
@@ -293,6 +293,13 @@ int fa_push_dma(const void* src, int64_t nbytes, void* const* dsts, int32_t n_ds
 
 /* `stream` waits for the work queued so far on streams[0..n) (n <= 16).  ABI 12.             */
 int fa_stream_join(void* stream, void* const* streams, int32_t n);
+
+/* A system-scope cache fence on every XCD's L2, queued on `stream`: FA_FENCE_RELEASE writes the
+ * L2 back to HBM (before a copy engine reads what kernels wrote), FA_FENCE_ACQUIRE invalidates it
+ * (before kernels read what a copy engine or a peer wrote).  ABI 14.                          */
+#define FA_FENCE_RELEASE 0
+#define FA_FENCE_ACQUIRE 1
+int fa_cache_fence(int32_t kind, void* stream);
 
 /* ---- wire codec (HOST functions: every pointer below is host memory) -------------------------
  * flearn's HTTP mode ships uploads and global models as base64(pickle.dumps(obj))

@@ -1,10 +1,14 @@
 """Are the push gather's copies ordered after the stripe's reduce when the pusher's streams have
-their own hardware queue?  (round 5)
+their own hardware queue?  (rounds 5-6)
 
-    python tests/push_order_probe.py --world 8 --steps 3 --reps 6 --priorities normal,high,product
+    python tests/push_order_probe.py --world 8 --steps 3 --reps 6 --priorities normal,high,product \
+        --dma-orders producer,chain
 
-(round 5: with the copy-engine push's streams at high priority, 32 of 576 in-place Adagrad
-rank-steps were wrong; flearn_amd.dist now gives only the kernel push a high-priority stream)
+(round 5: with the copy-engine push's pusher stream at high priority, 32 of 576 in-place Adagrad
+rank-steps were wrong.  Round 6: the legs waited on an event recorded on the pusher's stream after
+its wait on the reduce's stream — `--dma-orders chain` replays that; "producer", the product's
+order now, records the legs' event on the reduce's own stream.  "high" puts the pusher's stream
+AND every leg's stream at high priority: none of them shares the compute stream's hardware queue)
 
 `world` processes share cuda:0 over gloo (like tests/test_gpu_multirank.py); each runs
 ShardedReducer steps with the fused Adagrad epilogue in place (the reduce reads `prev` and writes
@@ -23,13 +27,15 @@ import json
 import os
 import socket
 import sys
+import time
 from pathlib import Path
 
 REPO = Path(__file__).resolve().parent.parent
 sys.path.insert(0, str(REPO))
 
 
-def _worker(rank, world, port, modes, priorities, steps, reps, out_path):
+def _worker(rank, world, port, modes, priorities, steps, reps, out_path, dma_orders=("producer",), fences=("none",),
+            forensic=False):
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -54,7 +60,12 @@ def _worker(rank, world, port, modes, priorities, steps, reps, out_path):
     want_mean = oracle.c_reduce(oracle.MODE_W32_DIV64, oracle.fill_uniform(n, p, 3), w_h, denom)
     results = []
 
-    def run_plans(mode, prio, rep):
+    L = na.lib()
+
+    def fence(kind):
+        na.check(L.fa_cache_fence(kind, torch.cuda.current_stream(cuda).cuda_stream), "fa_cache_fence")
+
+    def run_plans(mode, prio, rep, order, fen):
         for pi, plan in enumerate(plans):
             for op in ("mean", "adagrad"):  # the test's order (tests/multirank_worker.py)
                 stack = torch.empty((n, plan.local_stride), dtype=torch.float32, device=cuda)
@@ -69,14 +80,38 @@ def _worker(rank, world, port, modes, priorities, steps, reps, out_path):
                     epi = dict(op=na.OP_BY_NAME["adagrad"], prev=prev[0],
                                v=torch.zeros(plan.local_stride, dtype=torch.float64, device=cuda))
                     local_out = prev[0]
-                red = ShardedReducer(plan, hip_reduce_fn(stack, w, na.MODE_W32_DIV64, denom, **epi), cuda,
-                                     local_out=local_out, gather=True, push="dma" if mode == "dma" else True)
+                fn = hip_reduce_fn(stack, w, na.MODE_W32_DIV64, denom, **epi)
+                if fen in ("release", "both"):  # L2 written back after every stripe's reduce
+                    def fn(lo, sc, out, _f=fn):
+                        _f(lo, sc, out)
+                        fence(na.FENCE_RELEASE)
+                red = ShardedReducer(plan, fn, cuda, local_out=local_out, gather=True,
+                                     push="dma" if mode == "dma" else True)
                 prev_h = oracle.fill_uniform(1, p, 4)[0]
                 v_h = np.zeros(p)
                 last = prev_h.astype(np.float32) if op != "mean" else want_mean.astype(np.float32)
                 bad_steps = []
+                if forensic:  # global column -> (owner rank, owner's local column) of the stripes
+                    own_r = np.full(p, -1, dtype=np.int64)
+                    own_l = np.zeros(p, dtype=np.int64)
+                    for c in range(plan.stripes):
+                        for r in range(world):
+                            g0 = plan.global_begin(c, r)
+                            w_ = max(0, min(plan.widths[c], p - g0))
+                            own_r[g0 : g0 + w_] = r
+                            own_l[g0 : g0 + w_] = plan.local_begin(c) + np.arange(w_)
                 for step in range(steps):
-                    full = red.step().cpu().numpy()
+                    if forensic:  # what each sender's source and this rank's bucket held before
+                        src_snap = red.local_out.clone()
+                        bkt_snap = red.full[:p].clone()
+                    full = red.step()
+                    if fen in ("acquire", "both"):  # L2 invalidated before the bucket is read
+                        fence(na.FENCE_ACQUIRE)
+                    full = full.cpu().numpy()
+                    if forensic:
+                        srcs = [None] * world
+                        dist.all_gather_object(srcs, src_snap.cpu().numpy())
+                        bkt_before = bkt_snap.cpu().numpy()
                     if op == "mean":
                         want = want_mean.astype(np.float32)
                     else:
@@ -88,11 +123,27 @@ def _worker(rank, world, port, modes, priorities, steps, reps, out_path):
                         owners = sorted({next((r for r in range(world) for c in range(plan.stripes)
                                                if plan.global_begin(c, r) <= b < plan.global_begin(c, r)
                                                + plan.widths[c]), -1) for b in bad[:: max(1, len(bad) // 64)]})
-                        bad_steps.append({"step": step, "bad": int(len(bad)), "stale_prev_step": stale,
-                                          "owners": owners, "first": int(bad[0]), "last": int(bad[-1])})
+                        rec = {"step": step, "bad": int(len(bad)), "stale_prev_step": stale,
+                               "owners": owners, "first": int(bad[0]), "last": int(bad[-1])}
+                        if forensic:
+                            u = lambda a: a.view(np.uint32)  # noqa: E731
+                            ob = bad[own_r[bad] >= 0]
+                            pre_src = np.array([srcs[own_r[b]][own_l[b]] for b in ob], dtype=np.float32)
+                            rec["pushed_cols"] = int(len(ob))
+                            # = the sender's source BEFORE this step's reduce: the leg read it early
+                            rec["eq_sender_src_before"] = int(np.sum(u(full[ob]) == u(pre_src)))
+                            # = this rank's bucket before the step: the leg had not landed
+                            rec["eq_bucket_before"] = int(np.sum(u(full[bad]) == u(bkt_before[bad])))
+                            time.sleep(0.05)
+                            torch.cuda.synchronize()
+                            again = red.full[:p].cpu().numpy()
+                            # right when read again 50 ms later: the leg landed after the read
+                            rec["right_when_reread"] = int(np.sum(u(again[bad]) == u(want[bad])))
+                        bad_steps.append(rec)
                     last = want
                 red.release()
-                results.append({"priority": prio, "mode": mode, "rep": rep, "plan": pi, "op": op,
+                results.append({"priority": prio, "mode": mode, "order": order, "fence": fen, "rep": rep, "plan": pi,
+                                "op": op,
                                 "widths": list(plan.widths), "steps": steps, "bad_steps": bad_steps})
                 del stack, red
 
@@ -116,29 +167,54 @@ def _worker(rank, world, port, modes, priorities, steps, reps, out_path):
         return ok
 
     try:
+        product = (fd.side_stream, fd.peer_stream)
         for prio in priorities:
-            if prio != "product":  # "product": the streams as flearn_amd.dist creates them
-                fd.side_stream = (lambda dev: torch.cuda.Stream(dev, priority=-1)) if prio == "high" else (
-                    lambda dev: torch.cuda.Stream(dev, priority=0))
+            if prio == "product":  # the streams as flearn_amd.dist creates them
+                fd.side_stream, fd.peer_stream = product
+            else:  # "high": pusher and legs; "hipusher" / "hipeers": only that one at high priority
+                hi, lo = (lambda dev: torch.cuda.Stream(dev, priority=-1)), (lambda dev: torch.cuda.Stream(dev, priority=0))
+                fd.side_stream = hi if prio in ("high", "hipusher") else lo
+                fd.peer_stream = hi if prio in ("high", "hipeers") else lo
             for rep in range(reps):
                 for mode in modes:
-                    run_plans(mode, prio, rep)
-                    if not explicit_registration(mode):
-                        results.append({"priority": prio, "mode": mode, "rep": rep, "plan": "explicit", "op": "-",
-                                        "widths": [], "steps": 1, "bad_steps": [{"step": 0, "bad": -1}]})
+                    for order in (dma_orders if mode == "dma" else ("-",)):
+                        fd._DMA_ORDER = order if mode == "dma" else "producer"
+                        for fen in fences:
+                            run_plans(mode, prio, rep, order, fen)
+                            if rank == 0:
+                                print(f"{prio} rep {rep} {mode} {order} {fen}: done", file=sys.stderr, flush=True)
+                        if not explicit_registration(mode):
+                            results.append({"priority": prio, "mode": mode, "order": order, "rep": rep,
+                                            "plan": "explicit", "op": "-", "widths": [], "steps": 1,
+                                            "bad_steps": [{"step": 0, "bad": -1}]})
                 dist.barrier()
             fd.shutdown_push()
+        fd.side_stream, fd.peer_stream = product
+        fd._DMA_ORDER = "producer"
         gathered = [None] * world
         dist.all_gather_object(gathered, results)
         if rank == 0:
             summary = {}
             for r, res in enumerate(gathered):
                 for x in res:
-                    key = f"{x['priority']}/{x['mode']}/{x['op']}"
-                    s = summary.setdefault(key, {"runs": 0, "steps": 0, "bad_steps": 0, "examples": []})
+                    fen = x.get("fence", "none")
+                    key = f"{x['priority']}/{x['mode']}/{x.get('order', '-')}/" + (f"{fen}/" if fen != "none" else "") + x["op"]
+                    s = summary.setdefault(key, {"runs": 0, "steps": 0, "bad_steps": 0, "bad_by_step": {},
+                                                 "bad_by_plan": {}, "bad_elems": 0, "stale_prev_step": 0,
+                                                 "examples": []})
+                    if x["bad_steps"]:
+                        s["bad_by_plan"][str(x["plan"])] = s["bad_by_plan"].get(str(x["plan"]), 0) + len(x["bad_steps"])
+                    for b in x["bad_steps"]:
+                        for f in ("pushed_cols", "eq_sender_src_before", "eq_bucket_before", "right_when_reread"):
+                            if f in b:
+                                s[f] = s.get(f, 0) + b[f]
                     s["runs"] += 1
                     s["steps"] += x["steps"]
                     s["bad_steps"] += len(x["bad_steps"])
+                    for b in x["bad_steps"]:
+                        s["bad_by_step"][str(b["step"])] = s["bad_by_step"].get(str(b["step"]), 0) + 1
+                        s["bad_elems"] += max(b["bad"], 0)
+                        s["stale_prev_step"] += b.get("stale_prev_step", 0)
                     if x["bad_steps"] and len(s["examples"]) < 6:
                         s["examples"].append({"rank": r, "plan": x["plan"], "widths": x["widths"], **x["bad_steps"][0]})
             Path(out_path).write_text(json.dumps({"world": world, "summary": summary}, indent=1))
@@ -155,6 +231,14 @@ def main():
     ap.add_argument("--modes", default="kernel,dma")
     ap.add_argument("--reps", type=int, default=3, help="times the test's whole sequence runs per priority")
     ap.add_argument("--priorities", default="normal,high")
+    ap.add_argument("--dma-orders", default="producer",
+                    help="the copy-engine legs' start event: producer (the product) and/or chain (round 5)")
+    ap.add_argument("--fences", default="none",
+                    help="none / release (L2 written back after each stripe's reduce) / acquire (L2 invalidated "
+                         "before the bucket is read) / both: which cache fence removes wrong buckets")
+    ap.add_argument("--forensic", action="store_true",
+                    help="classify wrong values: the sender's source before the step (a leg read early), this "
+                         "rank's bucket before the step (a leg not landed), right when re-read 50 ms later")
     ap.add_argument("--out", default="gpurun_out/push_order.json")
     a = ap.parse_args()
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -162,8 +246,9 @@ def main():
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
     Path(a.out).parent.mkdir(parents=True, exist_ok=True)
-    mp.spawn(_worker, args=(a.world, port, a.modes.split(","), a.priorities.split(","), a.steps, a.reps, a.out),
-             nprocs=a.world, join=True)
+    mp.spawn(_worker, args=(a.world, port, a.modes.split(","), a.priorities.split(","), a.steps, a.reps, a.out,
+                            tuple(a.dma_orders.split(",")), tuple(a.fences.split(",")), a.forensic), nprocs=a.world,
+             join=True)
     print(Path(a.out).read_text())
 
 

@@ -49,6 +49,8 @@ def test_abi_version_and_constants(L):
         na.SRC_F64, na.SRC_I64, na.SRC_F32)
     for op, v in na.OP_BY_NAME.items():
         assert header_define(f"FA_OP_{op.upper()}") == v
+    assert (header_define("FA_FENCE_RELEASE"), header_define("FA_FENCE_ACQUIRE")) == (na.FENCE_RELEASE,
+                                                                                      na.FENCE_ACQUIRE)
 
 
 def test_epilogue_struct_layout_matches_c(tmp_path):
@@ -306,3 +308,8 @@ def test_reduce_window_count(L):
         assert L.fa_reduce_windows(adagrad, 86_567_656) == 1
     finally:
         L.fa_set_reduce_grid(prev)
+
+
+def test_cache_fence_rejects_an_unknown_kind(L):
+    assert L.fa_cache_fence(7, None) == header_define("FA_ERR_ARG")
+    assert b"fence" in L.fa_last_error()

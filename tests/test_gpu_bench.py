@@ -59,6 +59,8 @@ def test_bench_two_ranks_rehearsal(config, cuda):
     pair = pc["pair_us_by_grid"]
     assert set(pair) == set(pc["gather_us_by_grid"]) and pair[str(pc["grid"])] <= 1.03 * min(pair.values()) + 1e-6
     assert {t["gather"] for t in mg["plan_trials"]} == {"rccl", "push", "push_dma"}
+    rb = mg["push_receive_buckets"]  # parked receive buckets stay within the cap
+    assert rb["parked_bytes"] <= rb["park_cap_bytes"] and rb["pool_bytes"] > 0
     used = {"rccl": cal, "push": pc, "push_dma": pd}[mg["gather"]]
     assert mg["model"]["c_r"] == used["c_r"] and mg["model"]["c_g"] == used["c_g"]
     # the serial plan (one stripe, no tail) is among the measured trials
@@ -107,6 +109,11 @@ def test_bench_push_gather_is_verified(cuda):
         d = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][0])
         assert d["multi_gpu"]["gather"] == g and "push all-gather" in d["config"]["parallelism"]
         assert d["verify"]["verified"] is True and d["verify"]["ranks_checked"] == 2
+        # every one of 20 more steps checked end to end (each sender's slice checksums vs each
+        # receiver's bucket), not only the last one
+        a = d["multi_gpu"]["push_audit"]
+        assert a["verified"] is True and a["audited_steps"] == 20 and a["bad_steps_by_rank"] == [0, 0]
+        assert d["multi_gpu"]["phases"]["push"]["audit_verified"] is True
 
 
 @pytest.mark.timeout(300)
@@ -122,6 +129,26 @@ def test_bench_keeps_rccl_when_a_push_fails_its_check(cuda):
     assert mg["gather"] == "rccl" and mg["push_failed_self_check"]["gather"] == "push"
     assert mg["push_failed_self_check"]["mismatched_windows"] > 0
     assert mg["phases"]["push"]["status"] == "failed_self_check"
+    assert d["verify"]["verified"] is True and "RCCL all-gather" in d["config"]["parallelism"]
+
+
+@pytest.mark.timeout(300)
+def test_bench_push_audit_catches_one_bad_middle_step(cuda):
+    """FLEARN_BENCH_INJECT=push_skip_mid: rank 1 skips one push in ONE audited step (neither a
+    timed step nor the step verify_job bit-checks, which still passes): the step audit catches
+    the stale slice on every receiver, the line keeps the RCCL job (bench.push_audit)."""
+    p = _rehearse("c3", ("--no-weak", "--no-loopback", "--stripes", "2", "--gather", "push"), inject="push_skip_mid")
+    assert p.returncode == 0, p.stderr[-4000:]
+    assert "INJECTED: skipping one push" in p.stderr
+    assert "failed its step audit: keeping the RCCL line" in p.stderr
+    d = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][0])
+    mg = d["multi_gpu"]
+    assert mg["gather"] == "rccl" and mg["phases"]["push"]["status"] == "failed_self_check"
+    f = mg["push_failed_self_check"]
+    assert f["gather"] == "push" and f["mismatched_windows"] == 0  # the last step's windows pass
+    a = f["audit"]
+    assert a["verified"] is False and a["bad_steps_by_rank"] == [1, 1]
+    assert all(x["step"] == 7 for x in a["first_bad"]) and a["first_bad"][0]["slices"] == [{"sender": 1, "stripe": 0}]
     assert d["verify"]["verified"] is True and "RCCL all-gather" in d["config"]["parallelism"]
 
 

@@ -93,12 +93,13 @@ def test_push_setup_lifecycle(world, cuda):
 
 @pytest.mark.timeout(300)
 def test_push_order_under_the_products_streams(cuda, tmp_path):
-    """tests/push_order_probe.py with the product's streams (the kernel push on a high-priority
-    stream, the copy-engine push on normal ones): eight processes replay the push test's sequence
-    (mean and in-place Adagrad over four stripe plans, then an explicit registration) twice in
-    both push forms, every step's bucket bit-compared with the C oracle — 0 wrong rank-steps.
-    With the copy-engine push's streams at high priority this found 32 of 576 (DESIGN.md
-    section 6, "The pipeline's streams and the hardware queues")."""
+    """tests/push_order_probe.py: eight processes replay the push test's sequence (mean and in-place
+    Adagrad over four stripe plans, then an explicit registration) twice in both push forms, every
+    step's bucket bit-compared with the C oracle — 0 wrong rank-steps — with the product's streams
+    AND with every push stream (the pusher's, each copy-engine leg's) forced onto high priority, so
+    that none of them shares the compute stream's hardware queue.  Round 5's copy-engine push
+    failed that second configuration (32 of 576 in-place Adagrad rank-steps): its legs' start
+    event was recorded on the pusher's stream, not on the reduce's."""
     import json
     import subprocess
     import sys
@@ -107,10 +108,12 @@ def test_push_order_under_the_products_streams(cuda, tmp_path):
     out = tmp_path / "order.json"
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", HSA_ENABLE_IPC_MODE_LEGACY="0")
     p = subprocess.run([sys.executable, str(Path(__file__).with_name("push_order_probe.py")), "--world", "8",
-                        "--steps", "3", "--reps", "2", "--priorities", "product", "--out", str(out)],
+                        "--steps", "3", "--reps", "2", "--priorities", "product,high", "--out", str(out)],
                        env=env, capture_output=True, text=True, timeout=280)
     assert p.returncode == 0, p.stderr[-3000:]
     summary = json.loads(out.read_text())["summary"]
-    assert set(summary) == {f"product/{m}/{o}" for m in ("kernel", "dma") for o in ("mean", "adagrad")}
+    assert set(summary) == {f"{pr}/{m}/{o}" for pr in ("product", "high")
+                            for m, o in (("kernel", "-/mean"), ("kernel", "-/adagrad"), ("dma", "producer/mean"),
+                                         ("dma", "producer/adagrad"))}
     for key, s in summary.items():
         assert s["steps"] == 8 * 4 * 2 * 3 and s["bad_steps"] == 0, (key, s["examples"])

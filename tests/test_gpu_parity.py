@@ -97,6 +97,57 @@ def test_server_side_fused_optimizer_matches_reference(name, cuda):
         assert_dict_bitwise(v, g.output(f"v{r}"), f"{name} v{r}")
 
 
+@pytest.mark.parametrize("source", ["returned", "state_dict"])
+@pytest.mark.parametrize("name", ROUND_CASES)
+def test_server_optimizer_state_restores_on_a_fresh_strategy(name, source, cuda):
+    """A server restart between rounds: round 0 on one strategy, its state saved (the w_glob the
+    server returned + v_t(), or ServerOptimizer.state_dict()), then a FRESH AVGM / OPT(server_side)
+    restores it (load_state) and runs rounds 1-2 — bit-identical to the reference's 3 rounds
+    (avgm.py:28-35, opt.py:45-63 keep v_t across rounds; without the restore the momentum or
+    Adagrad state would silently restart from zero)."""
+    g = Golden(name)
+    op = g.meta["op"]
+
+    def fresh():
+        return AVGM(server_side=True) if op == "avgm" else OPT(server_side=True, method=op)
+
+    s = fresh()
+    s.server_opt.init_global({k[6:]: v for k, v in g.arrays.items() if k.startswith("prev0:")})
+    clients, weights = _round_inputs(g, 0)
+    got = s.server(upload(clients, weights), 0)["w_glob"]
+    assert_dict_bitwise(got, g.output("w0"), f"{name} w0")
+    if source == "returned":
+        saved = {"w_glob": {k: np.array(v, copy=True) for k, v in got.items()}, "v_t": s.server_opt.v_t()}
+    else:
+        saved = s.server_opt.state_dict()
+    del s
+    s = fresh()
+    s.server_opt.load_state(saved)
+    for r in range(1, g.meta["rounds"]):
+        clients, weights = _round_inputs(g, r)
+        got = s.server(upload(clients, weights), r)["w_glob"]
+        assert_dict_bitwise(got, g.output(f"w{r}"), f"{name} w{r} after restore")
+        assert_dict_bitwise(s.server_opt.v_t(), g.output(f"v{r}"), f"{name} v{r} after restore")
+
+
+def test_server_optimizer_restore_refuses_a_foreign_v_t(cuda):
+    """v_t restored for another model: a missing key raises KeyError, a wrong shape ValueError —
+    at the next round, before anything is launched."""
+    name = next(n for n in ROUND_CASES if Golden(n).meta["op"] == "adagrad")
+    g = Golden(name)
+    prev0 = {k[6:]: v for k, v in g.arrays.items() if k.startswith("prev0:")}
+    clients, weights = _round_inputs(g, 0)
+    v0 = {k: np.zeros(np.shape(v)) for k, v in prev0.items()}
+    missing = dict(v0)
+    missing.pop(next(iter(missing)))
+    wrong = {k: (np.zeros(3) if i == 0 else v) for i, (k, v) in enumerate(v0.items())}
+    for bad, exc in ((missing, SystemExit), (wrong, SystemExit)):
+        s = OPT(server_side=True, method="adagrad")
+        s.server_opt.load_state({"w_glob": prev0, "v_t": bad})
+        with pytest.raises(exc):  # a client/config data error: server_exception, as the reference's
+            s.server(upload(clients, weights), 0)
+
+
 def test_fused_round_refused_keeps_optimizer_state(cuda, monkeypatch):
     """A fused step whose launch is refused (here: reduce_stack raising before it queues anything)
     leaves the double-buffered state on the pair it had, so the rounds after it still match the
@@ -776,6 +827,29 @@ def test_dyn_strategy_matches_reference(name, shards, cuda):
         dev = s._dyn.dev_keys
         assert_dict_bitwise({k: v for k, v in s._dyn.theta_host().items() if k in dev},
                             {k: np.asarray(v) for k, v in g.output(f"theta{r}").items() if k in dev}, f"{name} theta{r}")
+
+
+@pytest.mark.parametrize("name", DYN_CASES)
+def test_dyn_state_restores_on_a_fresh_strategy(name, cuda):
+    """A server restart between FedDyn rounds: h and theta saved after round 0 (copies of
+    `strategy.h` and `strategy.theta`), a fresh Dyn(h) with `theta` assigned runs rounds 1-2 —
+    w_glob, h and theta bit-identical to the reference's (dyn.py:14-36)."""
+    from flearn_amd import Dyn
+
+    g = Golden(name)
+    s = Dyn(_dyn_h0(g))
+    clients, weights = _dyn_inputs(g, 0)
+    s.server(upload(clients, weights), 0)
+    h_saved = {k: np.array(v, copy=True) for k, v in s.h.items()}
+    theta_saved = {k: np.array(v, copy=True) for k, v in s.theta.items()}
+    del s
+    s = Dyn(h_saved)
+    s.theta = theta_saved
+    for r in range(1, g.meta["rounds"]):
+        clients, weights = _dyn_inputs(g, r)
+        got = s.server(upload(clients, weights), r)["w_glob"]
+        assert_dict_bitwise(got, g.output(f"w{r}"), f"{name} w{r} after restore")
+        assert_dict_bitwise(s.h, g.output(f"h{r}"), f"{name} h{r} after restore")
 
 
 @pytest.mark.parametrize("name", DYN_CASES)

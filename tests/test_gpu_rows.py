@@ -232,3 +232,112 @@ def test_back_to_back_device_output_rounds_with_host_uploads(cuda):
     for r, (o, w) in enumerate(zip(outs, wants)):
         assert bitwise_equal(o.cpu().numpy(), w), r
     assert layout
+
+
+# ---------------------------------------------------------------------------------------------
+# slab uploads (flearn_amd.device_state_dicts): the clients' fp32 tensors in ONE allocation laid
+# out as the bucket — read in place by the stack kernel (Packer._slab_stack)
+# ---------------------------------------------------------------------------------------------
+
+
+def _slab_clients(clients, cuda):
+    """The fixture's clients copied into device_state_dicts (values exact, dtypes kept)."""
+    from flearn_amd import device_state_dicts
+
+    cl = [_to_cuda(c, cuda) for c in clients]
+    sd = device_state_dicts(cl[0], len(cl), device=cuda)
+    for d, c in zip(sd, cl):
+        for k, v in c.items():
+            d[k].copy_(v)
+    return sd
+
+
+@pytest.mark.parametrize("name", ["avg_w1_n100", "avg_pyint_n100", "avg_np32_n10", "avg_special_n5",
+                                  "avg_negzero_n1", "avg_bnmodel_pyfloat_n4", "trace_lenet5_round0", "avg_lenet5_n10"])
+def test_slab_uploads_run_the_stack_kernel(name, cuda):
+    g = Golden(name)
+    sd = _slab_clients(g.clients(), cuda)
+    s = AVG()
+    got = s.server(_upload(list(sd), g.weights()), 0)["w_glob"]
+    if "f32" in s.engine.last_plan.groups:
+        assert s.engine.packer.last_row_tables.get("f32") == "slab", s.engine.packer.last_row_tables
+    for k, w in g.output().items():
+        assert bitwise_equal(_host(got[k]), np.asarray(w)), (name, k)
+
+
+@pytest.mark.parametrize("name", ["avgm_pyfloat_rounds3", "adagrad_np32_rounds3", "adam_pyfloat_rounds3"])
+def test_fused_optimizer_slab_uploads(name, cuda):
+    from golden_io import decode_weight, regenerate
+
+    g = Golden(name)
+    op = g.meta["op"]
+    s = AVGM(server_side=True) if op == "avgm" else OPT(server_side=True, method=op)
+    s.server_opt.init_global({k[6:]: v for k, v in g.arrays.items() if k.startswith("prev0:")})
+    layout = [(k, tuple(sh)) for k, sh in g.meta["gen"]["layout"]]
+    for r in range(g.meta["rounds"]):
+        sd = _slab_clients(regenerate(layout, 6, g.meta["gen"]["seeds"][r]), cuda)
+        weights = [decode_weight(e) for e in g.meta["round_weights"][r]]
+        got = s.server(_upload(list(sd), weights), r)["w_glob"]
+        assert s.engine.packer.last_row_tables.get("f32") == "slab"
+        for k, w in g.output(f"w{r}").items():
+            assert bitwise_equal(_host(got[k]), np.asarray(w)), (name, r, k)
+
+
+def test_slab_rows_subset_and_order(cuda):
+    """Clients 1..n-1 of a slab (a row offset) still run as a stack; reversed order (negative
+    pitch) or a foreign tensor among them falls back to the pointer table — same results."""
+    from flearn_amd import device_state_dicts
+
+    g = Golden("avg_w1_n10")
+    sd = _slab_clients(g.clients(), cuda)
+    want = None
+    for sel, path in ((list(sd)[1:], "slab"), (list(sd)[::-1], "rows"), (list(sd), "slab")):
+        s = AVG(output="float32")
+        got = s.server(_upload(sel, [1.0] * len(sel)), 0)["w_glob"]
+        assert s.engine.packer.last_row_tables.get("f32") == path, (path, s.engine.packer.last_row_tables)
+        ref = AVG(output="float32").server(_upload([{k: v.cpu().numpy() for k, v in c.items()} for c in sel],
+                                                   [1.0] * len(sel)), 0)["w_glob"]
+        for k in ref:
+            assert bitwise_equal(_host(got[k]), np.asarray(ref[k])), (path, k)
+        want = got
+    mixed = list(sd)
+    k0 = next(iter(mixed[3]))
+    mixed[3] = dict(mixed[3])
+    mixed[3][k0] = mixed[3][k0].clone()  # one tensor outside the slab
+    s = AVG(output="float32")
+    got = s.server(_upload(mixed, [1.0] * len(mixed)), 0)["w_glob"]
+    assert s.engine.packer.last_row_tables.get("f32") == "rows"
+    for k in want:
+        assert bitwise_equal(_host(got[k]), _host(want[k])), k
+    assert isinstance(device_state_dicts(sd[0], 2, device=cuda).slab, torch.Tensor)
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("layout_name,n,op", [("resnet50", 100, "mean"), ("resnet50", 100, "avgm")])
+def test_slab_uploads_baseline_size(layout_name, n, op, cuda):
+    """NS / C3-size slab uploads (100 x ResNet-50): the engine's reduce reads the slab as its
+    stack — bit-equal to the stack kernel over a packed copy of the same values."""
+    from flearn_amd import device_state_dicts
+
+    layout = layouts.get(layout_name)
+    template = {k: torch.zeros(shape, dtype=torch.float32 if t == "f32" else torch.int64) for k, shape, t in layout}
+    sd = device_state_dicts(template, n, device=cuda)
+    agg.fill_uniform(sd.slab, seed=77)
+    stride = sd.slab.shape[1]
+    x = sd.slab.clone()
+    w = torch.ones(n, dtype=torch.float32, device=cuda)
+    want = torch.empty(stride, dtype=torch.float32, device=cuda)
+    kw, s = {}, AVG(output="float32")
+    if op != "mean":
+        prev = torch.empty((1, stride), dtype=torch.float32, device=cuda)
+        agg.fill_uniform(prev, seed=5)
+        kw = dict(op=na.OP_BY_NAME[op], prev=prev[0].clone(), v=torch.zeros(stride, dtype=torch.float64, device=cuda))
+        s = AVGM(server_side=True, output="float32")
+        ph = prev[0].cpu().numpy()
+        s.server_opt.init_global({k: ph[o : o + m].reshape(shp) for k, (o, m, shp) in sd.offsets.items()})
+    agg.reduce_stack(x, w, na.MODE_W32_DIV64, float(n), out32=want, **kw)
+    got = s.server(_upload(list(sd), [1.0] * n), 0)["w_glob"]
+    assert s.engine.packer.last_row_tables.get("f32") == "slab"
+    want_h = want.cpu().numpy()
+    for k, (o, m, shp) in sd.offsets.items():
+        assert bitwise_equal(np.asarray(got[k]).reshape(-1), want_h[o : o + m]), k

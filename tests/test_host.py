@@ -389,3 +389,70 @@ def test_device_output_is_one_copy_per_shard_and_views(monkeypatch):
         assert base[kind] in (None, ptr)  # all keys of a kind view one fresh buffer
         base[kind] = ptr
     assert base[KIND_F32] != full32.untyped_storage().data_ptr()
+
+
+def test_server_optimizer_restore_binds_v_t_to_the_bucket():
+    """ServerOptimizer.load_state / set_v_t (host logic, CPU shards): the restored previous global
+    model (cast to fp32) and v_t land at every key's columns of the f32 bucket, split over shards;
+    state_dict() gives them back keyed like w_glob; set_v_t before init_global is refused."""
+    from flearn_amd.aggregator import ServerOptimizer
+    from flearn_amd.bucket import split_columns
+
+    rng = np.random.default_rng(5)
+    cl = [{"a": rng.random((3, 70), dtype=np.float32), "b": rng.random(5, dtype=np.float32)} for _ in range(2)]
+    plan = make_plan([1.0, 2.0], cl)
+    glob = {"a": rng.random((3, 70)), "b": rng.random(5)}  # f64, as w_glob comes back
+    v = {"a": rng.random((3, 70)), "b": rng.random(5)}
+    opt = ServerOptimizer("adagrad")
+    with pytest.raises(RuntimeError):
+        opt.set_v_t(v)
+    with pytest.raises(RuntimeError):
+        opt.state_dict(plan)  # nothing bound yet
+    opt.load_state({"w_glob": glob, "v_t": v})
+    shards = split_columns(plan.f32.stride, ["cpu", "cpu"])
+    assert opt.prepare(plan, shards)
+    got = opt.state_dict()
+    for k in glob:
+        assert got["w_glob"][k].dtype == np.float32 and np.array_equal(got["w_glob"][k], glob[k].astype(np.float32))
+        assert got["v_t"][k].dtype == np.float64 and np.array_equal(got["v_t"][k], v[k])
+    bad = ServerOptimizer("avgm")
+    bad.load_state({"w_glob": glob, "v_t": {"a": v["a"]}})
+    with pytest.raises(KeyError):
+        bad.prepare(plan, shards)
+    bad.load_state({"w_glob": glob, "v_t": {"a": v["a"], "b": np.zeros(4)}})
+    with pytest.raises(ValueError):
+        bad.prepare(plan, shards)
+
+
+def test_slab_stack_detection():
+    """Packer._slab_stack (host logic on CPU tensors): uploads carved from one allocation laid out
+    as the bucket become one [N, stride] view of it — rows from a subset keep their pitch and
+    offset; reversed order, a foreign tensor or another layout are refused (None)."""
+    from flearn_amd import device_state_dicts
+    from flearn_amd.bucket import Packer
+
+    rng = np.random.default_rng(3)
+    t = {"a": torch.from_numpy(rng.random((3, 70), dtype=np.float32)), "b": torch.from_numpy(rng.random(5, dtype=np.float32)),
+         "n": torch.tensor(4)}
+    sd = device_state_dicts(t, 5, device="cpu")
+    for i, d in enumerate(sd):
+        d["a"].add_(i)
+
+    def stack_of(clients):
+        plan = make_plan([1.0] * len(clients), clients)
+        g = plan.f32
+        segs = [s for s in g.segments if s.numel > 0]
+        ptrs = np.array([[c[s.key].data_ptr() for c in clients] for s in segs], dtype=np.int64)
+        return plan, g, Packer._slab_stack(plan, g, clients, (segs, ptrs, [], None))
+
+    plan, g, st = stack_of(list(sd))
+    assert st is not None and st.shape == (5, g.stride) and st.data_ptr() == sd.slab.data_ptr()
+    assert torch.equal(st, sd.slab[:, : g.stride])
+    plan, g, st = stack_of(list(sd)[2:])
+    assert st is not None and st.data_ptr() == sd.slab[2].data_ptr() and st.stride(0) == sd.slab.stride(0)
+    assert stack_of(list(sd)[::-1])[2] is None
+    mixed = [dict(c) for c in sd]
+    mixed[1]["b"] = mixed[1]["b"].clone()
+    assert stack_of(mixed)[2] is None
+    other = [{"a": c["a"].clone(), "b": c["b"].clone(), "n": c["n"]} for c in sd]  # separate allocations
+    assert stack_of(other)[2] is None

@@ -5,8 +5,10 @@ the collective protocol is real: buckets are mapped once and handed out again, t
 slot that fits is reused, a slot in use is never handed out twice, a larger request retires the
 free buckets (every peer unmaps, barrier, park) before it maps a new one, ranks whose pools
 disagree all raise, `shutdown_push` empties the pools with every import closed before any bucket
-is parked (exported memory is never freed: DESIGN.md section 6), the next pool re-exports a
-parked bucket, and a destroyed and re-created default group maps its buckets afresh."""
+is parked, the next pool re-exports a parked bucket, and a destroyed and re-created default group
+maps its buckets afresh.  `test_parked_buckets_stay_within_the_cap` runs the real DeviceBuffer and
+`_map_peers` over a shared-memory stand-in for HIP IPC: growing then shrinking requests keep the
+parked bytes within the cap, and every mapping is token-checked (a wrong one refused)."""
 import os
 import tempfile
 import types
@@ -68,15 +70,16 @@ def _install_stubs(fd, events):
 
     fd.DeviceBuffer = FakeBuf
     fd._map_peers = fake_map
+    fd._IPC = types.SimpleNamespace(close=L.fa_ipc_close, accepts=lambda d: torch.device(d).type == "cuda")
     fd._RecvPool._pools.clear()
     from flearn_amd import _native as na
 
-    na.lib = lambda: L  # shutdown_push binds the library for the unmaps
+    na.lib = lambda: L  # shutdown_push binds the library
     return L, FakeBuf
 
 
-def _cols(want):  # the pool's bucket size: 1/8 headroom, ALIGN-rounded
-    return (want + want // 8 + 64) // 64 * 64
+def _cols(want):  # the pool's request: ALIGN-rounded (DeviceBuffer.get applies the size class)
+    return -(-want // 64) * 64
 
 
 def _worker(rank, world, init):
@@ -154,3 +157,161 @@ def _worker(rank, world, init):
 def test_recv_pool_lifecycle():
     init = "file://" + os.path.join(tempfile.mkdtemp(prefix="fa_pool_"), "pg")
     mp.spawn(_worker, args=(2, init), nprocs=2, join=True)
+
+
+class _ShmIpc:
+    """HIP IPC's stand-in on CPU: a DeviceBuffer is a POSIX shared-memory segment, its handle the
+    segment's name, a peer's import an attachment of it; read16 copies through the mapping, as
+    the token check reads through a copy engine."""
+
+    def __init__(self, events, wrong_open=None):
+        from multiprocessing import shared_memory
+
+        self.sm, self.events, self.wrong_open = shared_memory, events, wrong_open
+        self.own = {}  # address -> SharedMemory (this rank's allocations)
+        self.attached = {}  # address -> SharedMemory (imports)
+
+    @staticmethod
+    def _addr(shm):
+        import ctypes
+
+        return ctypes.addressof(ctypes.c_char.from_buffer(shm.buf))
+
+    def alloc(self, nbytes):
+        shm = self.sm.SharedMemory(create=True, size=nbytes)
+        a = self._addr(shm)
+        self.own[a] = shm
+        return a
+
+    def release(self, ptr):
+        shm = self.own.pop(ptr)
+        try:
+            shm.close()
+        except BufferError:  # a tensor view still alive: the mapping goes with the process
+            pass
+        shm.unlink()
+        self.events.append(("freed", ptr))
+
+    def view(self, ptr, dtype):
+        return torch.frombuffer(self.own[ptr].buf, dtype=dtype)
+
+    def accepts(self, device):
+        return torch.device(device).type == "cpu"
+
+    def sync(self, device):
+        pass
+
+    def handle(self, ptr):
+        for a, shm in self.own.items():
+            if a <= ptr < a + shm.size:
+                return shm.name.encode().ljust(64, b"\0"), ptr - a
+        return None
+
+    def open(self, hb):
+        name = hb.rstrip(b"\0").decode()
+        if self.wrong_open is not None:  # an import that maps some other allocation
+            name, self.wrong_open = self.wrong_open, None
+        shm = self.sm.SharedMemory(name=name)
+        a = self._addr(shm)
+        self.attached[a] = shm
+        return a
+
+    def read16(self, probe, addr):
+        import ctypes
+
+        ctypes.memmove(probe.data_ptr(), addr, 16)
+        self.events.append(("token_read", addr))
+        return True
+
+    def close(self, base):
+        shm = self.attached.pop(base)
+        try:
+            shm.close()
+        except BufferError:
+            pass
+        self.events.append(("close", base))
+
+    def last_error(self):
+        return b""
+
+
+def _cap_worker(rank, world, init):
+    from flearn_amd import dist as fd
+
+    dist.init_process_group("gloo", init_method=init, rank=rank, world_size=world)
+    ev = []
+    ipc = _ShmIpc(ev)
+    fd._IPC = ipc
+    fd._RecvPool._pools.clear()
+    fd.DeviceBuffer._alloc = lambda self: ipc.alloc(self.nbytes)
+    fd.DeviceBuffer._release = lambda self, ptr: ipc.release(ptr)
+    fd.DeviceBuffer.tensor = lambda self, dtype=torch.float32: ipc.view(self.ptr, dtype)
+
+    def init_buf(self, nbytes, device):  # the real constructor minus the native library
+        self.L, self.na = None, None
+        self.nbytes, self.device = int(nbytes), torch.device(device)
+        self._exported = False
+        self._typestr = "<f4"
+        self.ptr = self._alloc()
+
+    fd.DeviceBuffer.__init__ = init_buf
+    try:
+        pg = types.SimpleNamespace(world=world, rank=rank, group=None, nccl=False, device=torch.device("cpu"))
+        pool = fd._RecvPool.get("cpu", None)
+        maps = 0
+        # growing by ~25% per request: each larger request retires the free bucket and maps a new
+        # one, so without the cap the parked bytes would reach ~4x the largest bucket
+        for cols in (100_000, 125_000, 160_000, 200_000, 250_000, 320_000, 400_000):
+            n0 = sum(1 for e in ev if e[0] == "token_read")
+            i, buf, dsts = pool.take(pg, cols)
+            maps += 1
+            # the new bucket's mapping read every peer's token through the mapping
+            assert sum(1 for e in ev if e[0] == "token_read") - n0 == world - 1
+            buf.fill_(float(rank + 1))
+            dist.barrier()
+            peer = (rank + 1) % world
+            probe = torch.empty(4, dtype=torch.float32)
+            ipc.read16(probe, dsts[peer])  # the mapping reaches the peer's bucket
+            assert probe.tolist() == [float(peer + 1)] * 4
+            dist.barrier()
+            pool.give(i)
+            assert fd.DeviceBuffer.parked_bytes("cpu") <= fd.DeviceBuffer.park_cap("cpu")
+        assert fd.DeviceBuffer.trimmed()["buckets"] > 0  # the cap did bind
+        assert any(e[0] == "freed" for e in ev)
+        # shrinking: smaller requests reuse the free bucket, no new mapping
+        n0 = sum(1 for e in ev if e[0] == "token_read")
+        for cols in (300_000, 20_000, 64):
+            i, buf, _ = pool.take(pg, cols)
+            pool.give(i)
+        assert sum(1 for e in ev if e[0] == "token_read") == n0
+        fd.shutdown_push()
+        assert fd.DeviceBuffer.parked_bytes("cpu") <= fd.DeviceBuffer.park_cap("cpu")
+        # a mapping of the wrong allocation is refused on every rank (the token check)
+        pool = fd._RecvPool.get("cpu", None)
+        if rank == 0:
+            victim = next(iter(ipc.own.values())).name  # rank 0's own segment, not the peer's
+            ipc.wrong_open = victim
+        with pytest.raises(RuntimeError, match="did not hold their tokens" if rank == 0 else "could not map"):
+            pool.take(pg, 450_000)
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+        for a in list(ipc.own):
+            ipc.release(a)
+
+
+def test_parked_buckets_stay_within_the_cap():
+    init = "file://" + os.path.join(tempfile.mkdtemp(prefix="fa_cap_"), "pg")
+    mp.spawn(_cap_worker, args=(2, init), nprocs=2, join=True)
+
+
+def test_size_classes():
+    from flearn_amd.dist import size_class
+
+    assert size_class(1) == 4096 and size_class(4096) == 4096
+    for n in (4097, 10_000, 123_457, 10**9 + 7):
+        c = size_class(n)
+        assert n <= c < n * 1.25 + 4096 and c % 256 == 0
+        assert size_class(c) == c  # a class is its own class
+    # requests a few percent apart share a class
+    assert size_class(1_000_000) == size_class(1_030_000)

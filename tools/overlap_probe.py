@@ -52,6 +52,9 @@ def main():
                     help="with --push-cus: the reduce's stream gets the other CUs (disjoint masks)")
     ap.add_argument("--push-cu-layout", default="spread", choices=["spread", "low"],
                     help="which CUs the copy stream gets: every (CUs/K)-th, or the lowest K")
+    ap.add_argument("--keep-streams", action="store_true",
+                    help="leave the CU-masked streams alive at exit (round 5's behaviour: a SIGSEGV in "
+                         "__cxa_finalize under rocprofv3, DESIGN.md section 7)")
     a = ap.parse_args()
     L = ctypes.CDLL(str(REPO / "tools" / "libprobe_copy.so"))
     L.probe_copy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_void_p]
@@ -81,6 +84,7 @@ def main():
     dst = torch.empty_like(src)
     sa, sb = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
     masks = None
+    created = []  # CU-masked streams this probe made: destroyed before exit
     if a.push_cus:
         ncu = torch.cuda.get_device_properties(0).multi_processor_count
         words = (ncu + 31) // 32
@@ -97,6 +101,7 @@ def main():
             assert L.probe_stream_cumask((ctypes.c_uint32 * words)(*m), words, ctypes.byref(h)) == 0
             got = (ctypes.c_uint32 * words)()
             assert L.probe_stream_cumask_get(h, words, got) == 0
+            created.append(h.value)
             return torch.cuda.ExternalStream(h.value, device=dev), [int(x) for x in got]
 
         sb, got_b = masked(mb)
@@ -265,7 +270,16 @@ def main():
     agg.set_reduce_grid(0)
     res["note"] = ("copy GB/s counts bytes copied (each read once and written once locally); a gather's local "
                    "HBM traffic at the same GB/s is about half of the copy's")
-    print(json.dumps(res))
+    print(json.dumps(res), flush=True)
+    if created and not a.keep_streams:
+        # a hipStream the runtime did not make for torch must be destroyed by its maker, before
+        # the HIP runtime's own static teardown (ExternalStream never destroys what it wraps)
+        torch.cuda.synchronize(dev)
+        sa = sb = None
+        L.probe_stream_destroy.argtypes = [ctypes.c_void_p]
+        for h in created:
+            assert L.probe_stream_destroy(h) == 0
+        print(f"destroyed {len(created)} CU-masked stream(s)", file=sys.stderr, flush=True)
 
 
 if __name__ == "__main__":
