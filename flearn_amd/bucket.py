@@ -378,7 +378,10 @@ class Packer:
         self._pool = None
         self.last_wire_rows = 0
         self.last_wire_staged = 0
-        self.last_row_tables = {}  # kind -> "rows" | "gather" | "copy" for device-resident uploads
+        self.last_row_tables = {}  # kind -> "slab" | "rows" | "gather" | "copy" for device-resident uploads
+        #: device uploads carved from one allocation laid out as the bucket run as a stack
+        #: (_slab_stack); False: always the pointer table (tools/rows_pmc.py measures that kernel)
+        self.use_slabs = True
         self.rank_cols = None  # (rank, world): pack only this rank's columns of the f32 bucket
         #: host uploads packed by native threads in growing row chunks (AsyncPack); False: the
         #: Python pool packs ~8 equal chunks (also the fallback for values off the plan)
@@ -468,7 +471,7 @@ class Packer:
                 pieces = plan.memo[pk] = self._pieces(g, shards)
             if plan.input_kind == "torch" and all(w_local_lst[0][s.key].device.type == "cuda" for s in g.segments):
                 rp = self._row_ptrs(plan, g, w_local_lst, shards)
-                if rp is not None and kind == KIND_F32:
+                if rp is not None and kind == KIND_F32 and self.use_slabs:
                     slab = self._slab_stack(plan, g, w_local_lst, rp)
                     if slab is not None:  # one allocation laid out as the bucket: the stack itself
                         out[kind] = [(shards[0], slab)]

@@ -795,7 +795,9 @@ int fa_copy(void* dst, const void* src, int64_t nbytes, void* stream) {
 // fa_push's default grid.  The kernel is paced (each wave drains its stores per round): a block
 // keeps 4 waves x 4 quads x 1 KiB = 16 KiB in flight per destination link, so 16 blocks keep
 // ~256 KiB per link — about an xGMI link's bandwidth-delay product (64-153 GB/s x 1-2 us), more
-// only queues in the fabric and slows a reduce beside the push
+// only queues in the fabric and slows a reduce beside the push.  Provisional:
+// no multi-GPU run has measured it against seven xGMI links; bench.py's calibration picks the grid
+// on the node and records every grid's push-beside-reduce pair, 16 included
 constexpr int64_t kPushGrid = 16;
 
 int fa_ipc_handle(const void* ptr, void* handle, int64_t* offset) {
@@ -905,6 +907,18 @@ static int stream_after(hipStream_t to, hipStream_t from) {
   return FA_OK;
 }
 
+// Gate kernels around every copy-engine leg (fa_push_dma): the leg's stream waits on the
+// producer's event with a one-wave kernel, copies, and runs another one-wave kernel that the
+// join's event follows — so both cross-queue edges of a leg are kernel-to-kernel waits and the
+// copy engine depends only on its own stream's neighbours.  Without them, with the legs' streams
+// on queues of their own and eight processes sharing a GPU, copy-engine legs that waited on the
+// producer's event directly copied their source before the reduce writing it had finished
+// (tests/push_order_probe.py --forensic: every wrong value was the sender's source as it was
+// before the step).
+static std::atomic<int> g_dma_gates{1};
+
+int fa_set_push_dma_gates(int32_t on) { return g_dma_gates.exchange(on ? 1 : 0); }
+
 int fa_push_dma(const void* src, int64_t nbytes, void* const* dsts, int32_t n_dsts, void* const* streams,
                 void* stream) {
   if (nbytes < 0 || n_dsts < 0 || n_dsts > 8) return fail(FA_ERR_ARG, "bad push size or destination count");
@@ -912,13 +926,22 @@ int fa_push_dma(const void* src, int64_t nbytes, void* const* dsts, int32_t n_ds
   if (!src || !dsts || !streams) return fail(FA_ERR_ARG, "null push pointer");
   for (int i = 0; i < n_dsts; ++i)
     if (!dsts[i] || !streams[i]) return fail(FA_ERR_ARG, "null push destination or stream");
+  const bool gates = g_dma_gates.load(std::memory_order_relaxed) != 0;
   hipEvent_t ev;
   hipError_t e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
   if (e == hipSuccess) e = hipEventRecord(ev, static_cast<hipStream_t>(stream));
   for (int i = 0; i < n_dsts && e == hipSuccess; ++i) {
     hipStream_t s = static_cast<hipStream_t>(streams[i]);
     e = hipStreamWaitEvent(s, ev, 0);
+    if (e == hipSuccess && gates) {
+      hipLaunchKernelGGL(gate_kernel, dim3(1), dim3(64), 0, s);
+      e = hipGetLastError();
+    }
     if (e == hipSuccess) e = hipMemcpyAsync(dsts[i], src, (size_t)nbytes, kCopyEngine, s);
+    if (e == hipSuccess && gates) {
+      hipLaunchKernelGGL(gate_kernel, dim3(1), dim3(64), 0, s);
+      e = hipGetLastError();
+    }
   }
   hipEventDestroy(ev);
   if (e != hipSuccess) return fail(FA_ERR_LAUNCH, hipGetErrorString(e));

@@ -275,7 +275,9 @@ int fa_mem_range(const void* ptr, void** base, int64_t* size);
  * stores before its next loads, so a block keeps ~16 KiB in flight per destination and the grid
  * sets the total; a small grid fills a link, and stores queued beyond a link's bandwidth-delay
  * product slow a reduce running beside the push (the data fabric backs up: DESIGN.md section 6).
- * Default (grid 0) 16 blocks; bench.py calibrates it on the node.  ABI 10 adds `grid`. */
+ * Default (grid 0) 16 blocks — PROVISIONAL: sized from one GPU's PCIe stand-in and a
+ * bandwidth-delay estimate, never measured against seven xGMI links; bench.py calibrates the grid
+ * on the node (push_calibration.pair_us_by_grid, 16 among the grids it times).  ABI 10 adds `grid`. */
 int fa_push(const void* src, int64_t nbytes, void* const* dsts, int32_t n_dsts, int32_t grid, void* stream);
 
 /* hipMemcpyAsync(dst, src, nbytes, hipMemcpyDeviceToDeviceNoCU) on `stream`: a copy-engine
@@ -284,12 +286,19 @@ int fa_push(const void* src, int64_t nbytes, void* const* dsts, int32_t n_dsts, 
  * these copies as blit kernels on the compute queues (rocprofv3).  ABI 11. */
 int fa_copy_dma(void* dst, const void* src, int64_t nbytes, void* stream);
 
-/* The copy-engine push leg of one stripe in one call: after the work queued so far on `stream`,
+/* The copy-engine push leg of one stripe in one call: after the work queued so far on `stream`
+ * (the stream that wrote src),
  * copy nbytes from src to dsts[i] on streams[i] (i < n_dsts <= 8; one copy engine per peer
  * stream).  What eight Python-level event records / waits / copies cost in host time per stripe
  * (~80 us) this does in a few; the stripe pipeline is host-bound otherwise.  ABI 12.           */
 int fa_push_dma(const void* src, int64_t nbytes, void* const* dsts, int32_t n_dsts, void* const* streams,
                 void* stream);
+
+/* fa_push_dma's gate kernels (default on): each leg's stream runs a one-wave kernel after its wait
+ * on `stream` and another after the copy, so that the copy engine's only dependencies are on its
+ * own stream.  on = 0 turns them off (tests/push_order_probe.py's A/B only).  Returns the previous
+ * setting.  ABI 14.                                                                             */
+int fa_set_push_dma_gates(int32_t on);
 
 /* `stream` waits for the work queued so far on streams[0..n) (n <= 16).  ABI 12.             */
 int fa_stream_join(void* stream, void* const* streams, int32_t n);

@@ -2,13 +2,16 @@
 their own hardware queue?  (rounds 5-6)
 
     python tests/push_order_probe.py --world 8 --steps 3 --reps 6 --priorities normal,high,product \
-        --dma-orders producer,chain
+        --dma-orders host,producer,chain [--forensic]
 
 (round 5: with the copy-engine push's pusher stream at high priority, 32 of 576 in-place Adagrad
-rank-steps were wrong.  Round 6: the legs waited on an event recorded on the pusher's stream after
-its wait on the reduce's stream — `--dma-orders chain` replays that; "producer", the product's
-order now, records the legs' event on the reduce's own stream.  "high" puts the pusher's stream
-AND every leg's stream at high priority: none of them shares the compute stream's hardware queue)
+rank-steps were wrong.  Round 6: with every push stream at high priority the copy-engine legs AND
+the pusher's own-copy kernel copied stripes before their reduce had finished, whatever the
+device-side order — `--dma-orders chain` (round 5: an event of the pusher's stream), `producer` (an
+event of the reduce's own stream), with gate kernels or L2 fences — while `host`, the product's
+order now, issues each stripe's legs only after the host has seen its reduce complete.  "high" puts
+the pusher's stream AND every leg's stream at high priority: none of them shares the compute
+stream's hardware queue; "hipusher" / "hipeers" only one side)
 
 `world` processes share cuda:0 over gloo (like tests/test_gpu_multirank.py); each runs
 ShardedReducer steps with the fused Adagrad epilogue in place (the reduce reads `prev` and writes
@@ -18,7 +21,7 @@ queue of their own: flearn_amd.streams.side_stream), and compares every step's b
 oracle.  For a mismatch it records which ranks' slices were wrong and whether the wrong values are
 the PREVIOUS step's model (a copy that read its source before the reduce had written it) or
 something else.  Prints one JSON object.  Test infrastructure (it checks against the C oracle, so it
-lives under tests/), run by hand or by tools/gpu_r05a*.sh, not by pytest.
+lives under tests/), run by tools/gpu_run.sh push_order and by tests/test_gpu_multirank.py.
 """
 from __future__ import annotations
 
@@ -34,8 +37,8 @@ REPO = Path(__file__).resolve().parent.parent
 sys.path.insert(0, str(REPO))
 
 
-def _worker(rank, world, port, modes, priorities, steps, reps, out_path, dma_orders=("producer",), fences=("none",),
-            forensic=False):
+def _worker(rank, world, port, modes, priorities, steps, reps, out_path, dma_orders=("host",), fences=("none",),
+            forensic=False, gates=("on",), compute="default"):
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -81,7 +84,7 @@ def _worker(rank, world, port, modes, priorities, steps, reps, out_path, dma_ord
                                v=torch.zeros(plan.local_stride, dtype=torch.float64, device=cuda))
                     local_out = prev[0]
                 fn = hip_reduce_fn(stack, w, na.MODE_W32_DIV64, denom, **epi)
-                if fen in ("release", "both"):  # L2 written back after every stripe's reduce
+                if fen.split("+")[0] in ("release", "both"):  # L2 written back after every stripe's reduce
                     def fn(lo, sc, out, _f=fn):
                         _f(lo, sc, out)
                         fence(na.FENCE_RELEASE)
@@ -105,7 +108,7 @@ def _worker(rank, world, port, modes, priorities, steps, reps, out_path, dma_ord
                         src_snap = red.local_out.clone()
                         bkt_snap = red.full[:p].clone()
                     full = red.step()
-                    if fen in ("acquire", "both"):  # L2 invalidated before the bucket is read
+                    if fen.split("+")[0] in ("acquire", "both"):  # L2 invalidated before the bucket is read
                         fence(na.FENCE_ACQUIRE)
                     full = full.cpu().numpy()
                     if forensic:
@@ -178,11 +181,21 @@ def _worker(rank, world, port, modes, priorities, steps, reps, out_path, dma_ord
             for rep in range(reps):
                 for mode in modes:
                     for order in (dma_orders if mode == "dma" else ("-",)):
-                        fd._DMA_ORDER = order if mode == "dma" else "producer"
+                        fd._DMA_ORDER = order if mode == "dma" else "host"
                         for fen in fences:
-                            run_plans(mode, prio, rep, order, fen)
-                            if rank == 0:
-                                print(f"{prio} rep {rep} {mode} {order} {fen}: done", file=sys.stderr, flush=True)
+                            for gate in (gates if mode == "dma" else ("on",)):
+                                L.fa_set_push_dma_gates(1 if gate == "on" else 0)
+                                tag = fen if gate == "on" else fen + "+nogates"
+                                if compute == "created":  # the whole job on a created compute stream
+                                    with torch.cuda.stream(torch.cuda.Stream(cuda)):
+                                        run_plans(mode, prio, rep, order, tag + "+created")
+                                        torch.cuda.synchronize()
+                                else:
+                                    run_plans(mode, prio, rep, order, tag)
+                                if rank == 0:
+                                    print(f"{prio} rep {rep} {mode} {order} {fen} gates {gate}: done", file=sys.stderr,
+                                          flush=True)
+                            L.fa_set_push_dma_gates(1)
                         if not explicit_registration(mode):
                             results.append({"priority": prio, "mode": mode, "order": order, "rep": rep,
                                             "plan": "explicit", "op": "-", "widths": [], "steps": 1,
@@ -190,7 +203,7 @@ def _worker(rank, world, port, modes, priorities, steps, reps, out_path, dma_ord
                 dist.barrier()
             fd.shutdown_push()
         fd.side_stream, fd.peer_stream = product
-        fd._DMA_ORDER = "producer"
+        fd._DMA_ORDER = "host"
         gathered = [None] * world
         dist.all_gather_object(gathered, results)
         if rank == 0:
@@ -231,14 +244,19 @@ def main():
     ap.add_argument("--modes", default="kernel,dma")
     ap.add_argument("--reps", type=int, default=3, help="times the test's whole sequence runs per priority")
     ap.add_argument("--priorities", default="normal,high")
-    ap.add_argument("--dma-orders", default="producer",
-                    help="the copy-engine legs' start event: producer (the product) and/or chain (round 5)")
+    ap.add_argument("--dma-orders", default="host",
+                    help="how the copy-engine legs follow their reduce: host (the product), producer (an event of "
+                         "the reduce's stream) and/or chain (round 5: an event of the pusher's stream)")
     ap.add_argument("--fences", default="none",
                     help="none / release (L2 written back after each stripe's reduce) / acquire (L2 invalidated "
                          "before the bucket is read) / both: which cache fence removes wrong buckets")
     ap.add_argument("--forensic", action="store_true",
                     help="classify wrong values: the sender's source before the step (a leg read early), this "
                          "rank's bucket before the step (a leg not landed), right when re-read 50 ms later")
+    ap.add_argument("--gates", default="on",
+                    help="on and/or off: fa_push_dma's gate kernels around each copy-engine leg (off: round 5's legs)")
+    ap.add_argument("--compute", default="default", choices=("default", "created"),
+                    help="the reduces' stream: torch's default (null) stream, or a created one")
     ap.add_argument("--out", default="gpurun_out/push_order.json")
     a = ap.parse_args()
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -247,8 +265,8 @@ def main():
         port = s.getsockname()[1]
     Path(a.out).parent.mkdir(parents=True, exist_ok=True)
     mp.spawn(_worker, args=(a.world, port, a.modes.split(","), a.priorities.split(","), a.steps, a.reps, a.out,
-                            tuple(a.dma_orders.split(",")), tuple(a.fences.split(",")), a.forensic), nprocs=a.world,
-             join=True)
+                            tuple(a.dma_orders.split(",")), tuple(a.fences.split(",")), a.forensic,
+                            tuple(a.gates.split(",")), a.compute), nprocs=a.world, join=True)
     print(Path(a.out).read_text())
 
 

@@ -113,7 +113,7 @@ def test_push_order_under_the_products_streams(cuda, tmp_path):
     assert p.returncode == 0, p.stderr[-3000:]
     summary = json.loads(out.read_text())["summary"]
     assert set(summary) == {f"{pr}/{m}/{o}" for pr in ("product", "high")
-                            for m, o in (("kernel", "-/mean"), ("kernel", "-/adagrad"), ("dma", "producer/mean"),
-                                         ("dma", "producer/adagrad"))}
+                            for m, o in (("kernel", "-/mean"), ("kernel", "-/adagrad"), ("dma", "host/mean"),
+                                         ("dma", "host/adagrad"))}
     for key, s in summary.items():
         assert s["steps"] == 8 * 4 * 2 * 3 and s["bad_steps"] == 0, (key, s["examples"])

@@ -1,4 +1,4 @@
-# Copy one tools/gpu_profile.sh pass into the tracked record and recompute profiles/traffic.json:
+# Copy one `tools/gpu_run.sh profile` pass into the tracked record and recompute profiles/traffic.json:
 #   bash tools/refresh_profiles.sh gpurun_out/<OUT> profiles/<round> tag [tag ...]
 set -e
 S=$1

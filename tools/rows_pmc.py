@@ -84,6 +84,7 @@ def main():
     out = torch.empty(stride, dtype=torch.float32, device=dev)
     out_rows = torch.empty(stride, dtype=torch.float32, device=dev)
     eng = Aggregator(output="device")
+    eng.packer.use_slabs = False  # --alloc stack IS a slab: measure the pointer-table kernel on it
     plan = make_plan([1.0] * n, clients)
     if op != "mean":  # double-buffered (prev, v_t) per kernel, same initial state
         pv, pr = ([torch.empty(stride, dtype=torch.float32, device=dev) for _ in range(2)] for _ in range(2))

@@ -1,7 +1,7 @@
 """Per-launch counter table of the row-pointer kernel vs the stack kernel from a
-tools/gpu_rows_pmc.sh pass directory (rocprofv3 csv).
+`tools/gpu_run.sh rows_pmc` / `slab_pmc` pass directory (rocprofv3 csv).
 
-    python tools/rows_pmc_table.py gpurun_out/<OUT> [--json]
+    python tools/rows_pmc_table.py gpurun_out/<OUT> [--json] [--pair=tagA,tagB ...]
 """
 from __future__ import annotations
 
@@ -53,6 +53,24 @@ def main():
         res[tag] = rec
     if "--json" in sys.argv:
         print(json.dumps(res, indent=1))
+        return
+    pairs = [a.split("=", 1)[1] for a in sys.argv if a.startswith("--pair=")]
+    if pairs:  # two tags that ran the SAME kernel in separate processes (slab_pmc: engine vs stack)
+        for pr in pairs:
+            ta, tb = pr.split(",")
+            ra, rb = res[ta], res[tb]
+            print(f"\n### {ta} vs {tb} (reduce_kernel_rowmajor in both)\n")
+            print(f"| counter (per launch) | {ta} | {tb} | ratio |")
+            print("|---|---|---|---|")
+            sa, sb = ra["time"].get("stack"), rb["time"].get("stack")
+            if sa and sb:
+                print(f"| kernel time (us, rocprof; calls {sa['calls']} / {sb['calls']}) | {sa['avg_us']:.1f} | "
+                      f"{sb['avg_us']:.1f} | {sa['avg_us'] / sb['avg_us']:.3f} |")
+            ca, cb = ra["counters"].get("stack", {}), rb["counters"].get("stack", {})
+            for ctr in sorted(set(ca) | set(cb)):
+                a, b = ca.get(ctr), cb.get(ctr)
+                ratio = f"{a / b:.3f}" if a is not None and b else "-"
+                print(f"| {ctr} | {'-' if a is None else f'{a:.4g}'} | {'-' if b is None else f'{b:.4g}'} | {ratio} |")
         return
     for tag, rec in res.items():
         print(f"\n### {tag}\n")

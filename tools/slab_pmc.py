@@ -76,7 +76,7 @@ def main():
         walls = []
         for r in range(a.reps):
             t0 = time.perf_counter()
-            g = s.server(uploads, r + 1)
+            g = s.server(uploads, r + 1)["w_glob"]
             torch.cuda.synchronize()
             walls.append(time.perf_counter() - t0)
         t = ev_time(lambda: s.server(uploads, 99), a.reps)

@@ -1,6 +1,6 @@
 // tune_rows.hip — geometry sweep of the row-pointer (device-upload) reduce; TOOL, not product.
 //
-// Built as tools/libtune_rows.so (hipcc, see tools/gpu_tune_rows.sh) and driven from Python
+// Built as tools/libtune_rows.so (hipcc --offload-arch=gfx950 -O3 -fPIC -shared tools/tune_rows.hip -o tools/libtune_rows.so) and driven from Python
 // (tools/tune_rows.py) with piece tables built there: the product kernel
 // (fa_device.hpp reduce_kernel_segrows, dynamic piece claiming) at several V / D / W.
 // Earlier sweeps of this file (profiles/r02/tune_rows/) also held a column-major kernel with
