@@ -47,12 +47,12 @@ from .streams import side_stream
 ALIGN = 64
 MAX_PUSH_RANKS = 8  # fa_push's destination count: one MI355X node
 
-#: how the copy-engine push's legs are ordered after their stripe's reduce: "host" (the host
-#: waits for the reduce, then issues the legs: no device-side cross-stream wait), "producer" (the
-#: legs' streams wait on an event of the reduce's stream) or "chain" (round 5: an event of the
-#: pusher's stream after its wait on the reduce's).  The device-side orders are kept so that
-#: tests/push_order_probe.py can replay them
-_DMA_ORDER = "host"
+#: how a push is ordered after its stripe's reduce: "host" (the host waits for the reduce, then
+#: issues the push — the copy-engine legs or the push kernel — with no device-side cross-stream
+#: wait), "producer" (the push's streams wait on an event of the reduce's stream) or "chain"
+#: (round 5: an event of the pusher's stream after its wait on the reduce's).  The device-side
+#: orders are kept so that tests/push_order_probe.py can replay them
+_PUSH_ORDER = "host"
 
 
 def peer_stream(device) -> torch.cuda.Stream:
@@ -535,7 +535,7 @@ class PushGather:
         # mode "dma": one stream per peer, each leg a copy-engine copy (fa_copy_dma) — copies on
         # one stream would run one after the other, one link at a time
         self.peer_streams = [peer_stream(self.device) for _ in range(self.world - 1)] if mode == "dma" else []
-        self._pending = None  # host order: the last stripe whose legs are not issued yet
+        self._pending = None  # host order: the last stripe whose push is not issued yet
         self._peer_handles = (ctypes.c_void_p * max(1, len(self.peer_streams)))(
             *[s.cuda_stream for s in self.peer_streams]) if self.peer_streams else None
 
@@ -560,55 +560,60 @@ class PushGather:
         if elem_offset < 0 or off + n > self.full.numel() * self.full.element_size():
             raise ValueError("push outside the receive buffer")
         cur = torch.cuda.current_stream(self.device)
-        self.stream.wait_stream(cur)
-        if self.mode == "kernel":
-            dsts = (ctypes.c_void_p * self.world)(*[d + off for d in self.dst])
-            self.na.check(self.L.fa_push(src.data_ptr(), n, dsts, self.world, self.grid, self.stream.cuda_stream),
-                          "fa_push")
-            return
-        # copy engines: the peers' legs on their own streams, this rank's own copy by a kernel on
-        # the pusher's stream.  HOST order (the default): the legs of stripe c are issued once the
-        # host has seen stripe c's reduce complete — at push(c+1), after reduce c+1 is queued, so
-        # the GPU never idles — and need no device-side wait.  With device-side waits (an event of
-        # the reduce's stream, "producer"; round 5's event on the pusher's stream, "chain"), eight
-        # processes sharing a GPU with the legs' streams on hardware queues of their own copied
-        # stripes before their reduce had finished, the own-copy kernel on the pusher's stream
-        # included (tests/push_order_probe.py --forensic)
-        if _DMA_ORDER == "host":
+        if _PUSH_ORDER == "host":
+            # the push of stripe c is issued once the host has seen stripe c's reduce complete — at
+            # push(c+1), after reduce c+1 is queued, so the GPU never idles — and needs no
+            # device-side wait.  With device-side waits (an event of the reduce's stream,
+            # "producer"; round 5's event on the pusher's stream, "chain"), eight processes sharing
+            # a GPU with the copy-engine legs' streams on hardware queues of their own copied
+            # stripes before their reduce had finished — the own-copy KERNEL on the pusher's stream
+            # included (tests/push_order_probe.py --forensic)
             ev = torch.cuda.Event()
             ev.record(cur)
             prev, self._pending = self._pending, (ev, src, off, n)
             if prev is not None:
-                self._issue_legs(*prev)
+                self._issue(*prev)
             return
-        after = self.stream if _DMA_ORDER == "chain" else cur
+        self.stream.wait_stream(cur)
+        if self.mode == "kernel":
+            self._push_kernel(src, off, n)
+            return
+        after = self.stream if _PUSH_ORDER == "chain" else cur
         peers = (ctypes.c_void_p * (self.world - 1))(*[d + off for r, d in enumerate(self.dst) if r != self.rank])
         self.na.check(self.L.fa_push_dma(src.data_ptr(), n, peers, self.world - 1, self._peer_handles,
                                          after.cuda_stream), "fa_push_dma")
         self.na.check(self.L.fa_copy(self.dst[self.rank] + off, src.data_ptr(), n, self.stream.cuda_stream), "fa_copy")
 
-    def _issue_legs(self, ev, src, off, n):
-        """Host order: wait on the host for the stripe's reduce, then its copy-engine legs and own copy."""
+    def _push_kernel(self, src, off, n):
+        dsts = (ctypes.c_void_p * self.world)(*[d + off for d in self.dst])
+        self.na.check(self.L.fa_push(src.data_ptr(), n, dsts, self.world, self.grid, self.stream.cuda_stream), "fa_push")
+
+    def _issue(self, ev, src, off, n):
+        """Host order: wait on the host for the stripe's reduce, then push it — the push kernel on
+        the pusher's stream, or the copy-engine legs on theirs and this rank's own copy."""
         ev.synchronize()
+        if self.mode == "kernel":
+            self._push_kernel(src, off, n)
+            return
         peers = [d + off for r, d in enumerate(self.dst) if r != self.rank]
         for d, s in zip(peers, self.peer_streams):
             self.na.check(self.L.fa_copy_dma(d, src.data_ptr(), n, s.cuda_stream), "fa_copy_dma")
         self.na.check(self.L.fa_copy(self.dst[self.rank] + off, src.data_ptr(), n, self.stream.cuda_stream), "fa_copy")
 
     def join(self):
-        """The copy-engine legs are complete before the closing barrier (mode "dma"): in host order
-        the host waits for the legs' streams; otherwise the pusher's stream waits on them."""
-        if not self.peer_streams:
-            return
-        if _DMA_ORDER == "host":
+        """Every push of the step is issued and the copy-engine legs are complete before the
+        closing barrier: in host order the pending stripe is pushed and the host waits for the
+        legs' streams; otherwise the pusher's stream waits on them."""
+        if _PUSH_ORDER == "host":
             if self._pending is not None:
                 pending, self._pending = self._pending, None
-                self._issue_legs(*pending)
+                self._issue(*pending)
             for s in self.peer_streams:
                 s.synchronize()
             return
-        self.na.check(self.L.fa_stream_join(self.stream.cuda_stream, self._peer_handles, len(self.peer_streams)),
-                      "fa_stream_join")
+        if self.peer_streams:
+            self.na.check(self.L.fa_stream_join(self.stream.cuda_stream, self._peer_handles, len(self.peer_streams)),
+                          "fa_stream_join")
 
     def end(self):
         self.join()

@@ -11,15 +11,13 @@ priority) compute stream's: the same pipeline then ran 91-93% of its gather time
 Priority also lets the gather's small kernels be dispatched ahead of the reduce's blocks, which
 suits work on the step's critical path.
 
-Used for KERNEL work beside the compute stream only.  Copy-engine transfers (hipMemcpyAsync ...
-NoCU) run on the copy engines whatever queue their stream has, and with high-priority streams a
-rank's slice was wrong in the buckets after the step's closing barrier — half of the wrong values
-the previous step's, half the bucket's older contents: tests/push_order_probe.py, eight processes,
-the copy-engine push with in-place Adagrad, 32 of 576 rank-steps wrong with high-priority streams
-and 0 of 576 with normal ones (the kernel push: 0 of 576 either way;
-profiles/r05/pipeline_queues/).  RCCL's internal stream stays in torch's normal pool (the process
-group's default): a high-priority one would give the all-gather its own queue too, but the line
-bench.py must not lose runs on it, and one GPU cannot test RCCL between ranks.
+The push gathers' pusher stream (both forms): its push kernels or own copies run beside the next
+stripe's reduce.  The copy-engine legs' streams stay at normal priority (flearn_amd.dist.peer_stream).
+Round 5 saw wrong buckets with the copy-engine push's streams at high priority; round 6 found the
+cause — device-side cross-queue event waits that let copies start before their reduce finished,
+with several processes' streams on queues of their own — and removed the push's reliance on them
+(host-ordered pushes), so correctness no longer depends on which queues the
+streams get.  RCCL's internal stream stays in torch's normal pool (the process group's default).
 """
 from __future__ import annotations
 

@@ -290,7 +290,11 @@ int fa_copy_dma(void* dst, const void* src, int64_t nbytes, void* stream);
  * (the stream that wrote src),
  * copy nbytes from src to dsts[i] on streams[i] (i < n_dsts <= 8; one copy engine per peer
  * stream).  What eight Python-level event records / waits / copies cost in host time per stripe
- * (~80 us) this does in a few; the stripe pipeline is host-bound otherwise.  ABI 12.           */
+ * (~80 us) this does in a few.  ABI 12.  The ordering is a device-side cross-queue event wait:
+ * with eight processes sharing a GPU and the legs' streams on hardware queues of their own, legs
+ * ordered this way copied stripes before their reduce had finished.
+ * flearn_amd.dist issues its legs in HOST order instead — fa_copy_dma per leg once the host has
+ * seen the reduce complete — and keeps this entry for C callers and the probe's A/B.            */
 int fa_push_dma(const void* src, int64_t nbytes, void* const* dsts, int32_t n_dsts, void* const* streams,
                 void* stream);
 

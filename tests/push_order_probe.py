@@ -181,7 +181,7 @@ def _worker(rank, world, port, modes, priorities, steps, reps, out_path, dma_ord
             for rep in range(reps):
                 for mode in modes:
                     for order in (dma_orders if mode == "dma" else ("-",)):
-                        fd._DMA_ORDER = order if mode == "dma" else "host"
+                        fd._PUSH_ORDER = order if mode == "dma" else "host"
                         for fen in fences:
                             for gate in (gates if mode == "dma" else ("on",)):
                                 L.fa_set_push_dma_gates(1 if gate == "on" else 0)
@@ -203,7 +203,7 @@ def _worker(rank, world, port, modes, priorities, steps, reps, out_path, dma_ord
                 dist.barrier()
             fd.shutdown_push()
         fd.side_stream, fd.peer_stream = product
-        fd._DMA_ORDER = "host"
+        fd._PUSH_ORDER = "host"
         gathered = [None] * world
         dist.all_gather_object(gathered, results)
         if rank == 0:

@@ -123,11 +123,12 @@ def test_bench_keeps_rccl_when_a_push_fails_its_check(cuda):
     before the push phase, so the run still ends verified."""
     p = _rehearse("c2", ("--no-weak", "--no-loopback", "--stripes", "2", "--gather", "push"), inject="push_offset")
     assert p.returncode == 0, p.stderr[-4000:]
-    assert "failed the self-check: keeping the RCCL line" in p.stderr
+    assert "gather failed its step audit: keeping the RCCL line" in p.stderr  # every step is off
     d = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][0])
     mg = d["multi_gpu"]
     assert mg["gather"] == "rccl" and mg["push_failed_self_check"]["gather"] == "push"
-    assert mg["push_failed_self_check"]["mismatched_windows"] > 0
+    assert mg["push_failed_self_check"]["mismatched_windows"] > 0  # and the last step's windows
+    assert mg["push_failed_self_check"]["audit"]["bad_steps_by_rank"] == [20, 20]
     assert mg["phases"]["push"]["status"] == "failed_self_check"
     assert d["verify"]["verified"] is True and "RCCL all-gather" in d["config"]["parallelism"]
 
