@@ -37,6 +37,7 @@ host memory around the collective (`all_gather_into`).
 from __future__ import annotations
 
 import ctypes
+import warnings
 from dataclasses import dataclass
 
 import torch
@@ -994,12 +995,13 @@ class ShardedReducer:
 
     def __del__(self):
         if getattr(self, "pusher", None) is not None:
-            import warnings
-
             # release() is collective: it cannot run here; the bucket stays taken until
             # shutdown_push frees the pool
-            warnings.warn("ShardedReducer with a push gather dropped without release(): its receive bucket "
-                          "stays in use until shutdown_push", ResourceWarning, stacklevel=2)
+            try:
+                warnings.warn("ShardedReducer with a push gather dropped without release(): its receive bucket "
+                              "stays in use until shutdown_push", ResourceWarning, stacklevel=2)
+            except Exception:  # noqa: BLE001 - interpreter shutdown: nothing left to warn
+                pass
 
     @property
     def local_out(self) -> torch.Tensor:

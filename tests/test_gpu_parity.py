@@ -671,14 +671,13 @@ def test_sharded_reducer_push_rccl_one_rank(push, cuda, tmp_path):
         w = torch.ones(n, dtype=torch.float32, device=cuda)
         red = ShardedReducer(plan, hip_reduce_fn(stack, w, na.MODE_W32_DIV64, float(n)), cuda, gather=True, push=push)
         assert red.pusher is not None and red.pusher.nccl
-        # the kernel push's stream is high priority (a hardware queue apart from the compute
-        # stream's); the copy-engine push's streams are normal priority (flearn_amd/streams.py)
+        # both forms push from a high-priority stream (a hardware queue apart from the compute
+        # stream's); the copy-engine legs' streams are normal priority.  Pushes are host-ordered,
+        # so correctness does not depend on either
         from flearn_amd import streams
 
-        if push is True:
-            assert red.pusher.stream.priority == streams.HIGH
-        else:
-            assert red.pusher.stream.priority == 0 and all(x.priority == 0 for x in red.pusher.peer_streams)
+        assert red.pusher.stream.priority == streams.HIGH
+        assert all(x.priority == 0 for x in red.pusher.peer_streams)
         want = oracle.c_reduce(oracle.MODE_W32_DIV64, oracle.fill_uniform(n, p, 5), np.ones(n, np.float32), float(n))
         for _ in range(3):
             full = red.step()
