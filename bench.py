@@ -151,9 +151,12 @@ class Job:
     columns (plan) resident in HBM, the fused HIP reduce per stripe and (world > 1) the RCCL
     all-gather of every stripe."""
 
-    def __init__(self, cfg, layout, n, plan, dev, world, reorder, push=False, push_grid=0):
+    def __init__(self, cfg, layout, n, plan, dev, world, reorder, push=False, push_grid=0, reducer=True):
+        """reducer=False: allocate and fill only (local); make_reducer() then builds the sharded
+        reducer — collective when pushing (the peers map each other's buckets)."""
         self.cfg, self.n, self.plan, self.dev = cfg, n, plan, dev
-        self.push = push
+        self.world, self.push, self.push_grid = world, push, push_grid
+        self.red = None
         cols, stride = plan.local_cols, plan.local_stride
         log(f"[rank {plan.rank}] alloc {n} x {cols} fp32 = {n * cols * 4 / 1e9:.2f} GB, stripes {plan.widths}"
             + (f" + replicated tail {plan.rep}" if plan.rep else ""))
@@ -172,7 +175,13 @@ class Job:
             self.reset_state(state)
             epi = dict(op=na.OP_BY_NAME[cfg["op"]], state=state)
         self.fn = hip_reduce_fn(self.stack, self.weights, na.MODE_W32_DIV64, self.denom, reorder=reorder, **epi)
-        self.red = ShardedReducer(plan, self.fn, dev, gather=world > 1, state=state, push=push, push_grid=push_grid)
+        self._state = state
+        if reducer:
+            self.make_reducer()
+
+    def make_reducer(self):
+        self.red = ShardedReducer(self.plan, self.fn, self.dev, gather=self.world > 1, state=self._state, push=self.push,
+                                  push_grid=self.push_grid)
 
     def reset_state(self, state=None):
         """The fused optimizers' initial state: prev = the seed-1 synthetic model on this rank's
@@ -437,10 +446,23 @@ def _trial(cfg, layout, n, args, world, rank, dev, g_eff, gather, widths, rep, m
     p_real = layouts.fp32_elems(layout)
     rec = {"gather": gather, "stripe_widths": list(widths), "replicated_cols": rep,
            "predicted_ms": round(model.makespan(widths, rep)[0] * 1e3, 4)}
+    # the allocation is local, so it may fail on some ranks only (out of memory): agree on it
+    # before anything collective, so that every rank skips the candidate together
+    tj, err = None, None
     try:
         tj = Job(cfg, layout, n, ShardPlan.from_widths(p_real, g_eff, rank, widths, rep=rep), dev, world, args.reorder,
-                 push=PUSH_MODE.get(gather, False), push_grid=push_grid)
-    except RuntimeError as e:  # a push that every rank refused to set up (PushGather)
+                 push=PUSH_MODE.get(gather, False), push_grid=push_grid, reducer=False)
+    except (torch.OutOfMemoryError, RuntimeError) as e:
+        err = f"{type(e).__name__}: {e}"[:200]
+    if _max_over_ranks((0.0 if tj is not None else 1.0,), world, dev)[0] > 0.0:
+        tj = None
+        torch.cuda.empty_cache()
+        rec.update(measured_ms=None, error=err or "another rank could not allocate this candidate")
+        return rec
+    try:
+        tj.make_reducer()
+    except RuntimeError as e:  # a push that every rank refused to set up (PushGather, collective)
+        tj = None
         torch.cuda.empty_cache()
         rec.update(measured_ms=None, error=str(e))
         return rec
@@ -479,9 +501,11 @@ def plan_rccl(cfg, layout, n, args, world, rank, dev, g_eff):
     trials, best_s = [], None
     if world > 1 and len(cands) > 1:
         trials = [_trial(cfg, layout, n, args, world, rank, dev, g_eff, "rccl", w_c, r_c, model) for w_c, r_c in cands]
-        i = min(range(len(cands)), key=lambda k: trials[k]["measured_ms"])
-        widths, rep = cands[i]
-        best_s = trials[i]["measured_ms"] * 1e-3
+        ok = [k for k in range(len(cands)) if trials[k]["measured_ms"] is not None]
+        if ok:  # (a candidate some rank could not allocate is skipped on every rank)
+            i = min(ok, key=lambda k: trials[k]["measured_ms"])
+            widths, rep = cands[i]
+            best_s = trials[i]["measured_ms"] * 1e-3
     plan = ShardPlan.from_widths(p_real, g_eff, rank, widths, rep=rep)
     info = dict(stripe_choice=("model (flearn_amd.dist.plan_shards: stripes + replicated tail), coefficients fitted "
                                "on this job" + ("; the fastest of the model's plan and its neighbours over 5 measured "
@@ -670,10 +694,12 @@ def push_audit(job, world, dev, steps: int = AUDIT_STEPS) -> dict:
     idx = (torch.arange(max(p.widths), dtype=torch.int64, device=dev) % 65521) + 1
     real = red.reduce_fn
     sent = {}
+    starts = {p.local_begin(c) for c in range(p.stripes)}  # the replicated tail is not pushed
 
     def hooked(lo, sc, out):
         real(lo, sc, out)
-        sent[lo] = _checksums(out, idx)
+        if lo in starts:
+            sent[lo] = _checksums(out, idx)
 
     red.reduce_fn = hooked
     bad = []

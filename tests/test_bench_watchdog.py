@@ -110,3 +110,42 @@ def test_signal_after_the_line_was_printed_adds_nothing():
     assert p.returncode == -signal.SIGTERM
     lines = [ln for ln in p.stdout.splitlines() if ln.strip()]
     assert len(lines) == 1 and "ended_by_signal" not in lines[0]
+
+
+def _outcome_worker(rank, world, init, stuck, out):
+    import torch.distributed as dist
+
+    sys.path.insert(0, str(REPO))
+    import bench
+
+    dist.init_process_group("gloo", init_method=init, rank=rank, world_size=world)
+    try:
+        if stuck and rank == 1:  # a rank still inside the phase: it never posts its outcome
+            time.sleep(4.0)
+            return
+        got = bench._agree_outcomes("adopted" if rank == 0 else "failed_self_check", rank, world, 2.0)
+        Path(out).with_suffix(f".{rank}").write_text(json.dumps(got))
+    finally:
+        if not (stuck and rank == 1):
+            time.sleep(2.5)  # let the stuck peer's sleep end before the group goes away
+        dist.destroy_process_group()
+
+
+def test_push_phase_outcomes_are_agreed_through_the_store(tmp_path):
+    """bench._agree_outcomes: every rank's push-phase outcome through the process
+    group's store, no collective — all ranks see all outcomes; a rank that never posts (stuck in
+    a collective of the phase) makes the others' wait time out (None) instead of pairing with an
+    unrelated collective."""
+    import os
+
+    import torch.multiprocessing as mp
+
+    for stuck in (False, True):
+        init = "file://" + os.path.join(str(tmp_path), f"pg_{stuck}")
+        out = tmp_path / f"out_{stuck}"
+        mp.spawn(_outcome_worker, args=(2, init, stuck, str(out)), nprocs=2, join=True)
+        if stuck:
+            assert json.loads(out.with_suffix(".0").read_text()) is None
+        else:
+            for r in (0, 1):
+                assert json.loads(out.with_suffix(f".{r}").read_text()) == ["adopted", "failed_self_check"]
