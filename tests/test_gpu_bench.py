@@ -218,3 +218,60 @@ def test_single_gpu_line_is_verified(cuda):
     assert p.returncode == 0, p.stderr[-3000:]
     d = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][0])
     assert d["verify"]["verified"] is True and d["verify"]["windows"] >= 64 and d["verify"]["state_windows"] >= 2
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("push", [True, "dma"])
+def test_push_audit_with_a_replicated_tail(push, cuda, tmp_path, monkeypatch):
+    """bench.push_audit on a plan with a replicated tail (the tail is reduced, not pushed: the
+    audit checks the stripes only), a 1-rank RCCL group: 20 clean steps verify; one push skipped
+    in the 5th audited step is caught on that step alone."""
+    import types
+
+    import torch
+    import torch.distributed as dist
+
+    sys.path.insert(0, str(REPO))
+    import bench
+    from flearn_amd import _native as na
+    from flearn_amd import aggregator as agg
+    from flearn_amd import dist as fd
+    from flearn_amd.dist import PingPong, ShardedReducer, ShardPlan, hip_reduce_fn
+
+    created = False
+    if not dist.is_initialized():
+        dist.init_process_group("nccl", init_method=f"file://{tmp_path}/pg", rank=0, world_size=1, device_id=cuda)
+        created = True
+    try:
+        n, p = 5, 300_032
+        plan = ShardPlan.from_widths(p, 1, 0, (64_000, 128_000), rep=p - 192_000)
+        stack = torch.empty((n, plan.local_stride), dtype=torch.float32, device=cuda)
+        for lo, g0, width in plan.segments():
+            agg.fill_uniform(stack[:, lo:], seed=9, col_begin=g0, n_cols=width)
+        prev = torch.empty((1, plan.local_stride), dtype=torch.float32, device=cuda)
+        agg.fill_uniform(prev, seed=4)
+        state = PingPong(prev[0], torch.zeros(plan.local_stride, dtype=torch.float64, device=cuda))
+        w = torch.ones(n, dtype=torch.float32, device=cuda)
+        fn = hip_reduce_fn(stack, w, na.MODE_W32_DIV64, float(n), op=na.OP_BY_NAME["avgm"], state=state)
+        red = ShardedReducer(plan, fn, cuda, gather=True, state=state, push=push)
+        job = types.SimpleNamespace(red=red, plan=plan)
+        a = bench.push_audit(job, 1, cuda)
+        assert a["verified"] is True and a["audited_steps"] == 20 and a["bad_steps_by_rank"] == [0]
+        real_push, count = fd.PushGather.push, {"n": 0}
+
+        def skip_one(self, src, off):
+            count["n"] += 1
+            if count["n"] == 2 * 4 + 2:  # the 5th step's second stripe
+                return None
+            return real_push(self, src, off)
+
+        monkeypatch.setattr(fd.PushGather, "push", skip_one)
+        a = bench.push_audit(job, 1, cuda)
+        assert a["verified"] is False and a["bad_steps_by_rank"] == [1]
+        assert a["first_bad"] == [{"step": 4, "slices": [{"sender": 0, "stripe": 1}]}]
+        monkeypatch.setattr(fd.PushGather, "push", real_push)
+        red.release()
+        fd.shutdown_push()
+    finally:
+        if created:
+            dist.destroy_process_group()
