@@ -52,6 +52,7 @@ def run(a):
         agg.fill_uniform(stack, seed=2024)
         w = torch.ones(n, dtype=torch.float32, device=dev)
         push = {"rccl": False, "push": True, "push_dma": "dma"}[a.gather]
+        fd._PUSH_ORDER = a.order  # host (the product) or producer (a device-side event wait)
         red = fd.ShardedReducer(plan, fd.hip_reduce_fn(stack, w, na.MODE_W32_DIV64, float(n)), dev, gather=True,
                                 push=push)
         if red.pusher is not None and a.pusher_stream != "default":
@@ -75,7 +76,7 @@ def run(a):
         red.release()
         fd.shutdown_push()
         print(json.dumps({"gather": a.gather, "stripes": a.stripes, "clients": n, "cols": p, "steps": a.steps,
-                          "pusher_stream": a.pusher_stream, "nccl_high": a.nccl_high,
+                          "pusher_stream": a.pusher_stream, "nccl_high": a.nccl_high, "order": a.order,
                           "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"), "ms_per_step": round(ms, 4)}))
     finally:
         dist.destroy_process_group()
@@ -125,6 +126,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gather", default="push", choices=["rccl", "push", "push_dma"])
     ap.add_argument("--stripes", type=int, default=4)
+    ap.add_argument("--order", default="host", choices=["host", "producer"],
+                    help="how each stripe's push follows its reduce (flearn_amd.dist._PUSH_ORDER)")
     ap.add_argument("--clients", type=int, default=100)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--analyze", default=None, help="a rocprofv3 kernel_trace.csv of a run")
