@@ -84,3 +84,52 @@ def test_resolve_matches_numpy_or_refuses(ws, xdtype):
     for w, c in zip(ws, nm.weights):
         one = (w * np.ones(1, xdtype))[0]  # numpy's cast of the weight in its product (x 1: exact)
         assert one.dtype == acc.dtype and (one == c or (np.isnan(one) and np.isnan(c)))
+
+
+@settings(max_examples=120, deadline=None)
+@given(layout, st.integers(1, 6), st.data())
+def test_slab_stack_is_the_uploads_or_nothing(lay, n, data):
+    """Packer._slab_stack over random layouts and random client selections from one
+    device_state_dicts slab (CPU tensors): a selection of consecutive rows in order becomes a
+    [N, stride] view whose every key segment IS each client's tensor (same bytes, same address);
+    any other selection (reordered, gapped, a foreign tensor) is refused."""
+    import torch
+
+    from flearn_amd import device_state_dicts
+    from flearn_amd.bucket import Packer
+
+    keys = [f"layer{i}.{'weight' if i % 2 else 'bias'}" for i in range(len(lay))]
+    template = {k: torch.from_numpy(np.zeros(s, dt)) for k, (s, dt) in zip(keys, lay)}
+    plan0 = make_plan([1.0], [template])
+    if KIND_F32 not in plan0.groups:
+        return
+    sd = device_state_dicts(template, n + 2, device="cpu")
+    torch.manual_seed(n)
+    sd.slab.copy_(torch.randn_like(sd.slab))
+    start = data.draw(st.integers(0, 2))
+    order = list(range(start, start + n))
+    kind = data.draw(st.sampled_from(["consecutive", "reversed", "gapped", "foreign"]))
+    if kind == "reversed" and n > 1:
+        order = order[::-1]
+    elif kind == "gapped" and n > 1 and start == 0:
+        order = [0] + list(range(2, n + 1))  # row 1 skipped: no single pitch
+    clients = [dict(sd[i]) for i in order]
+    if kind == "foreign":
+        k = next(s.key for s in plan0.groups[KIND_F32].segments)
+        clients[-1][k] = clients[-1][k].clone()
+    plan = make_plan([1.0] * len(clients), clients)
+    g = plan.groups[KIND_F32]
+    segs = [s for s in g.segments if s.numel > 0]
+    if not segs:
+        return
+    ptrs = np.array([[c[s.key].data_ptr() for c in clients] for s in segs], dtype=np.int64)
+    st_ = Packer._slab_stack(plan, g, clients, (segs, ptrs, [], None))
+    in_order = all(b - a == 1 for a, b in zip(order, order[1:]))
+    if kind == "foreign" or not in_order:
+        assert st_ is None
+        return
+    assert st_ is not None and st_.shape == (len(clients), g.stride)
+    for r, c in enumerate(clients):
+        for s in segs:
+            view = st_[r, s.offset : s.offset + s.numel]
+            assert view.data_ptr() == c[s.key].data_ptr() and torch.equal(view, c[s.key].reshape(-1))
