@@ -902,7 +902,7 @@ static int stream_after(hipStream_t to, hipStream_t from) {
   hipError_t e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
   if (e == hipSuccess) e = hipEventRecord(ev, from);
   if (e == hipSuccess) e = hipStreamWaitEvent(to, ev, 0);
-  hipEventDestroy(ev);
+  (void)hipEventDestroy(ev);
   if (e != hipSuccess) return fail(FA_ERR_LAUNCH, hipGetErrorString(e));
   return FA_OK;
 }
@@ -943,7 +943,7 @@ int fa_push_dma(const void* src, int64_t nbytes, void* const* dsts, int32_t n_ds
       e = hipGetLastError();
     }
   }
-  hipEventDestroy(ev);
+  (void)hipEventDestroy(ev);
   if (e != hipSuccess) return fail(FA_ERR_LAUNCH, hipGetErrorString(e));
   return FA_OK;
 }
