@@ -36,3 +36,20 @@ def test_mnist_loop_server_steps_match_reference(http, cuda):
                   on_server=on_server, log=lambda *a: None)
     assert checked == [0, 1] and len(hist) == 2
     assert all(np.isfinite(h["mean_local_loss"]) for h in hist)
+
+
+def test_run2_slab_uploads_with_a_server_restart(cuda):
+    """examples/run2_slab_restart.py: clients' parameters live in one device_state_dicts slab,
+    the server-fused FedAVGM reads them in place every round (path "slab"), and a restart at
+    round 2 through server_opt.state_dict() / load_state gives the same global models, bit for
+    bit, as the uninterrupted run."""
+    import run2_slab_restart as ex
+
+    quiet = dict(clients=6, rounds=4, device=cuda, log=lambda *a: None, train=False)
+    with_restart, paths = ex.run(restart_at=2, **quiet)
+    straight, paths2 = ex.run(restart_at=None, **quiet)
+    assert paths == paths2 == ["slab"] * 4
+    for r, (a, b) in enumerate(zip(with_restart, straight)):
+        assert set(a) == set(b)
+        for k in a:
+            assert torch.equal(a[k].view(torch.int32), b[k].view(torch.int32)), (r, k)
