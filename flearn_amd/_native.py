@@ -55,7 +55,6 @@ EXPORTS = (
     "fa_push_dma",
     "fa_stream_join",
     "fa_cache_fence",
-    "fa_set_push_dma_gates",
     "fa_set_reduce_grid",
     "fa_reduce_windows",
     "fa_b64_decoded_size",
@@ -215,7 +214,6 @@ def load(require_gpu: bool = False):
                 "fa_push_dma": ([P, I64, ctypes.POINTER(P), I32, ctypes.POINTER(P), P], ctypes.c_int),
                 "fa_stream_join": ([P, ctypes.POINTER(P), I32], ctypes.c_int),
                 "fa_cache_fence": ([I32, P], ctypes.c_int),
-                "fa_set_push_dma_gates": ([I32], ctypes.c_int),
                 "fa_set_reduce_grid": ([I32], ctypes.c_int),
                 "fa_reduce_windows": ([I32, I64], ctypes.c_int),
                 "fa_b64_decoded_size": ([P, I64], I64),

@@ -1548,9 +1548,6 @@ struct PushDsts {
 // (K = 1) invalidates it, so that a copy engine (which reads and writes HBM behind the L2) and the
 // kernels around it see each other's data (fa_cache_fence).  Each XCD has its own L2: the launch
 // spreads one wave over every XCD, several times over.
-// an empty one-wave kernel: an ordering point on a stream (fa_push_dma's gates)
-__global__ __launch_bounds__(64) void gate_kernel() {}
-
 template <int K>
 __global__ __launch_bounds__(64) void cache_fence_kernel() {
   if (K == 0)

@@ -907,18 +907,6 @@ static int stream_after(hipStream_t to, hipStream_t from) {
   return FA_OK;
 }
 
-// Gate kernels around every copy-engine leg (fa_push_dma): the leg's stream waits on the
-// producer's event with a one-wave kernel, copies, and runs another one-wave kernel that the
-// join's event follows — so both cross-queue edges of a leg are kernel-to-kernel waits and the
-// copy engine depends only on its own stream's neighbours.  Without them, with the legs' streams
-// on queues of their own and eight processes sharing a GPU, copy-engine legs that waited on the
-// producer's event directly copied their source before the reduce writing it had finished
-// (tests/push_order_probe.py --forensic: every wrong value was the sender's source as it was
-// before the step).
-static std::atomic<int> g_dma_gates{1};
-
-int fa_set_push_dma_gates(int32_t on) { return g_dma_gates.exchange(on ? 1 : 0); }
-
 int fa_push_dma(const void* src, int64_t nbytes, void* const* dsts, int32_t n_dsts, void* const* streams,
                 void* stream) {
   if (nbytes < 0 || n_dsts < 0 || n_dsts > 8) return fail(FA_ERR_ARG, "bad push size or destination count");
@@ -926,22 +914,13 @@ int fa_push_dma(const void* src, int64_t nbytes, void* const* dsts, int32_t n_ds
   if (!src || !dsts || !streams) return fail(FA_ERR_ARG, "null push pointer");
   for (int i = 0; i < n_dsts; ++i)
     if (!dsts[i] || !streams[i]) return fail(FA_ERR_ARG, "null push destination or stream");
-  const bool gates = g_dma_gates.load(std::memory_order_relaxed) != 0;
   hipEvent_t ev;
   hipError_t e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
   if (e == hipSuccess) e = hipEventRecord(ev, static_cast<hipStream_t>(stream));
   for (int i = 0; i < n_dsts && e == hipSuccess; ++i) {
     hipStream_t s = static_cast<hipStream_t>(streams[i]);
     e = hipStreamWaitEvent(s, ev, 0);
-    if (e == hipSuccess && gates) {
-      hipLaunchKernelGGL(gate_kernel, dim3(1), dim3(64), 0, s);
-      e = hipGetLastError();
-    }
     if (e == hipSuccess) e = hipMemcpyAsync(dsts[i], src, (size_t)nbytes, kCopyEngine, s);
-    if (e == hipSuccess && gates) {
-      hipLaunchKernelGGL(gate_kernel, dim3(1), dim3(64), 0, s);
-      e = hipGetLastError();
-    }
   }
   (void)hipEventDestroy(ev);
   if (e != hipSuccess) return fail(FA_ERR_LAUNCH, hipGetErrorString(e));

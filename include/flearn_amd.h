@@ -298,11 +298,6 @@ int fa_copy_dma(void* dst, const void* src, int64_t nbytes, void* stream);
 int fa_push_dma(const void* src, int64_t nbytes, void* const* dsts, int32_t n_dsts, void* const* streams,
                 void* stream);
 
-/* fa_push_dma's gate kernels (default on): each leg's stream runs a one-wave kernel after its wait
- * on `stream` and another after the copy, so that the copy engine's only dependencies are on its
- * own stream.  on = 0 turns them off (tests/push_order_probe.py's A/B only).  Returns the previous
- * setting.  ABI 14.                                                                             */
-int fa_set_push_dma_gates(int32_t on);
 
 /* `stream` waits for the work queued so far on streams[0..n) (n <= 16).  ABI 12.             */
 int fa_stream_join(void* stream, void* const* streams, int32_t n);

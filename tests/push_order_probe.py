@@ -8,7 +8,8 @@ their own hardware queue?  (rounds 5-6)
 rank-steps were wrong.  Round 6: with every push stream at high priority the copy-engine legs AND
 the pusher's own-copy kernel copied stripes before their reduce had finished, whatever the
 device-side order — `--dma-orders chain` (round 5: an event of the pusher's stream), `producer` (an
-event of the reduce's own stream), with gate kernels or L2 fences — while `host`, the product's
+event of the reduce's own stream), with L2 fences (or, in round 6's first build, one-wave gate kernels
+around each leg) — while `host`, the product's
 order now, issues each stripe's legs only after the host has seen its reduce complete.  "high" puts
 the pusher's stream AND every leg's stream at high priority: none of them shares the compute
 stream's hardware queue; "hipusher" / "hipeers" only one side)
@@ -38,7 +39,7 @@ sys.path.insert(0, str(REPO))
 
 
 def _worker(rank, world, port, modes, priorities, steps, reps, out_path, dma_orders=("host",), fences=("none",),
-            forensic=False, gates=("on",), compute="default"):
+            forensic=False, compute="default"):
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -183,19 +184,14 @@ def _worker(rank, world, port, modes, priorities, steps, reps, out_path, dma_ord
                     for order in (dma_orders if mode == "dma" else ("-",)):
                         fd._PUSH_ORDER = order if mode == "dma" else "host"
                         for fen in fences:
-                            for gate in (gates if mode == "dma" else ("on",)):
-                                L.fa_set_push_dma_gates(1 if gate == "on" else 0)
-                                tag = fen if gate == "on" else fen + "+nogates"
-                                if compute == "created":  # the whole job on a created compute stream
-                                    with torch.cuda.stream(torch.cuda.Stream(cuda)):
-                                        run_plans(mode, prio, rep, order, tag + "+created")
-                                        torch.cuda.synchronize()
-                                else:
-                                    run_plans(mode, prio, rep, order, tag)
-                                if rank == 0:
-                                    print(f"{prio} rep {rep} {mode} {order} {fen} gates {gate}: done", file=sys.stderr,
-                                          flush=True)
-                            L.fa_set_push_dma_gates(1)
+                            if compute == "created":  # the whole job on a created compute stream
+                                with torch.cuda.stream(torch.cuda.Stream(cuda)):
+                                    run_plans(mode, prio, rep, order, fen + "+created")
+                                    torch.cuda.synchronize()
+                            else:
+                                run_plans(mode, prio, rep, order, fen)
+                            if rank == 0:
+                                print(f"{prio} rep {rep} {mode} {order} {fen}: done", file=sys.stderr, flush=True)
                         if not explicit_registration(mode):
                             results.append({"priority": prio, "mode": mode, "order": order, "rep": rep,
                                             "plan": "explicit", "op": "-", "widths": [], "steps": 1,
@@ -253,8 +249,6 @@ def main():
     ap.add_argument("--forensic", action="store_true",
                     help="classify wrong values: the sender's source before the step (a leg read early), this "
                          "rank's bucket before the step (a leg not landed), right when re-read 50 ms later")
-    ap.add_argument("--gates", default="on",
-                    help="on and/or off: fa_push_dma's gate kernels around each copy-engine leg (off: round 5's legs)")
     ap.add_argument("--compute", default="default", choices=("default", "created"),
                     help="the reduces' stream: torch's default (null) stream, or a created one")
     ap.add_argument("--out", default="gpurun_out/push_order.json")
@@ -265,8 +259,8 @@ def main():
         port = s.getsockname()[1]
     Path(a.out).parent.mkdir(parents=True, exist_ok=True)
     mp.spawn(_worker, args=(a.world, port, a.modes.split(","), a.priorities.split(","), a.steps, a.reps, a.out,
-                            tuple(a.dma_orders.split(",")), tuple(a.fences.split(",")), a.forensic,
-                            tuple(a.gates.split(",")), a.compute), nprocs=a.world, join=True)
+                            tuple(a.dma_orders.split(",")), tuple(a.fences.split(",")), a.forensic, a.compute),
+             nprocs=a.world, join=True)
     print(Path(a.out).read_text())
 
 
