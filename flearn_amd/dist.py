@@ -201,7 +201,8 @@ class DeviceBuffer:
         return t
 
     def free(self):
-        """Release: an exported buffer is parked for reuse (never freed), any other freed."""
+        """Release: an exported buffer is parked for reuse (freed only beyond the parking cap), any
+        other freed."""
         if not self.ptr:
             return
         if self.exported:
@@ -374,9 +375,9 @@ class _RecvPool:
     job (`take` / `give`: a few ms of collective set-up and token checks saved per job — the
     bench's plan trials build a dozen jobs).  Released collectively: `shutdown_push(group)`
     (call it before destroying the group) has every peer close its imports, then a barrier, and
-    the buckets are parked (DeviceBuffer: exported memory is never freed while the process lives
-    — freeing it is what made later imports map the wrong allocation) for
-    the next pool to re-export.  A `take` that finds no free bucket large enough first releases
+    the buckets are parked (DeviceBuffer: exported memory is parked for re-export, freed only
+    beyond the parking cap — freeing imported memory is what made later imports map the wrong
+    allocation) for the next pool to re-export.  A `take` that finds no free bucket large enough first releases
     the free ones (same protocol) and takes a parked one that fits or a new one of the request's
     size class (DeviceBuffer.get), so the buckets held stay near the largest set in use at once
     and the parked ones within DeviceBuffer's cap.  Every rank takes and gives in the
@@ -417,7 +418,7 @@ class _RecvPool:
         _unmap_all([b for i in idx for b in self.slots[i][3]], pg.group)
         for i in sorted(idx, reverse=True):
             buf = self.slots.pop(i)[0]
-            buf.free()  # exported: parked for reuse, never freed
+            buf.free()  # exported: parked for reuse (within the parking cap)
 
     def take(self, pg, cols: int):
         i = next((j for j, s in enumerate(self.slots) if not s[4] and s[1].numel() >= cols), None)
@@ -434,7 +435,7 @@ class _RecvPool:
             buf = DeviceBuffer.get(-(-want // ALIGN) * ALIGN * 4, self.device)
             view = buf.tensor(torch.float32)
             pg.full, pg.device = view, self.device
-            buf.exported = True  # from here on never freed: parked when released
+            buf.exported = True  # from here on parked when released
             try:
                 bases, dsts, _stale = _map_peers(pg, view)
             except RuntimeError:
@@ -470,7 +471,8 @@ class _RecvPool:
 def shutdown_push(group=None, device=None):
     """Collective over `group`: release the push gather's receive buckets of this process for
     that group — every peer's mapping closed, then a barrier, then each rank parks its own
-    (DeviceBuffer.get hands them to the next pool; exported memory is never freed).  Call it
+    (DeviceBuffer.get hands them to the next pool; beyond the parking cap the smallest are
+    freed).  Call it
     before dist.destroy_process_group; the next push job maps its buckets afresh."""
     g = _resolve_group(group)
     for key in [k for k, p in _RecvPool._pools.items() if p.gobj is g
@@ -522,7 +524,7 @@ class PushGather:
             self.pool_slot, buf, self.dst = self.pool.take(self, cols)
             self.full, self.bases, self.stale = buf[:cols], [], []
         else:
-            if isinstance(full, DeviceBuffer):  # exported from here on: never freed (parked)
+            if isinstance(full, DeviceBuffer):  # exported from here on: parked when released
                 full.exported = True
                 self.owner, full = full, full.tensor(torch.float32)
             self.full, self.device = full, full.device
