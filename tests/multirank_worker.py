@@ -358,10 +358,45 @@ def case_push_lifecycle(rank, world):
     assert len(pool_ptrs | own_ptrs) <= 6, (len(pool_ptrs), len(own_ptrs))
 
 
+def case_push_growth_trim(rank, world):
+    """Growing receive buckets (x1.25 per job, both push forms): each larger request retires the
+    free bucket, and the parked bytes pass the cap (2 x the largest exported), so parked buckets
+    are FREED — the operation that, with several processes on one GPU, made later imports map the
+    wrong allocation.  The guarantee under test: a job either gathers exactly the all-gather's
+    bucket or its set-up is refused on every rank by the token check (RCCL then); never a wrong
+    bucket.  Parked bytes stay within the cap throughout."""
+    from flearn_amd import dist as fd
+
+    cuda = torch.device("cuda", 0)
+    fd.shutdown_push()
+    refused = 0
+    cols0 = world * 65536
+    for it in range(10):
+        cols = (int(cols0 * 1.25 ** it) // (world * 64)) * world * 64
+        src = torch.arange(cols // world, dtype=torch.float32, device=cuda) + 1e5 * rank + it
+        want = torch.empty(cols, dtype=torch.float32, device=cuda)
+        fd.all_gather_into(want, src)
+        try:
+            pg = fd.PushGather(None, None, mode="kernel" if it % 2 == 0 else "dma", cols=cols, device=cuda)
+        except RuntimeError as e:  # refused together: every rank raised, nothing stays mapped
+            assert "tokens" in str(e) or "could not map" in str(e), e
+            refused += 1
+            continue
+        pg.gather(src, rank * (cols // world))
+        torch.cuda.synchronize()
+        assert torch.equal(pg.full, want), (rank, it)
+        pg.close()
+        assert fd.DeviceBuffer.parked_bytes(cuda) <= fd.DeviceBuffer.park_cap(cuda)
+    fd.shutdown_push()
+    assert fd.DeviceBuffer.parked_bytes(cuda) <= fd.DeviceBuffer.park_cap(cuda)
+    assert fd.DeviceBuffer.trimmed()["buckets"] > 0  # the cap did free exported buckets
+    print(f"[rank {rank}] growth: {fd.DeviceBuffer.trimmed()} trimmed, {refused} set-ups refused", flush=True)
+
+
 CASES = {f.__name__[5:]: f for f in (case_avg_fixtures, case_setup_strategy, case_fused_rounds,
                                       case_first_round_adopt, case_empty_ranks, case_dyn, case_sharded_reducer,
                                       case_sharded_reducer_push, case_sharded_reducer_push_dma,
-                                      case_push_lifecycle)}
+                                      case_push_lifecycle, case_push_growth_trim)}
 
 
 def rank_main(rank, world, port, names):

@@ -92,6 +92,15 @@ def test_push_setup_lifecycle(world, cuda):
 
 
 @pytest.mark.timeout(300)
+@pytest.mark.parametrize("world", [2, 3])
+def test_push_buckets_trimmed_beyond_the_cap(world, cuda):
+    """Receive buckets growing x1.25 per job: parked buckets beyond the cap are freed, and every
+    later job either gathers exactly the all-gather's bucket or is refused on every rank by the
+    token check — never a wrong bucket (flearn_amd.dist.DeviceBuffer)."""
+    _run_ranks(world, ["push_growth_trim"])
+
+
+@pytest.mark.timeout(300)
 def test_push_order_under_the_products_streams(cuda, tmp_path):
     """tests/push_order_probe.py: eight processes replay the push test's sequence (mean and in-place
     Adagrad over four stripe plans, then an explicit registration) twice in both push forms, every
