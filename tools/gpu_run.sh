@@ -7,7 +7,8 @@
 #
 #   suite          pytest -m gpu (whole suite), smoke(), the default bench line   (the driver's round end)
 #   bench          the default bench line (ARGS are passed to bench.py)
-#   rehearsal      bench.py's N>1 path: ranks sharing the GPU over gloo (ARGS: config [ranks], default ns 2)
+#   rehearsal      bench.py's N>1 path: ranks sharing the GPU over gloo (ARGS: config ranks [bench flags],
+#                  default ns 2)
 #   profile        per config (ARGS: tag:config[:flags] ..., default ns:ns): bench line, bench under
 #                  rocprofv3 --kernel-trace --stats, separate --pmc FETCH_SIZE / WRITE_SIZE passes
 #                  (then tools/refresh_profiles.sh gpurun_out/OUT profiles/<round> <tags>)
@@ -52,9 +53,10 @@ bench() {
 
 rehearsal() {
   local cfg=${1:-ns} g=${2:-2}
+  if [ $# -ge 2 ]; then shift 2; else set --; fi
   FLEARN_BENCH_BACKEND=gloo MASTER_ADDR=127.0.0.1 timeout -k 10 600 python3 -m torch.distributed.run --nnodes=1 \
     --nproc-per-node="$g" --master-addr=127.0.0.1 --master-port=29533 bench.py --gpus "$g" --steps 5 --warmup 2 \
-    --config "$cfg" > "$O/rehearsal_${cfg}_g$g.json" 2> "$O/rehearsal_${cfg}_g$g.err" \
+    --config "$cfg" "$@" > "$O/rehearsal_${cfg}_g$g.json" 2> "$O/rehearsal_${cfg}_g$g.err" \
     || { echo "rehearsal failed"; tail "$O/rehearsal_${cfg}_g$g.err"; return 1; }
   echo "rehearsal $cfg g$g ok"
 }
