@@ -163,6 +163,10 @@ bool rowmajor_geometry(int64_t chunks, int cus, int64_t target, int64_t* grid, i
   return false;
 }
 
+// The widest grid of one-piece blocks (reduce_kernel_rows) the geometry below uses: 13/16 of the
+// CUs (100 x 3.2 M columns on 196 blocks 89.7-90.1%, 100 x 3.5 M on 214 blocks 88.6%)
+int64_t rows_grid_max(int cus) { return (int64_t)cus * 13 / 16; }
+
 // fa_set_reduce_grid: 0 = the geometry below chooses the grid
 std::atomic<int> g_reduce_grid{0};
 
@@ -200,8 +204,14 @@ int launch_reduce_window(const typename P::x_t* stack, int64_t stride, int n, co
           default: return launch_rowmajor<P, T, OP, 4>(stack, stride, n, wt, col0, ncols, e, g, s);
         }
       }
-      if (forced <= 0 && chunks > (int64_t)cus * kPieceChunks &&
-          rowmajor_geometry(chunks, cus, (int64_t)(cus * kRowsBlocksPerCU + 0.5), &g, &kg)) {
+      // Past one round of the grid: row-major groups.  So also where one piece per block would
+      // take more than rows_grid_max blocks — two pieces per block on a grid near 13/16 of the
+      // CUs instead (100 x 4.19 M columns: 256 one-piece blocks 246 us = 86.0%, 208 blocks x 2
+      // pieces 235 us = 90.2%; tools/width_sweep.py, profiles/r06/width/)
+      const bool past = chunks > (int64_t)cus * kPieceChunks;
+      if (forced <= 0 && chunks > rows_grid_max(cus) * kPieceChunks &&
+          rowmajor_geometry(chunks, cus, past ? (int64_t)(cus * kRowsBlocksPerCU + 0.5) : (int64_t)cus * 13 / 16, &g,
+                            &kg)) {
         switch (kg) {
           case 2: return launch_rowmajor<P, T, OP, 2>(stack, stride, n, wt, col0, ncols, e, g, s);
           case 3: return launch_rowmajor<P, T, OP, 3>(stack, stride, n, wt, col0, ncols, e, g, s);
@@ -216,7 +226,7 @@ int launch_reduce_window(const typename P::x_t* stack, int64_t stride, int n, co
       grid = (chunks + kPieceChunks - 1) / kPieceChunks;
     if (grid < 1) grid = 1;
     if (grid > chunks) grid = chunks;
-    const int64_t share = (chunks + grid - 1) / grid;  // chunks per block
+    int64_t share = (chunks + grid - 1) / grid;  // chunks per block
     if (share <= 2) {
       // narrow windows (at most two 1-KiB chunks of every row per block: LeNet-sized models, deep
       // client stacks): reduce_kernel_narrow, one single-wave block per chunk, a D-deep pipeline
@@ -234,6 +244,21 @@ int launch_reduce_window(const typename P::x_t* stack, int64_t stride, int n, co
     }
     if constexpr (OP == FA_OP_MEAN) {
       constexpr int W = 4;
+      // A share just past a power of two leaves about half of every pipeline slot empty (the
+      // piece is V*W KiB wide, `share` KiB of it real, D = 64/(V*W) rows deep).  Where a grid of
+      // at most kRowsGridMax blocks makes the share a whole power of two, take that grid: plain
+      // mean 100 x 1.6 M columns 95.1 -> 91.1 us, 100 x 800 K 48.6 -> 47.3 us; shares >= 60% full
+      // (100 x 2.4 M, 1.2 M, 600 K, 200 K) lose with it, and so do the fused epilogues
+      // (tools/width_sweep.py, profiles/r06/width/)
+      if (forced <= 0) {
+        int64_t cap = W;
+        while (cap < share) cap *= 2;
+        const int64_t g2 = (chunks + cap / 2 - 1) / (cap / 2);
+        if (cap > W && share * 5 < cap * 3 && g2 <= rows_grid_max(cus)) {
+          grid = g2;
+          share = (chunks + grid - 1) / grid;
+        }
+      }
       if (share <= 1 * W) return launch_rows<P, T, OP, 1, W>(stack, stride, n, wt, col0, ncols, e, grid, s);
       if (share <= 2 * W) return launch_rows<P, T, OP, 2, W>(stack, stride, n, wt, col0, ncols, e, grid, s);
       if (share <= 4 * W) return launch_rows<P, T, OP, 4, W>(stack, stride, n, wt, col0, ncols, e, grid, s);
@@ -241,7 +266,11 @@ int launch_reduce_window(const typename P::x_t* stack, int64_t stride, int n, co
       return launch_rows<P, T, OP, 16, W>(stack, stride, n, wt, col0, ncols, e, grid, s);
     } else {
       constexpr int W = 8;
-      if (share <= 1 * W) return launch_rows<P, T, OP, 1, W>(stack, stride, n, wt, col0, ncols, e, grid, s);
+      // shares of at most 8 KiB on 4 waves: with 8 waves one quad per lane (V = 1, 8 rows deep)
+      // compiles into register copies — 240 VGPRs, scratch spills and ~1,290 v_mov_b64 per
+      // kernel, for every epilogue — and 100 x 200 K FedAVGM took 45 us, 3x the plain mean
+      if (share <= 4) return launch_rows<P, T, OP, 1, 4>(stack, stride, n, wt, col0, ncols, e, grid, s);
+      if (share <= 8) return launch_rows<P, T, OP, 2, 4>(stack, stride, n, wt, col0, ncols, e, grid, s);
       if (share <= 2 * W) return launch_rows<P, T, OP, 2, W>(stack, stride, n, wt, col0, ncols, e, grid, s);
       if (share <= 4 * W) return launch_rows<P, T, OP, 4, W>(stack, stride, n, wt, col0, ncols, e, grid, s);
       return launch_rows<P, T, OP, 8, W>(stack, stride, n, wt, col0, ncols, e, grid, s);

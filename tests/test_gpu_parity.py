@@ -261,7 +261,9 @@ def test_reduce_kernel_big_tiles_ragged(n, ncols, cuda):
 # per wave) and pipeline depth D = 16/V on the 192/224-block grid, with ragged piece and window
 # ends; deep stacks are the per-rank shapes of the multi-GPU runs
 ROW_SHAPES = [(800, 150001), (300, 390001), (200, 700003), (64, 1500007), (40, 3300001), (17, 33), (2, 5000003),
-              (12, 3500001),  # widens the grid to one full piece per block
+              (10, 3300001),  # one piece per block on a widened grid (at most 13/16 of the CUs)
+              (12, 3500001), (8, 4194304),  # past that: two pieces per block, row-major groups
+              (20, 1600635), (30, 800318),  # a share just past a power of two: the grid that fills the piece
               (3, 14000003), (2, 9000001),  # row-major groups of 5 and 3 pieces
               (1000, 44426), (150, 44426), (300, 70001), (349, 70001), (600, 44426), (700, 3), (256, 1),
               (2000, 5)]  # narrow windows: one-wave blocks, D 16/32/40, tail rounds
@@ -306,7 +308,10 @@ def test_row_pipeline_geometries(n, ncols, cuda):
 @pytest.mark.parametrize("n,ncols,op", [(300, 390001, "avgm"), (64, 1500007, "adagrad"), (800, 150001, "adam"),
                                          (50, 700003, "yogi"), (20, 3000001, "avgm"), (10, 3500001, "adagrad"),
                                          (6, 9000003, "avgm"), (1000, 44426, "avgm"), (400, 70001, "adagrad"),
-                                         (120, 44426, "yogi"), (1000, 44426, "adam")])
+                                         (120, 44426, "yogi"), (1000, 44426, "adam"),
+                                         # shares of <= 8 KiB: the 4-wave kernels; past 13/16 of the CUs
+                                         (100, 200080, "adagrad"), (60, 100000, "yogi"), (100, 300000, "adam"),
+                                         (8, 4194304, "avgm")])
 def test_row_pipeline_fused_epilogues(n, ncols, op, cuda):
     stride = -(-ncols // 64) * 64
     x = _device_stack(n, stride, seed=ncols)
