@@ -38,7 +38,8 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--pitch", default="contiguous", choices=("contiguous", "full"))
     ap.add_argument("--grids", default="0", help="comma list of forced grids per width (fa_set_reduce_grid; 0 = "
-                    "the library's choice); 'fit' = the grid whose share fills the piece (ceil(chunks / 2^j))")
+                    "the library's choice); 'fit' = the grid whose share fills the piece (ceil(chunks / 2^j)); "
+                    "'narrow' = a share of 2 chunks (the one-wave-per-chunk kernel)")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
@@ -64,7 +65,8 @@ def main():
                       v_out=torch.zeros(wdt, dtype=torch.float64, device=dev))
         fn = lambda: agg.reduce_stack(x, w, na.MODE_W32_DIV64, float(n), n_cols=wdt, out32=out, **kw)  # noqa: E731
         for gs in a.grids.split(","):
-            grid = fit_grid(wdt, a.op) if gs == "fit" else int(gs)
+            chunks = -(-(-(-wdt // 4)) // 64)
+            grid = fit_grid(wdt, a.op) if gs == "fit" else -(-chunks // 2) if gs == "narrow" else int(gs)
             L.fa_set_reduce_grid(grid)  # returns the previous setting
             time_one(a, L, n, wdt, fn, grid)
         L.fa_set_reduce_grid(0)
