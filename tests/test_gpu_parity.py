@@ -910,10 +910,11 @@ def test_dyn_errors_like_reference(cuda):
 
 
 @pytest.mark.parametrize("prec", ["f64", "f32", "w64"])
-@pytest.mark.parametrize("p", [1, 4093, 5001, 8388608 + 5])
+@pytest.mark.parametrize("p", [1, 4093, 5001, 100001, 200081, 8388608 + 5])
 def test_dyn_epilogue_vs_c_oracle(prec, p, cuda):
     """Kernel level, 2 rounds with state carried: fused reduce+FedDyn vs the C restatement,
-    small (balanced grid) and big-tile (buffer-descriptor path, ragged tail) buckets."""
+    small (balanced grid), one-piece 4-wave (100 K, 200 K columns) and big-tile
+    (buffer-descriptor path, ragged tail) buckets."""
     n = 7 if p < 10**6 else 3
     stride = -(-p // 64) * 64
     mode = {"f64": na.MODE_W32_DIV64, "f32": na.MODE_W32_DIV32, "w64": na.MODE_W64}[prec]
