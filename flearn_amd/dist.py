@@ -551,6 +551,9 @@ class PushGather:
             dist.barrier(group=self.group)
 
     def begin(self):
+        # a step abandoned between its pushes (an exception before end()) leaves its last stripe
+        # pending: never issue it into this step's buckets
+        self._pending = None
         self.stream.wait_stream(torch.cuda.current_stream(self.device))
         self._barrier()
 
