@@ -454,8 +454,6 @@ class _RecvPool:
         """Collective: unmap every bucket on every rank, barrier, park."""
         busy = [j for j, s in enumerate(self.slots) if s[4]]
         if busy:
-            import warnings
-
             warnings.warn(f"shutdown_push: {len(busy)} receive bucket(s) still in use by a reducer that was "
                           "not released; their results are overwritten by the next push job", stacklevel=3)
         self._retire(pg, list(range(len(self.slots))))
