@@ -246,8 +246,8 @@ int launch_reduce_window(const typename P::x_t* stack, int64_t stride, int n, co
       constexpr int W = 4;
       // A share just past a power of two leaves about half of every pipeline slot empty (the
       // piece is V*W KiB wide, `share` KiB of it real, D = 64/(V*W) rows deep).  Where a grid of
-      // at most kRowsGridMax blocks makes the share a whole power of two, take that grid: plain
-      // mean 100 x 1.6 M columns 95.1 -> 91.1 us, 100 x 800 K 48.6 -> 47.3 us; shares >= 60% full
+      // at most rows_grid_max blocks makes the share a whole power of two, take that grid: plain
+      // mean 100 x 1.6 M columns 95.1 -> 90.3-90.8 us, 100 x 800 K 48.6 -> 46.5 us; shares >= 60% full
       // (100 x 2.4 M, 1.2 M, 600 K, 200 K) lose with it, and so do the fused epilogues
       // (tools/width_sweep.py, profiles/r06/width/)
       if (forced <= 0) {
@@ -271,6 +271,20 @@ int launch_reduce_window(const typename P::x_t* stack, int64_t stride, int n, co
       // kernel, for every epilogue — and 100 x 200 K FedAVGM took 45 us, 3x the plain mean
       if (share <= 4) return launch_rows<P, T, OP, 1, 4>(stack, stride, n, wt, col0, ncols, e, grid, s);
       if (share <= 8) return launch_rows<P, T, OP, 2, 4>(stack, stride, n, wt, col0, ncols, e, grid, s);
+      // a share just past 16 or 32 KiB: the grid that makes it a whole 16 / 32 KiB piece, on 4
+      // waves (the mean's rule; 8 waves lose there): FedAVGM 100 x 1.6 M 85.0 -> 88.4-88.6%,
+      // 100 x 800 K 83.0 -> 85.8-86.0%; shares of 9-16 KiB stay on 8 waves (100 x 400 K: 77.9%
+      // against 75.6-75.9% filled on 4; tools/width_sweep.py, profiles/r06/width/fused_*)
+      if (forced <= 0 && share > 16) {
+        const int64_t cap = share <= 32 ? 32 : 64;
+        const int64_t g2 = (chunks + cap / 2 - 1) / (cap / 2);
+        if (share * 5 < cap * 3 && g2 <= rows_grid_max(cus)) {
+          grid = g2;
+          share = (chunks + grid - 1) / grid;
+          if (share <= 16) return launch_rows<P, T, OP, 4, 4>(stack, stride, n, wt, col0, ncols, e, grid, s);
+          return launch_rows<P, T, OP, 8, 4>(stack, stride, n, wt, col0, ncols, e, grid, s);
+        }
+      }
       if (share <= 2 * W) return launch_rows<P, T, OP, 2, W>(stack, stride, n, wt, col0, ncols, e, grid, s);
       if (share <= 4 * W) return launch_rows<P, T, OP, 4, W>(stack, stride, n, wt, col0, ncols, e, grid, s);
       return launch_rows<P, T, OP, 8, W>(stack, stride, n, wt, col0, ncols, e, grid, s);

@@ -311,7 +311,9 @@ def test_row_pipeline_geometries(n, ncols, cuda):
                                          (120, 44426, "yogi"), (1000, 44426, "adam"),
                                          # shares of <= 8 KiB: the 4-wave kernels; past 13/16 of the CUs
                                          (100, 200080, "adagrad"), (60, 100000, "yogi"), (100, 300000, "adam"),
-                                         (8, 4194304, "avgm")])
+                                         (8, 4194304, "avgm"),
+                                         # shares just past 32 / 16 KiB: filled, on 4 waves
+                                         (40, 1600635, "yogi"), (50, 800318, "adagrad")])
 def test_row_pipeline_fused_epilogues(n, ncols, op, cuda):
     stride = -(-ncols // 64) * 64
     x = _device_stack(n, stride, seed=ncols)

@@ -37,12 +37,15 @@ def main():
     ap.add_argument("--op", default="mean", choices=("mean", "avgm"))
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--pitch", default="contiguous", choices=("contiguous", "full"))
+    ap.add_argument("--lib", default=None, help="a tuning build of libflearn_amd.so to load instead of the product's")
     ap.add_argument("--grids", default="0", help="comma list of forced grids per width (fa_set_reduce_grid; 0 = "
                     "the library's choice); 'fit' = the grid whose share fills the piece (ceil(chunks / 2^j)); "
                     "'narrow' = a share of 2 chunks (the one-wave-per-chunk kernel)")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
+    if a.lib:
+        na.LIB_PATH = Path(a.lib).resolve()
     L = na.lib()
     n = a.clients
     widths = [int(x) for x in a.widths.split(",")]
