@@ -90,9 +90,10 @@ def test_resolve_matches_numpy_or_refuses(ws, xdtype):
 @given(layout, st.integers(1, 6), st.data())
 def test_slab_stack_is_the_uploads_or_nothing(lay, n, data):
     """Packer._slab_stack over random layouts and random client selections from one
-    device_state_dicts slab (CPU tensors): a selection of consecutive rows in order becomes a
-    [N, stride] view whose every key segment IS each client's tensor (same bytes, same address);
-    any other selection (reordered, gapped, a foreign tensor) is refused."""
+    device_state_dicts slab (CPU tensors): a selection of rows at one positive pitch (consecutive
+    rows in order, or two rows with a gap) becomes a [N, stride] view whose every key segment IS
+    each client's tensor (same bytes, same address); any other selection (reordered, unevenly
+    gapped, a foreign tensor) is refused."""
     import torch
 
     from flearn_amd import device_state_dicts
@@ -112,7 +113,7 @@ def test_slab_stack_is_the_uploads_or_nothing(lay, n, data):
     if kind == "reversed" and n > 1:
         order = order[::-1]
     elif kind == "gapped" and n > 1 and start == 0:
-        order = [0] + list(range(2, n + 1))  # row 1 skipped: no single pitch
+        order = [0] + list(range(2, n + 1))  # row 1 skipped: one pitch only for two rows
     clients = [dict(sd[i]) for i in order]
     if kind == "foreign":  # a non-empty key (an empty tensor reads no bytes: its address is moot)
         k = next((s.key for s in plan0.groups[KIND_F32].segments if s.numel > 0), None)
@@ -126,8 +127,10 @@ def test_slab_stack_is_the_uploads_or_nothing(lay, n, data):
         return
     ptrs = np.array([[c[s.key].data_ptr() for c in clients] for s in segs], dtype=np.int64)
     st_ = Packer._slab_stack(plan, g, clients, (segs, ptrs, [], None))
-    in_order = all(b - a == 1 for a, b in zip(order, order[1:]))
-    if kind == "foreign" or not in_order:
+    # rows at one positive pitch (consecutive, or two rows with a gap) are a strided [N, stride] view
+    steps = {b - a for a, b in zip(order, order[1:])}
+    uniform = not steps or (len(steps) == 1 and steps.pop() > 0)
+    if kind == "foreign" or not uniform:
         assert st_ is None
         return
     assert st_ is not None and st_.shape == (len(clients), g.stride)
