@@ -49,11 +49,22 @@ ALIGN = 64
 MAX_PUSH_RANKS = 8  # fa_push's destination count: one MI355X node
 
 #: how a push is ordered after its stripe's reduce: "host" (the host waits for the reduce, then
-#: issues the push — the copy-engine legs or the push kernel — with no device-side cross-stream
-#: wait), "producer" (the push's streams wait on an event of the reduce's stream) or "chain"
-#: (round 5: an event of the pusher's stream after its wait on the reduce's).  The device-side
-#: orders are kept so that tests/push_order_probe.py can replay them
-_PUSH_ORDER = "host"
+#: issues the push with no device-side cross-stream wait), "producer" (the push's streams wait on
+#: an event of the reduce's stream) or "chain" (round 5: an event of the pusher's stream after its
+#: wait on the reduce's).  "auto", the product's: the copy-engine push in host order — with
+#: device-side waits its legs (and its own-copy kernel) started before the reduce had finished,
+#: 1-30% of rank-steps among eight processes on one GPU — and the kernel push in producer order:
+#: never wrong in the same probes (0 of 6,656 rank-steps, tests/push_order_probe.py), and host
+#: order costs it a host round trip per stripe (100 x 3.2 M columns, a rank's share of NS at G = 8,
+#: 4 stripes: 0.32-0.40 ms per step against 0.275)
+_PUSH_ORDER = "auto"
+
+
+def push_order(mode: str) -> str:
+    """The order a PushGather of `mode` uses now (_PUSH_ORDER resolved)."""
+    if _PUSH_ORDER != "auto":
+        return _PUSH_ORDER
+    return "producer" if mode == "kernel" else "host"
 
 
 def peer_stream(device) -> torch.cuda.Stream:
@@ -564,14 +575,16 @@ class PushGather:
         if elem_offset < 0 or off + n > self.full.numel() * self.full.element_size():
             raise ValueError("push outside the receive buffer")
         cur = torch.cuda.current_stream(self.device)
-        if _PUSH_ORDER == "host":
-            # the push of stripe c is issued once the host has seen stripe c's reduce complete — at
-            # push(c+1), after reduce c+1 is queued, so the GPU never idles — and needs no
+        order = push_order(self.mode)
+        if order == "host":
+            # (the copy-engine push) the push of stripe c is issued once the host has seen stripe
+            # c's reduce complete — at push(c+1), after reduce c+1 is queued — and needs no
             # device-side wait.  With device-side waits (an event of the reduce's stream,
             # "producer"; round 5's event on the pusher's stream, "chain"), eight processes sharing
             # a GPU with the copy-engine legs' streams on hardware queues of their own copied
             # stripes before their reduce had finished — the own-copy KERNEL on the pusher's stream
-            # included (tests/push_order_probe.py --forensic)
+            # included (tests/push_order_probe.py --forensic).  The kernel push
+            # (no copy-engine streams) takes the device-side order below: see _PUSH_ORDER
             ev = torch.cuda.Event()
             ev.record(cur)
             prev, self._pending = self._pending, (ev, src, off, n)
@@ -582,7 +595,7 @@ class PushGather:
         if self.mode == "kernel":
             self._push_kernel(src, off, n)
             return
-        after = self.stream if _PUSH_ORDER == "chain" else cur
+        after = self.stream if order == "chain" else cur
         peers = (ctypes.c_void_p * (self.world - 1))(*[d + off for r, d in enumerate(self.dst) if r != self.rank])
         self.na.check(self.L.fa_push_dma(src.data_ptr(), n, peers, self.world - 1, self._peer_handles,
                                          after.cuda_stream), "fa_push_dma")
@@ -607,8 +620,9 @@ class PushGather:
     def join(self):
         """Every push of the step is issued and the copy-engine legs are complete before the
         closing barrier: in host order the pending stripe is pushed and the host waits for the
-        legs' streams; otherwise the pusher's stream waits on them."""
-        if _PUSH_ORDER == "host":
+        legs' streams; otherwise the pusher's stream waits on them (a pending stripe left by a
+        switch of _PUSH_ORDER mid-step is flushed either way)."""
+        if push_order(self.mode) == "host" or self._pending is not None:
             if self._pending is not None:
                 pending, self._pending = self._pending, None
                 self._issue(*pending)

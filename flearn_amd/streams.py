@@ -15,9 +15,10 @@ The push gathers' pusher stream (both forms): its push kernels or own copies run
 stripe's reduce.  The copy-engine legs' streams stay at normal priority (flearn_amd.dist.peer_stream).
 Round 5 saw wrong buckets with the copy-engine push's streams at high priority; round 6 found the
 cause — device-side cross-queue event waits that let copies start before their reduce finished,
-with several processes' streams on queues of their own — and removed the push's reliance on them
-(host-ordered pushes), so correctness no longer depends on which queues the
-streams get.  RCCL's internal stream stays in torch's normal pool (the process group's default).
+with several processes' streams on queues of their own — and removed the copy-engine push's
+reliance on them (its legs are host-ordered); the kernel push, never wrong
+with its device-side wait in the same probes, keeps it.  RCCL's internal stream stays in torch's
+normal pool (the process group's default).
 """
 from __future__ import annotations
 

@@ -39,7 +39,7 @@ sys.path.insert(0, str(REPO))
 
 
 def _worker(rank, world, port, modes, priorities, steps, reps, out_path, dma_orders=("host",), fences=("none",),
-            forensic=False, compute="default"):
+            forensic=False, compute="default", kernel_orders=("-",)):
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -181,8 +181,8 @@ def _worker(rank, world, port, modes, priorities, steps, reps, out_path, dma_ord
                 fd.peer_stream = hi if prio in ("high", "hipeers") else lo
             for rep in range(reps):
                 for mode in modes:
-                    for order in (dma_orders if mode == "dma" else ("-",)):
-                        fd._PUSH_ORDER = order if mode == "dma" else "host"
+                    for order in (dma_orders if mode == "dma" else kernel_orders):
+                        fd._PUSH_ORDER = order if order != "-" else "auto"
                         for fen in fences:
                             if compute == "created":  # the whole job on a created compute stream
                                 with torch.cuda.stream(torch.cuda.Stream(cuda)):
@@ -199,7 +199,7 @@ def _worker(rank, world, port, modes, priorities, steps, reps, out_path, dma_ord
                 dist.barrier()
             fd.shutdown_push()
         fd.side_stream, fd.peer_stream = product
-        fd._PUSH_ORDER = "host"
+        fd._PUSH_ORDER = "auto"
         gathered = [None] * world
         dist.all_gather_object(gathered, results)
         if rank == 0:
@@ -240,6 +240,8 @@ def main():
     ap.add_argument("--modes", default="kernel,dma")
     ap.add_argument("--reps", type=int, default=3, help="times the test's whole sequence runs per priority")
     ap.add_argument("--priorities", default="normal,high")
+    ap.add_argument("--kernel-orders", default="-",
+                    help="comma list for the kernel push: host / producer ('-': the product's order, labelled '-')")
     ap.add_argument("--dma-orders", default="host",
                     help="how the copy-engine legs follow their reduce: host (the product), producer (an event of "
                          "the reduce's stream) and/or chain (round 5: an event of the pusher's stream)")
@@ -259,7 +261,8 @@ def main():
         port = s.getsockname()[1]
     Path(a.out).parent.mkdir(parents=True, exist_ok=True)
     mp.spawn(_worker, args=(a.world, port, a.modes.split(","), a.priorities.split(","), a.steps, a.reps, a.out,
-                            tuple(a.dma_orders.split(",")), tuple(a.fences.split(",")), a.forensic, a.compute),
+                            tuple(a.dma_orders.split(",")), tuple(a.fences.split(",")), a.forensic, a.compute,
+                            tuple(a.kernel_orders.split(","))),
              nprocs=a.world, join=True)
     print(Path(a.out).read_text())
 

@@ -103,12 +103,13 @@ def test_push_buckets_trimmed_beyond_the_cap(world, cuda):
 @pytest.mark.timeout(300)
 def test_push_order_under_the_products_streams(cuda, tmp_path):
     """tests/push_order_probe.py: eight processes replay the push test's sequence (mean and in-place
-    Adagrad over four stripe plans, then an explicit registration) twice in both push forms, every
-    step's bucket bit-compared with the C oracle — 0 wrong rank-steps — with the product's streams
-    AND with every push stream (the pusher's, each copy-engine leg's) forced onto high priority, so
-    that none of them shares the compute stream's hardware queue.  Round 5's copy-engine push
-    failed that second configuration (32 of 576 in-place Adagrad rank-steps): its legs' start
-    event was recorded on the pusher's stream, not on the reduce's."""
+    Adagrad over four stripe plans, then an explicit registration) twice in both push forms, in the
+    product's orders (the kernel push after a device-side wait on the reduce's stream, the
+    copy-engine push in host order), every step's bucket bit-compared with the C oracle — 0 wrong
+    rank-steps — with the product's streams AND with every push stream (the pusher's, each
+    copy-engine leg's) forced onto high priority, so that none of them shares the compute stream's
+    hardware queue.  The copy-engine push with device-side waits fails that second configuration
+    (1-30% of rank-steps wrong)."""
     import json
     import subprocess
     import sys

@@ -45,14 +45,14 @@ def run(a):
         kw["pg_options"] = dist.ProcessGroupNCCL.Options(is_high_priority_stream=True)
     dist.init_process_group("nccl", init_method=init, rank=0, world_size=1, device_id=dev, **kw)
     try:
-        p = layouts.padded_f32_stride(layouts.get("resnet50"))
+        p = a.cols or layouts.padded_f32_stride(layouts.get("resnet50"))
         n = a.clients
         plan = fd.ShardPlan.make(p, 1, 0, stripes=a.stripes)
         stack = torch.empty((n, plan.local_cols), dtype=torch.float32, device=dev)
         agg.fill_uniform(stack, seed=2024)
         w = torch.ones(n, dtype=torch.float32, device=dev)
         push = {"rccl": False, "push": True, "push_dma": "dma"}[a.gather]
-        fd._PUSH_ORDER = a.order  # host (the product) or producer (a device-side event wait)
+        fd._PUSH_ORDER = a.order  # auto (the product), host, or producer (a device-side event wait)
         red = fd.ShardedReducer(plan, fd.hip_reduce_fn(stack, w, na.MODE_W32_DIV64, float(n)), dev, gather=True,
                                 push=push)
         if red.pusher is not None and a.pusher_stream != "default":
@@ -126,9 +126,12 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gather", default="push", choices=["rccl", "push", "push_dma"])
     ap.add_argument("--stripes", type=int, default=4)
-    ap.add_argument("--order", default="host", choices=["host", "producer"],
-                    help="how each stripe's push follows its reduce (flearn_amd.dist._PUSH_ORDER)")
+    ap.add_argument("--order", default="auto", choices=["auto", "host", "producer"],
+                    help="how each stripe's push follows its reduce (flearn_amd.dist._PUSH_ORDER; auto: the "
+                         "product's — producer for the kernel push, host for the copy-engine push)")
     ap.add_argument("--clients", type=int, default=100)
+    ap.add_argument("--cols", type=int, default=0, help="columns of the stack (0: NS, 100 x ResNet-50; "
+                    "a multi-GPU rank's share, e.g. 3201280 for NS at G = 8)")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--analyze", default=None, help="a rocprofv3 kernel_trace.csv of a run")
     ap.add_argument("--pusher-stream", default="default", choices=["default", "normal", "high"],
